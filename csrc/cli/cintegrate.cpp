@@ -1,0 +1,99 @@
+// cintegrate — train distance from the interpolated velocity profile (reference:
+// cintegrate.cu, the active `cuda_test` path).
+//
+// Reference behaviour: 64 threads each interpolate 28 s of the
+// 1801-point profile at 1e4 samples/s into a 144 MB device array, re-read and sum it,
+// the host sums 64 partials; output (cintegrate.cu:140-141):
+//   %lf seconds
+//   final distance is:%lf
+// Here (default): the table is staged in LDS and the interpolation is summed on the fly by
+// the Riemann kernel with the Table integrand (h = 1e-4, left rule) over the full 1800 s —
+// nothing is materialised, every second is covered.
+//   --materialize        reference data flow: fill the 144 MB profile (coalesced), then an
+//                        HBM-bound vectorised sum pass
+//   --parity [--sp 32 --sm 2]  the reference's coverage: W=SP*SM workers of floor(1800/W) s
+//                        (121999.800663 at 32x2; the last 8 s are dropped, B5)
+//   --kernel sin         the disabled cuda_function path: sin on [0, pi], STEPS = 1e9
+//   --gpus G / torchrun  split the samples across GPUs, RCCL all-reduce
+#include <cmath>
+#include <cstdio>
+
+#include "cli_common.hpp"
+#include "miint/integrator.hpp"
+#include "miint/kernels.hpp"
+#include "miint/oracle.hpp"
+
+using namespace miint;
+
+int main(int argc, char** argv) {
+  try {
+    cli::Args a(argc, argv);
+    const cli::Topology topo = cli::topology(a);
+    const int sps = static_cast<int>(a.integer("steps-per-sec", oracle::kStepsPerSec));
+    double seconds = oracle::kProfileSeconds;
+    if (a.flag("parity")) {
+      const int w = static_cast<int>(a.integer("sp", 32) * a.integer("sm", 2));
+      seconds = (oracle::kProfileSeconds / w) * w;  // cintegrate.cu:81-82 coverage
+    }
+    const bool sin_kernel = a.str("kernel", "table") == "sin";
+    double result = 0.0, dev_ms = 0.0;
+    std::mutex mu;
+
+    if (a.flag("materialize") && !sin_kernel) {
+      cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
+        DeviceGuard g(dev);
+        const uint64_t total = static_cast<uint64_t>(seconds) * sps;
+        uint64_t b, c;
+        rank_slice(total, rank, topo.world, &b, &c);
+        const auto& tab = oracle::profile_table();
+        DeviceBuffer<double> dtab(tab.size()), prof(c + 2), out(1);
+        const int grid = default_reduce_grid(device_info(dev).num_cus);
+        DeviceBuffer<double> partials(static_cast<size_t>(grid));
+        PinnedBuffer<double> host(1);
+        Stream s;
+        MIINT_HIP(hipMemcpyAsync(dtab.get(), tab.data(), dtab.bytes(), hipMemcpyHostToDevice, s.get()));
+        Event e0, e1;
+        e0.record(s.get());
+        launch_interp_fill(dtab.get(), static_cast<int>(tab.size()), 1.0 / sps, b, c, prof.get(), s.get());
+        launch_sum_array(prof.get(), c, 1.0 / sps, partials.get(), grid, out.get(), s.get());
+        if (comm) comm->allreduce_sum(out.get(), out.get(), 1, s.get());
+        MIINT_HIP(hipMemcpyAsync(host.get(), out.get(), sizeof(double), hipMemcpyDeviceToHost, s.get()));
+        e1.record(s.get());
+        s.sync();
+        std::lock_guard<std::mutex> lk(mu);
+        if (rank == topo.rank0) { result = host[0]; dev_ms = Event::elapsed_ms(e0, e1); }
+      });
+    } else {
+      RiemannConfig cfg;
+      if (sin_kernel) {
+        cfg.integrand = Integrand::kSin;
+        cfg.a = 0.0;
+        cfg.b = 3.14159265358979323846;
+        cfg.n = static_cast<uint64_t>(a.num("n", 1e9));  // cintegrate.cu:20 STEPS
+      } else {
+        cfg.integrand = Integrand::kTable;
+        cfg.table = oracle::profile_table();
+        cfg.a = 0.0;
+        cfg.b = seconds;
+        cfg.n = static_cast<uint64_t>(seconds) * static_cast<uint64_t>(sps);
+      }
+      cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
+        RiemannPlan plan(cfg, dev, comm);
+        StepTiming t = plan.run_steps(1, false, false);
+        std::lock_guard<std::mutex> lk(mu);
+        if (rank == topo.rank0) { result = plan.host_result(0); dev_ms = t.device_ms; }
+      });
+    }
+    if (topo.rank0 != 0) return 0;
+    const double secs = wall_seconds() - process_start_seconds();
+    std::printf("%lf seconds\n", secs);
+    std::printf("final distance is:%lf\n", result);
+    if (a.flag("json"))
+      std::printf("{\"program\":\"cintegrate\",\"gpus\":%d,\"result\":%.17g,\"device_ms\":%.6f,"
+                  "\"seconds_wall\":%.6f}\n", topo.world, result, dev_ms, secs);
+    return 0;
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "cintegrate: %s\n", e.what());
+    return 1;
+  }
+}

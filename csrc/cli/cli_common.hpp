@@ -1,0 +1,145 @@
+// Shared plumbing for the miint command-line tools.
+//
+// The reference takes no arguments at all (every knob is a #define, SURVEY §5 "Config /
+// flags"); these tools default to the reference's configuration and expose the rest as
+// --flags. Launch topologies (replacing `mpirun -np P`):
+//   * one process driving G GPUs:      ./riemann --gpus 8          (ncclCommInitAll + threads)
+//   * one process per GPU via torchrun: torchrun --no-python --nproc-per-node 8 ./riemann
+//     (RANK/WORLD_SIZE/LOCAL_RANK from the env, RCCL unique id over a TCP rendezvous on
+//     MASTER_ADDR:MASTER_PORT+17)
+#pragma once
+
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "miint/comm.hpp"
+#include "miint/runtime.hpp"
+
+namespace miint {
+namespace cli {
+
+class Args {
+ public:
+  Args(int argc, char** argv) {
+    for (int i = 1; i < argc; ++i) {
+      std::string a = argv[i];
+      if (a.rfind("--", 0) != 0) { pos_.push_back(a); continue; }
+      a = a.substr(2);
+      const auto eq = a.find('=');
+      if (eq != std::string::npos) kv_[a.substr(0, eq)] = a.substr(eq + 1);
+      else if (i + 1 < argc && std::string(argv[i + 1]).rfind("--", 0) != 0) kv_[a] = argv[++i];
+      else kv_[a] = "1";
+    }
+  }
+  bool has(const std::string& k) const { return kv_.count(k) > 0; }
+  std::string str(const std::string& k, const std::string& d) const {
+    auto it = kv_.find(k);
+    return it == kv_.end() ? d : it->second;
+  }
+  double num(const std::string& k, double d) const {
+    auto it = kv_.find(k);
+    return it == kv_.end() ? d : std::strtod(it->second.c_str(), nullptr);
+  }
+  long long integer(const std::string& k, long long d) const {
+    auto it = kv_.find(k);
+    return it == kv_.end() ? d : static_cast<long long>(std::strtod(it->second.c_str(), nullptr));
+  }
+  bool flag(const std::string& k) const {
+    auto it = kv_.find(k);
+    return it != kv_.end() && it->second != "0" && it->second != "false";
+  }
+  const std::vector<std::string>& positional() const { return pos_; }
+
+ private:
+  std::map<std::string, std::string> kv_;
+  std::vector<std::string> pos_;
+};
+
+inline int env_int(const char* k, int d) {
+  const char* v = std::getenv(k);
+  return v ? std::atoi(v) : d;
+}
+
+struct Topology {
+  int world = 1;        // total ranks (GPUs)
+  int rank0 = 0;        // first rank handled by this process
+  int local = 1;        // ranks (threads) in this process
+  bool multiproc = false;
+};
+
+// Decide who runs what: torchrun env -> one rank per process; else --gpus threads.
+inline Topology topology(const Args& a) {
+  Topology t;
+  const int ws = env_int("WORLD_SIZE", 1);
+  if (ws > 1) {
+    t.world = ws;
+    t.rank0 = env_int("RANK", 0);
+    t.local = 1;
+    t.multiproc = true;
+  } else {
+    t.world = static_cast<int>(a.integer("gpus", 1));
+    if (t.world < 1) t.world = 1;
+    const int nd = device_count();
+    if (nd < t.world) fail("--gpus " + std::to_string(t.world) + " but only " +
+                           std::to_string(nd) + " HIP devices visible", __FILE__, __LINE__);
+    t.local = t.world;
+  }
+  return t;
+}
+
+// Run fn(rank, device, comm) for every rank this process owns (threads when > 1) and
+// rethrow the first failure. comm is null when world == 1.
+inline void run_ranks(const Topology& t,
+                      const std::function<void(int rank, int device, const Comm* comm)>& fn) {
+  std::vector<std::unique_ptr<Comm>> comms;
+  if (t.multiproc) {
+    const char* addr = std::getenv("MASTER_ADDR");
+    const int port = env_int("MASTER_PORT", 29500) + 17;
+    const std::string id = rendezvous_unique_id(addr ? addr : "127.0.0.1", port, t.rank0, t.world);
+    const int dev = env_int("LOCAL_RANK", 0);
+    comms.emplace_back(new Comm(id, t.rank0, t.world, dev));
+    fn(t.rank0, dev, comms[0].get());
+    return;
+  }
+  if (t.world == 1) {
+    fn(0, 0, nullptr);
+    return;
+  }
+  std::vector<int> devs(t.world);
+  for (int i = 0; i < t.world; ++i) devs[i] = i;
+  comms = Comm::init_all(devs);
+  std::vector<std::thread> th;
+  std::mutex mu;
+  std::string err;
+  for (int r = 0; r < t.world; ++r) {
+    th.emplace_back([&, r] {
+      try {
+        fn(r, r, comms[r].get());
+      } catch (const std::exception& e) {
+        std::lock_guard<std::mutex> g(mu);
+        if (err.empty()) err = "rank " + std::to_string(r) + ": " + e.what();
+      }
+    });
+  }
+  for (auto& x : th) x.join();
+  if (!err.empty()) throw Error(err);
+}
+
+inline std::string json_escape(const std::string& s) {
+  std::string o;
+  for (char c : s) {
+    if (c == '"' || c == '\\') o += '\\';
+    o += c;
+  }
+  return o;
+}
+
+}  // namespace cli
+}  // namespace miint

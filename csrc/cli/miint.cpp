@@ -1,0 +1,177 @@
+// miint — unified native driver: device info, benchmark sweeps, oracle self-checks.
+//
+//   ./miint info
+//   ./miint bench [--integrand pi4] [--n 1e9] [--dtype fp64] [--rule left] [--iters 200]
+//                 [--gpus G] [--div series|ieee] [--unfused] [--no-graph]      (JSON lines)
+//   ./miint sweep [--gpus G]     N in {1e6,1e9,1e10} x dtype {fp64,fp32} x integrand
+//   ./miint selfcheck            every SURVEY §6.1 oracle on the GPU, exit 1 on mismatch
+//
+// The reference has no benchmark harness (its only artefact is a wall-clock
+// "%lf seconds" line covering process start to print); this tool reports device time per
+// integration from hipEvents around graph replays, plus subintervals/s and |error|.
+#include <cmath>
+#include <cstdio>
+#include <string>
+#include <vector>
+
+#include "cli_common.hpp"
+#include "miint/integrator.hpp"
+#include "miint/oracle.hpp"
+#include "miint/trainscan.hpp"
+
+using namespace miint;
+
+namespace {
+
+struct BenchRow {
+  std::string integrand, dtype, rule;
+  double n = 0, result = 0, exact = 0, ms = 0;
+  int gpus = 1;
+};
+
+Integrand integrand_of(const std::string& s) {
+  if (s == "sin") return Integrand::kSin;
+  if (s == "poly") return Integrand::kPoly;
+  if (s == "train") return Integrand::kTrainVel;
+  if (s == "table") return Integrand::kTable;
+  return Integrand::kPi4;
+}
+
+RiemannConfig make_cfg(const std::string& integ, double n, const std::string& dtype,
+                       const std::string& rule, const std::string& div) {
+  RiemannConfig c;
+  c.integrand = integrand_of(integ);
+  c.a = 0.0;
+  c.b = c.integrand == Integrand::kPi4 || c.integrand == Integrand::kPoly ? 1.0
+      : c.integrand == Integrand::kSin ? 3.14159265358979323846 : 1800.0;
+  c.n = static_cast<uint64_t>(n);
+  c.dtype = dtype == "fp32" ? DType::kF32 : DType::kF64;
+  c.rule = rule == "mid" ? Rule::kMid : (rule == "right" ? Rule::kRight : Rule::kLeft);
+  c.div = div == "ieee" ? DivMode::kIeee : DivMode::kSeries;
+  if (c.integrand == Integrand::kTrainVel) { c.p0 = oracle::kTrainTs; c.p1 = oracle::kTrainVs; }
+  if (c.integrand == Integrand::kTable) c.table = oracle::profile_table();
+  if (c.integrand == Integrand::kPoly) c.coef = {0.3, -1.2, 0.7, 0.05, -0.4, 0.9, 0.1};
+  return c;
+}
+
+BenchRow bench_one(const cli::Topology& topo, RiemannConfig cfg, int iters, bool graphs) {
+  BenchRow row;
+  row.n = static_cast<double>(cfg.n);
+  row.gpus = topo.world;
+  row.exact = oracle::analytic(cfg.integrand, cfg.a, cfg.b, cfg.coef, cfg.p0, cfg.p1);
+  std::mutex mu;
+  cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
+    RiemannPlan plan(cfg, dev, comm);
+    plan.run_steps(3, comm != nullptr, graphs);  // warmup + capture
+    StepTiming t = plan.run_steps(iters, comm != nullptr, graphs);
+    std::lock_guard<std::mutex> g(mu);
+    const double ms = t.wall_s * 1e3 / iters;
+    if (ms > row.ms) row.ms = ms;  // slowest rank
+    if (rank == topo.rank0) row.result = plan.host_result(graphs ? (iters - 1) % cfg.slots : (iters - 1) % plan.host_capacity());
+  });
+  return row;
+}
+
+void print_row(const BenchRow& r, const char* integ, const char* dtype, const char* rule) {
+  std::printf("{\"integrand\":\"%s\",\"dtype\":\"%s\",\"rule\":\"%s\",\"n\":%.0f,\"gpus\":%d,"
+              "\"ms_per_integration\":%.6f,\"subintervals_per_s\":%.6e,\"result\":%.17g,"
+              "\"analytic\":%.17g,\"abs_err\":%.3e}\n",
+              integ, dtype, rule, r.n, r.gpus, r.ms, r.n / (r.ms * 1e-3), r.result, r.exact,
+              std::fabs(r.result - r.exact));
+  std::fflush(stdout);
+}
+
+int selfcheck() {
+  int bad = 0;
+  auto check = [&](const char* what, double got, double want, double tol) {
+    const bool ok = std::fabs(got - want) <= tol;
+    std::printf("%-44s got %.9f want %.9f  %s\n", what, got, want, ok ? "ok" : "MISMATCH");
+    bad += !ok;
+  };
+  {
+    RiemannPlan p(make_cfg("pi4", 1e9, "fp64", "left", "series"), 0);
+    check("pi4 left N=1e9 (|err| = h)", p.run(), 3.14159265358979323846 + 1e-9, 2e-12);
+  }
+  {
+    RiemannPlan p(make_cfg("pi4", 1e9, "fp64", "mid", "series"), 0);
+    check("pi4 mid N=1e9", p.run(), 3.14159265358979323846, 1e-13);
+  }
+  {
+    RiemannPlan p(make_cfg("sin", 1e9, "fp64", "left", "series"), 0);
+    check("sin [0,pi] N=1e9", p.run(), 2.0, 1e-12);
+  }
+  {
+    RiemannConfig c = make_cfg("table", 18e6, "fp64", "left", "series");
+    RiemannPlan p(c, 0);
+    check("cintegrate full coverage", p.run(), 122000.004030, 5e-6);
+    c.b = 1792.0;
+    c.n = 17920000;
+    RiemannPlan q(c, 0);
+    check("cintegrate --parity (SP=32,SM=2)", q.run(), 121999.800663, 5e-6);
+  }
+  {
+    TrainScanConfig tc;
+    TrainScan ts(tc, 0);
+    const TrainScanResult r = ts.run();
+    check("trainscan distance (P=1)", r.distance, 122000.004030, 5e-6);
+  }
+  std::printf("%s\n", bad ? "SELFCHECK FAILED" : "SELFCHECK OK");
+  return bad ? 1 : 0;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  try {
+    cli::Args a(argc, argv);
+    const std::string cmd = a.positional().empty() ? "info" : a.positional()[0];
+    if (cmd == "info") {
+      const int nd = device_count();
+      std::printf("miint: %d HIP device(s), RCCL %s\n", nd, nd ? Comm::version().c_str() : "-");
+      for (int d = 0; d < nd; ++d) {
+        const DeviceInfo i = device_info(d);
+        std::printf("  [%d] %s %s  %d CUs  %.1f GHz  %.1f GB  L2 %d KB\n", d, i.name.c_str(),
+                    i.arch.c_str(), i.num_cus, i.clock_khz / 1e6, i.total_mem / 1e9,
+                    i.l2_bytes / 1024);
+      }
+      return 0;
+    }
+    if (cmd == "selfcheck") return selfcheck();
+    const cli::Topology topo = cli::topology(a);
+    const int iters = static_cast<int>(a.integer("iters", 100));
+    const bool graphs = !a.flag("no-graph");
+    if (cmd == "bench") {
+      RiemannConfig c = make_cfg(a.str("integrand", "pi4"), a.num("n", 1e9), a.str("dtype", "fp64"),
+                                 a.str("rule", "left"), a.str("div", "series"));
+      c.fused = !a.flag("unfused");
+      c.grid = static_cast<int>(a.integer("grid", 0));
+      c.waves_per_cu = static_cast<int>(a.integer("waves-per-cu", 32));
+      const BenchRow r = bench_one(topo, c, iters, graphs);
+      if (topo.rank0 == 0)
+        print_row(r, a.str("integrand", "pi4").c_str(), a.str("dtype", "fp64").c_str(),
+                  a.str("rule", "left").c_str());
+      return 0;
+    }
+    if (cmd == "sweep") {
+      const std::vector<double> ns = {1e6, 1e9, 1e10};
+      const std::vector<std::string> integs = {"pi4", "sin", "poly", "train"};
+      for (const auto& integ : integs)
+        for (const char* dt : {"fp64", "fp32"}) {
+          if (std::string(dt) == "fp32" && integ != "pi4") continue;
+          for (double n : ns) {
+            if (integ != "pi4" && n > 1e9) continue;
+            RiemannConfig c = make_cfg(integ, n, dt, "left", "series");
+            const int it = n >= 1e10 ? 10 : (n >= 1e9 ? 50 : 500);
+            const BenchRow r = bench_one(topo, c, it, graphs);
+            if (topo.rank0 == 0) print_row(r, integ.c_str(), dt, "left");
+          }
+        }
+      return 0;
+    }
+    std::fprintf(stderr, "usage: miint info|bench|sweep|selfcheck [--flags]\n");
+    return 2;
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "miint: %s\n", e.what());
+    return 1;
+  }
+}

@@ -1,0 +1,118 @@
+// riemann — Riemann sum of sin(x) on [0, pi] (reference: riemann.cpp, MPI master/worker).
+//
+// Default output is the reference's two lines (riemann.cpp:92-96):
+//   %lf seconds
+//   The integral of f(x) from 0.0 to <b> with <n> steps is <sum>      (precision 15)
+// Differences by design: every GPU works (the reference's rank 0 only receives, so P
+// processes give P-1 workers and P=1 prints 0 — SURVEY B10); the partial sums meet in one
+// RCCL all-reduce instead of P-1 MPI_Send/Recv pairs; N is 64-bit (1e10 works, B9).
+// --parity reproduces the master/worker partition numerics (P-1 workers, (int)(N/W)
+// samples each, rank-order sum, P=1 -> 0) on the GPU.
+//
+//   ./riemann [--n 1e9] [--gpus G] [--integrand sin|pi4|poly|train] [--rule left|mid]
+//             [--dtype fp64|fp32] [--iters K] [--parity] [--json]
+#include <cmath>
+#include <cstdio>
+#include <iostream>
+#include <sstream>
+
+#include "cli_common.hpp"
+#include "miint/integrator.hpp"
+#include "miint/oracle.hpp"
+
+using namespace miint;
+
+namespace {
+
+Integrand parse_integrand(const std::string& s) {
+  if (s == "sin") return Integrand::kSin;
+  if (s == "pi4") return Integrand::kPi4;
+  if (s == "poly") return Integrand::kPoly;
+  if (s == "train") return Integrand::kTrainVel;
+  if (s == "table") return Integrand::kTable;
+  fail("unknown integrand " + s, __FILE__, __LINE__);
+}
+Rule parse_rule(const std::string& s) {
+  if (s == "left") return Rule::kLeft;
+  if (s == "mid") return Rule::kMid;
+  if (s == "right") return Rule::kRight;
+  fail("unknown rule " + s, __FILE__, __LINE__);
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  try {
+    cli::Args a(argc, argv);
+    const Integrand f = parse_integrand(a.str("integrand", "sin"));
+    const double pi = 3.14159265358979323846;
+    double lo = 0.0, hi = pi;  // riemann.cpp:6 RANGE = M_PI
+    if (f == Integrand::kPi4) hi = 1.0;
+    if (f == Integrand::kTrainVel || f == Integrand::kTable) hi = 1800.0;
+    lo = a.num("a", lo);
+    hi = a.num("b", hi);
+    const double nd = a.num("n", 1e9);  // riemann.cpp:10 STEPS
+    const auto n = static_cast<uint64_t>(nd);
+    const int iters = static_cast<int>(a.integer("iters", 1));
+    const cli::Topology topo = cli::topology(a);
+
+    RiemannConfig cfg;
+    cfg.integrand = f;
+    cfg.a = lo;
+    cfg.b = hi;
+    cfg.n = n;
+    cfg.rule = parse_rule(a.str("rule", "left"));
+    cfg.dtype = a.str("dtype", "fp64") == "fp32" ? DType::kF32 : DType::kF64;
+    cfg.div = a.str("div", "series") == "ieee" ? DivMode::kIeee : DivMode::kSeries;
+    cfg.fused = !a.flag("unfused");
+    if (f == Integrand::kTrainVel) { cfg.p0 = oracle::kTrainTs; cfg.p1 = oracle::kTrainVs; }
+    if (f == Integrand::kTable) cfg.table = oracle::profile_table();
+    if (f == Integrand::kPoly) cfg.coef = {1.0, -0.5, 0.25, 0.125};
+
+    double result = 0.0, dev_ms = 0.0;
+    if (a.flag("parity")) {
+      // riemann.cpp:65-86 numerics on the GPU: P = world ranks -> W = P-1 workers.
+      const int P = topo.world;
+      const int W = P - 1;
+      double g_sum = 0.0;
+      for (int w = 0; w < W; ++w) {
+        RiemannConfig c = cfg;
+        c.a = w * ((hi - lo) / W);
+        c.b = c.a + (hi - lo) / W;
+        c.n = static_cast<uint64_t>(static_cast<int>(nd / W));
+        RiemannPlan plan(c, w % device_count());
+        g_sum += plan.run();  // root receives in rank order
+      }
+      result = g_sum;
+    } else {
+      std::mutex mu;
+      cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
+        RiemannPlan plan(cfg, dev, comm);
+        StepTiming t = plan.run_steps(iters, comm != nullptr, iters > 1);
+        std::lock_guard<std::mutex> g(mu);
+        if (rank == topo.rank0) {
+          result = plan.host_result(iters > 1 ? (iters - 1) % cfg.slots : 0);
+          dev_ms = t.device_ms / iters;
+        }
+      });
+    }
+    if (topo.rank0 != 0) return 0;
+    const double secs = wall_seconds() - process_start_seconds();
+    std::printf("%lf seconds\n", secs);
+    std::cout.precision(15);
+    std::cout << "The integral of f(x) from 0.0 to " << hi << " with " << nd << " steps is "
+              << result << std::endl;
+    if (a.flag("json")) {
+      const double exact = oracle::analytic(f, lo, hi, cfg.coef, cfg.p0, cfg.p1);
+      std::printf("{\"program\":\"riemann\",\"n\":%.0f,\"gpus\":%d,\"result\":%.17g,"
+                  "\"analytic\":%.17g,\"abs_err\":%.3e,\"device_ms\":%.6f,"
+                  "\"subintervals_per_s\":%.6e,\"seconds_wall\":%.6f}\n",
+                  nd, topo.world, result, exact, std::fabs(result - exact), dev_ms,
+                  dev_ms > 0 ? nd / (dev_ms * 1e-3) : 0.0, secs);
+    }
+    return 0;
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "riemann: %s\n", e.what());
+    return 1;
+  }
+}

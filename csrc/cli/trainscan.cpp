@@ -1,0 +1,54 @@
+// trainscan — distributed two-phase prefix scan of the train profile (reference: 4main.c).
+//
+// Output (4main.c:73,239,241):
+//   Step size of 10000
+//   %lf seconds
+//   Total distance traveled = %lf
+// Per GPU: one fused interp+scan kernel (decoupled look-back) per phase; across GPUs an
+// allgather of one fp64 total per rank and an on-device carry add (no 144 MB gathers, no
+// serial carry loop on a root, no broadcast). --parity reproduces 4main's partitions and
+// printed element (P=7 -> 0.000000, P=16 -> 117642.707174). --replicate allgathers the full
+// table to every rank like 4main.c:157.
+//
+//   ./trainscan [--gpus G] [--parity] [--replicate] [--no-phase2] [--json]
+#include <cstdio>
+
+#include "cli_common.hpp"
+#include "miint/oracle.hpp"
+#include "miint/trainscan.hpp"
+
+using namespace miint;
+
+int main(int argc, char** argv) {
+  try {
+    cli::Args a(argc, argv);
+    const cli::Topology topo = cli::topology(a);
+    TrainScanConfig cfg;
+    cfg.steps_per_sec = static_cast<int>(a.integer("steps-per-sec", oracle::kStepsPerSec));
+    cfg.parity = a.flag("parity");
+    cfg.replicate = a.flag("replicate");
+    cfg.phase2 = !a.flag("no-phase2");
+    if (topo.rank0 == 0)  // 4main.c:72-74 (tablelen/1800)
+      std::printf("Step size of %ld\n", static_cast<long>(cfg.steps_per_sec));
+    TrainScanResult res;
+    std::mutex mu;
+    cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
+      TrainScan ts(cfg, dev, comm);
+      TrainScanResult r = ts.run();
+      std::lock_guard<std::mutex> lk(mu);
+      if (rank == topo.rank0) res = r;
+    });
+    if (topo.rank0 != 0) return 0;
+    const double secs = wall_seconds() - process_start_seconds();
+    std::printf("%lf seconds\n", secs);
+    std::printf("Total distance traveled = %lf\n", res.distance);
+    if (a.flag("json"))
+      std::printf("{\"program\":\"trainscan\",\"gpus\":%d,\"distance\":%.17g,\"sum_of_sums\":%.17g,"
+                  "\"device_ms\":%.6f,\"timeout\":%u,\"seconds_wall\":%.6f}\n",
+                  topo.world, res.distance, res.sum_of_sums, res.device_ms, res.timeout, secs);
+    return res.timeout ? 3 : 0;
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "trainscan: %s\n", e.what());
+    return 1;
+  }
+}

@@ -1,0 +1,127 @@
+// Integration plans: the user-facing native API.
+//
+// A RiemannPlan owns everything one rank needs to integrate f over [a, b] with n samples:
+// its 64-bit slice of the sample range, the kernel launch shape, device workspace, a ring
+// of result slots, pinned host results, and (optionally) an RCCL communicator for the
+// cross-GPU sum. Work is split in three stream-ordered stages so a driver can pipeline
+// them on separate HIP streams or capture them into a hipGraph:
+//
+//   compute  : Riemann kernel(s) -> this rank's scaled partial in slot k (device)
+//   reduce   : RCCL allreduce of slot k across ranks (xGMI)          [skipped if world==1]
+//   copyout  : 8-byte hipMemcpyAsync of slot k into pinned host memory
+//
+// Reference mapping: riemann.cpp:47-101 (MPI master/worker) and cintegrate.cu:101-150
+// (CUDA host driver) are both instances of this plan (see csrc/cli/).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <memory>
+#include <vector>
+
+#include "miint/comm.hpp"
+#include "miint/common.hpp"
+#include "miint/kernels.hpp"
+#include "miint/runtime.hpp"
+
+namespace miint {
+
+struct RiemannConfig {
+  Integrand integrand = Integrand::kPi4;
+  double a = 0.0, b = 1.0;
+  uint64_t n = 1000000000ull;  // total samples over all ranks
+  Rule rule = Rule::kLeft;
+  DType dtype = DType::kF64;
+  DivMode div = DivMode::kSeries;
+  std::vector<double> coef;    // Integrand::kPoly
+  double p0 = 0.0, p1 = 0.0;   // Integrand::kTrainVel (ts, vs)
+  std::vector<double> table;   // Integrand::kTable (host copy, uploaded once)
+  int grid = 0;                // workgroups; 0 = auto (waves_per_cu per CU)
+  int waves_per_cu = 32;
+  bool fused = true;           // one launch (ticket reduction) vs partials + finalize
+  int slots = 4;               // result ring depth for pipelined steps
+  int rank = 0, world = 1;     // slice of [0, n) when no communicator is given (e.g. the
+                               // torch.distributed path reduces results itself)
+};
+
+// Balanced 64-bit slice of [0, n) for rank r of w: first (n % w) ranks get one extra.
+inline void rank_slice(uint64_t n, int r, int w, uint64_t* begin, uint64_t* count) {
+  const uint64_t q = n / static_cast<uint64_t>(w), rem = n % static_cast<uint64_t>(w);
+  const uint64_t ur = static_cast<uint64_t>(r);
+  *count = q + (ur < rem ? 1 : 0);
+  *begin = ur * q + (ur < rem ? ur : rem);
+}
+
+struct StepTiming {
+  double wall_s = 0.0;    // host wall clock around the whole run
+  double device_ms = 0.0; // hipEvent time on the compute stream
+  int steps = 0;
+};
+
+class RiemannPlan {
+ public:
+  RiemannPlan(const RiemannConfig& cfg, int device, const Comm* comm = nullptr);
+  ~RiemannPlan();
+  RiemannPlan(const RiemannPlan&) = delete;
+  RiemannPlan& operator=(const RiemannPlan&) = delete;
+
+  const RiemannConfig& config() const { return cfg_; }
+  int device() const { return device_; }
+  int rank() const { return rank_; }
+  int world() const { return world_; }
+  uint64_t begin() const { return params_.i_begin; }
+  uint64_t count() const { return params_.n; }
+  double h() const { return params_.h; }
+  double scale() const { return scale_; }
+  LaunchShape shape() const { return shape_; }
+  DivMode effective_div() const;
+
+  void enqueue_compute(hipStream_t s, int slot) const;
+  void enqueue_reduce(hipStream_t s, int slot) const;
+  void enqueue_copyout(hipStream_t s, int slot, int host_index) const;
+  void enqueue(hipStream_t s, int slot, int host_index) const;
+
+  double* device_result(int slot) const { return result_.get() + slot; }
+  double host_result(int host_index) const { return host_[host_index]; }
+  int host_capacity() const { return static_cast<int>(host_.size()); }
+
+  // One synchronous integration on the plan's own stream; returns the global value.
+  double run();
+  // Capture compute(+reduce+copyout) for every slot into hipGraphs.
+  void capture_graphs();
+  bool graphs_ready() const { return !graphs_.empty(); }
+
+  // Run `steps` complete integrations back to back. With pipeline=true (and world > 1)
+  // step k's allreduce+copyout runs on the comm stream while step k+1 computes; with
+  // graphs=true each stage is a graph replay. Returns when every result is on the host.
+  StepTiming run_steps(int steps, bool pipeline, bool graphs);
+  // The same without the final synchronisation (bench.py brackets it with its own
+  // barrier + device synchronize); call sync() before reading host results.
+  void launch_steps(int steps, bool pipeline, bool graphs);
+  void sync() const;
+  hipStream_t compute_stream() const { return compute_.get(); }
+  hipStream_t comm_stream() const { return comm_stream_.get(); }
+
+ private:
+  RiemannConfig cfg_;
+  int device_;
+  const Comm* comm_;
+  int rank_ = 0, world_ = 1;
+  RiemannParams params_{};
+  double scale_ = 1.0;
+  LaunchShape shape_{1, kRiemannBlock};
+  DeviceBuffer<double> partials_;
+  DeviceBuffer<double> result_;
+  DeviceBuffer<unsigned int> ticket_;
+  DeviceBuffer<double> table_;
+  PinnedBuffer<double> host_;
+  Stream compute_;
+  Stream comm_stream_;
+  std::vector<std::unique_ptr<Event>> ev_computed_, ev_drained_;
+  Event ev_t0_, ev_t1_;
+  std::vector<std::unique_ptr<Graph>> graphs_;       // compute graph per slot
+  std::vector<std::unique_ptr<Graph>> comm_graphs_;  // reduce+copyout graph per slot
+};
+
+}  // namespace miint

@@ -1,0 +1,108 @@
+// Host-side launch API for every miint HIP kernel (gfx950 only).
+//
+// All launchers are asynchronous on the given stream, allocate nothing and never
+// synchronise, so they can be captured into a hipGraph (cdna_hip_programming.md §6 G9).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstddef>
+#include <cstdint>
+
+#include "miint/common.hpp"
+
+namespace miint {
+
+enum class DType : int { kF64 = 0, kF32 = 1 };
+
+// Tile (unroll) size of the Riemann kernels: U consecutive samples per lane per step.
+constexpr int kRiemannTile = 32;
+constexpr int kRiemannBlock = 256;
+
+// True when the fp64 Pi4 series reciprocal is exact to fp64 for this h (see integrands.hpp).
+inline bool series_ok(double h) { return 0.5 * kRiemannTile * (h < 0 ? -h : h) <= 2e-6; }
+
+struct LaunchShape {
+  int grid;   // workgroups
+  int block;  // threads per workgroup
+};
+
+// Default grid: enough workgroups to hold `waves_per_cu` waves on every CU.
+LaunchShape default_riemann_shape(int num_cus, int waves_per_cu = 32);
+
+// Riemann partial sums: writes one fp64 partial per workgroup into partials[0..grid).
+// Partials are *unscaled* sums of f; multiply by h * integrand scale at finalize.
+// `table` (device, `table_n` doubles) is used only for Integrand::kTable.
+void launch_riemann_partials(const RiemannParams& p, DType dtype, DivMode div,
+                             LaunchShape shape, const double* table, int table_n,
+                             double* partials, hipStream_t stream);
+
+// out[0] = scale * sum(partials[0..n)) in a fixed order (bitwise reproducible).
+void launch_finalize(const double* partials, int n, double scale, double* out,
+                     hipStream_t stream);
+
+// One-launch variant: partials + last-workgroup ticket reduction (agent-scope hand-off,
+// cdna_hip_programming.md §6 G16). `ticket` must be zero before the first launch; the
+// last workgroup re-arms it.
+void launch_riemann_fused(const RiemannParams& p, DType dtype, DivMode div, LaunchShape shape,
+                          const double* table, int table_n, double* partials,
+                          unsigned int* ticket, double scale, double* out, hipStream_t stream);
+
+// Debug/validation: write every sample's f value (as the hot tile path computes it) to
+// `out[0..p.n)`; fp64 only. Used by the per-point accuracy tests of the series division.
+void launch_riemann_point_values(const RiemannParams& p, DivMode div, const double* table,
+                                 int table_n, double* out, hipStream_t stream);
+
+// Integrand scale factor (4 for Pi4, 1 otherwise).
+double integrand_scale(Integrand f);
+
+// ---------------------------------------------------------------- reductions / tables
+// out[0] = scale * sum(x[0..n)) — vectorised HBM-bound two-pass sum (fixed order).
+// `partials` needs default_reduce_grid() doubles.
+int default_reduce_grid(int num_cus);
+void launch_sum_array(const double* x, uint64_t n, double scale, double* partials, int grid,
+                      double* out, hipStream_t stream);
+
+// Materialise the interpolated profile: y[i] = interp(table, (i0 + i) * dt) for i < n.
+// (cintegrate.cu:88-92 / 4main.c:82-86 fill loop, coalesced and LDS-staged here.)
+void launch_interp_fill(const double* table, int table_n, double dt, uint64_t i0, uint64_t n,
+                        double* y, hipStream_t stream);
+
+// ---------------------------------------------------------------- scan (scan.hip)
+// Single-pass decoupled look-back inclusive scan of fp64 (replaces 4main.c:95-221's
+// gather-to-root + serial carry + broadcast). `state` needs scan_state_bytes(n) bytes and
+// is re-initialised by the launcher on the stream every call. out may alias in.
+// If `carry_in` is non-null its device value is added to every output (multi-GPU carry).
+size_t scan_state_bytes(uint64_t n);
+void launch_inclusive_scan(const double* in, double* out, uint64_t n, void* state,
+                           const double* carry_in, hipStream_t stream);
+// Fused: y = inclusive_scan(interp(table, (i0+i)*dt)) without materialising the fill.
+void launch_interp_scan(const double* table, int table_n, double dt, uint64_t i0, uint64_t n,
+                        double* out, void* state, const double* carry_in, hipStream_t stream);
+// Same, but samples whose global index i0+g lies outside [win_lo, win_hi) contribute 0:
+// emulates 4main.c's per-rank private fill windows (4main.c:76-86) for --parity runs.
+void launch_interp_scan_window(const double* table, int table_n, double dt, uint64_t i0,
+                               uint64_t n, uint64_t win_lo, uint64_t win_hi, double* out,
+                               void* state, const double* carry_in, hipStream_t stream);
+// Reads back the scan's spin-timeout word (non-zero = a look-back gave up; never expected).
+unsigned scan_timeout_flag(const void* state, hipStream_t stream);
+// x[i] += carry[0] for i < n (fix-up after a multi-GPU carry exchange).
+void launch_add_carry(double* x, uint64_t n, const double* carry, hipStream_t stream);
+
+// ---------------------------------------------------------------- 2-D table (table2d.hip)
+// Integrate the bilinear interpolant of a row-major ny x nx fp64 table spanning
+// [0, X] x [0, Y] with a midpoint rule on gx x gy points, rows [row0, row1) of the sample
+// grid only (multi-GPU row split). Writes one partial per workgroup.
+struct Table2DParams {
+  const double* table;
+  int nx, ny;        // table dims (entries)
+  double X, Y;       // physical extents
+  int gx, gy;        // sample grid
+  int row0, row1;    // sample rows owned by this launch
+};
+int table2d_grid(const Table2DParams& p);
+void launch_table2d_partials(const Table2DParams& p, double* partials, hipStream_t stream);
+void launch_outer_product(const double* v, int n, double* table, hipStream_t stream);
+
+}  // namespace miint

@@ -1,0 +1,361 @@
+// Riemann-sum kernels for gfx950 (MI355X / CDNA4).
+//
+// Reference behaviour being replaced:
+//   cuda_function  cintegrate.cu:47-72  — 64 fat threads, 15.6 M sequential sin() each,
+//                                         partials summed on the host.
+//   riemann_sum    riemann.cpp:29-44    — serial host loop, int counter (overflows >2^31).
+//
+// Design (MI355X-first):
+//   * Work unit = a tile of U=32 consecutive samples owned by one lane. Tiles are dealt
+//     grid-stride over 64-bit indices, so N = 1e10+ is fine (fixes SURVEY B9) and every
+//     launch fills all 256 CUs x 8 waves/SIMD regardless of N.
+//   * Sample coordinates are formed from the integer index every tile
+//     (x0 = fma(i0 + off, h, a), then fma(u, h, x0)) — no running x += h drift.
+//   * Per-lane fp64 accumulation over ~60 tiles, then wave64 DPP reduction, LDS across the
+//     4 waves of the workgroup, one partial per workgroup, and a fixed-order finalize
+//     (two-kernel) or last-workgroup ticket (one kernel). No float atomics anywhere:
+//     results are bitwise reproducible run to run.
+//   * fp32 path: packed float2 math (v_pk_fma_f32), tile coordinates from an fp64 base.
+#include <hip/hip_runtime.h>
+
+#include "miint/common.hpp"
+#include "miint/integrands.hpp"
+#include "miint/kernels.hpp"
+#include "miint/wave_reduce.hpp"
+
+namespace miint {
+namespace {
+
+constexpr int U = kRiemannTile;
+constexpr int B = kRiemannBlock;
+
+// Accumulate f over this launch's samples [p.i_begin, p.i_begin + p.n) into a per-lane sum.
+// The tile's first index is carried as an exact double (integers < 2^53 are exact), so the
+// loop pays one v_add_f64 per tile instead of a u64->f64 conversion.
+template <DivMode M, class F>
+__device__ __forceinline__ double lane_sum(const RiemannParams& p, const F& f) {
+  const uint64_t lanes = static_cast<uint64_t>(gridDim.x) * B;
+  const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * B + threadIdx.x;
+  const uint64_t ntile = p.n / U;
+  const double base = static_cast<double>(p.i_begin) + p.off;
+  const double istep = static_cast<double>(lanes * U);
+  double ib = base + static_cast<double>(gid * U);
+  double acc = 0.0;
+  for (uint64_t t = gid; t < ntile; t += lanes, ib += istep)
+    acc += f.template tile<U, M>(fma(ib, p.h, p.a), p.h);
+  const uint64_t done = ntile * U;
+  if (gid < p.n - done) acc += f.point(fma(base + static_cast<double>(done + gid), p.h, p.a));
+  return acc;
+}
+
+constexpr int kMaxTable = 2048;  // LDS budget for a 1-D table: 16 KB
+
+// ---------------------------------------------------------------------------- fp32 functor
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) {
+  return __builtin_elementwise_fma(a, b, c);
+}
+
+// 4/(1+x^2) in packed fp32 (v_pk_fma_f32 pairs). Tile base comes in as fp64 so sample
+// coordinates do not collapse at 1e9 samples; in-tile offsets and all
+// per-point math are fp32. Series division as in Pi4 (first order suffices: e^2 < 2^-24).
+struct Pi4F32 {
+  static constexpr double kScale = 4.0;
+  __device__ __forceinline__ double point(double xd) const {
+    const float x = static_cast<float>(xd);
+    return static_cast<double>(1.0f / fmaf(x, x, 1.0f));
+  }
+  template <int UU, DivMode M>
+  __device__ __forceinline__ double tile(double x0d, double h) const {
+    const float x0 = static_cast<float>(x0d);
+    const float hf = static_cast<float>(h);
+    const f32x2 xb = {x0, x0};
+    const f32x2 hh = {hf, hf};
+    const f32x2 one = {1.0f, 1.0f};
+    if constexpr (M == DivMode::kIeee) {
+      f32x2 acc = {0.0f, 0.0f};
+#pragma unroll
+      for (int u = 0; u < UU; u += 2) {
+        const f32x2 uu = {static_cast<float>(u), static_cast<float>(u + 1)};
+        const f32x2 x = pk_fma(uu, hh, xb);
+        acc += one / pk_fma(x, x, one);
+      }
+      return static_cast<double>(acc.x) + static_cast<double>(acc.y);
+    } else {
+      const float xm = fmaf(0.5f * (UU - 1), hf, x0);
+      const float dm = fmaf(xm, xm, 1.0f);
+      float s = __builtin_amdgcn_rcpf(dm);
+      s = fmaf(s, fmaf(-dm, s, 1.0f), s);
+      const f32x2 ns = {-s, -s};
+      f32x2 t = {0.0f, 0.0f};
+#pragma unroll
+      for (int u = 0; u < UU; u += 2) {
+        const f32x2 uu = {static_cast<float>(u), static_cast<float>(u + 1)};
+        const f32x2 x = pk_fma(uu, hh, xb);
+        t += pk_fma(pk_fma(x, x, one), ns, one);  // e = 1 - d*s
+      }
+      const double sd = static_cast<double>(s);
+      return sd * (static_cast<double>(UU) + (static_cast<double>(t.x) + static_cast<double>(t.y)));
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------- functor makers
+// Each integrand gets its own kernel instantiation (own register allocation); only the
+// table integrand reserves LDS.
+template <class F> struct Maker;
+template <> struct Maker<Pi4> {
+  static constexpr int kLds = 1;
+  __device__ static Pi4 make(const RiemannParams&, const double*, int, double*) { return {}; }
+};
+template <> struct Maker<Pi4F32> {
+  static constexpr int kLds = 1;
+  __device__ static Pi4F32 make(const RiemannParams&, const double*, int, double*) { return {}; }
+};
+template <> struct Maker<Sin> {
+  static constexpr int kLds = 1;
+  __device__ static Sin make(const RiemannParams&, const double*, int, double*) { return {}; }
+};
+template <> struct Maker<Poly> {
+  static constexpr int kLds = 1;
+  __device__ static Poly make(const RiemannParams& p, const double*, int, double*) {
+    return {p.coef, p.ncoef};
+  }
+};
+template <> struct Maker<TrainVel> {
+  static constexpr int kLds = 1;
+  __device__ static TrainVel make(const RiemannParams& p, const double*, int, double*) {
+    return {1.0 / p.p0, p.p1};
+  }
+};
+template <> struct Maker<Table> {
+  static constexpr int kLds = kMaxTable;
+  __device__ static Table make(const RiemannParams&, const double* table, int n, double* lds) {
+    for (int i = threadIdx.x; i < n; i += B) lds[i] = table[i];  // 14.4 KB, once per block
+    __syncthreads();
+    return {lds, n - 1};
+  }
+};
+
+// Partials kernel: one fp64 partial per workgroup.
+template <DivMode M, class F>
+__global__ __launch_bounds__(B) void riemann_kernel(RiemannParams p, const double* table,
+                                                    int table_n, double* partials) {
+  __shared__ double red[B / kWave];
+  __shared__ double lds[Maker<F>::kLds];
+  const F f = Maker<F>::make(p, table, table_n, lds);
+  const double s = block_sum<B>(lane_sum<M>(p, f), red);
+  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
+
+// ---------------------------------------------------------------------------- finalize
+constexpr int kFinalBlock = 1024;
+
+__device__ __forceinline__ double ordered_sum(const double* partials, int n, double* red) {
+  double v = 0.0;
+  for (int i = threadIdx.x; i < n; i += kFinalBlock) v += partials[i];
+  return block_sum<kFinalBlock>(v, red);
+}
+
+__global__ __launch_bounds__(kFinalBlock) void finalize_kernel(const double* partials, int n,
+                                                               double scale, double* out) {
+  __shared__ double red[kFinalBlock / kWave];
+  const double s = ordered_sum(partials, n, red);
+  if (threadIdx.x == 0) out[0] = s * scale;
+}
+
+// ---------------------------------------------------------------------------- fused (ticket)
+// Every workgroup publishes its partial with an agent-scope (sc1, write-through) store,
+// drains it (s_waitcnt vmcnt(0)), then takes a ticket with an agent-scope atomic. The
+// workgroup that draws the last ticket acquires (buffer_inv sc1) and reduces all partials
+// in index order with sc1 loads — the R1 hand-off of cdna_hip_programming.md §6 G16.
+// Placement-independent: correctness never depends on which XCD a block lands on, and the
+// index-ordered final sum keeps the result bitwise identical to the two-kernel path.
+template <DivMode M, class F>
+__global__ __launch_bounds__(B) void riemann_fused_kernel(RiemannParams p, const double* table,
+                                                          int table_n, double* partials,
+                                                          unsigned int* ticket, double scale,
+                                                          double* out) {
+  __shared__ double red[B / kWave];
+  __shared__ double lds[Maker<F>::kLds];
+  __shared__ int is_last;
+  const F f = Maker<F>::make(p, table, table_n, lds);
+  const double s = block_sum<B>(lane_sum<M>(p, f), red);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(&partials[blockIdx.x], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev =
+        __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    is_last = (prev == gridDim.x - 1);
+  }
+  __syncthreads();
+  if (!is_last) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  double v = 0.0;
+  for (int i = threadIdx.x; i < static_cast<int>(gridDim.x); i += B)
+    v += __hip_atomic_load(&partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const double tot = block_sum<B>(v, red + 0);
+  if (threadIdx.x == 0) {
+    out[0] = tot * scale;
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+  }
+}
+
+// ---------------------------------------------------------------------------- validation
+// Writes every sample's f value exactly as the hot tile path evaluates it (one lane per
+// tile), so tests can compare the series division point by point against IEEE division.
+template <DivMode M, class F>
+__global__ __launch_bounds__(B) void point_values_kernel(RiemannParams p, const double* table,
+                                                         int table_n, double* out) {
+  __shared__ double lds[Maker<F>::kLds];
+  const F f = Maker<F>::make(p, table, table_n, lds);
+  const uint64_t t = static_cast<uint64_t>(blockIdx.x) * B + threadIdx.x;
+  if (t * U >= p.n) return;
+  const double x0 = fma(static_cast<double>(p.i_begin) + p.off + static_cast<double>(t * U),
+                        p.h, p.a);
+  const double xm = fma(0.5 * (U - 1), p.h, x0);
+  for (int u = 0; u < U && t * U + u < p.n; ++u) {
+    const double x = fma(static_cast<double>(u), p.h, x0);
+    double v;
+    if constexpr (M == DivMode::kSeries && sizeof(F) == sizeof(Pi4) &&
+                  __is_same(F, Pi4)) {
+      const double dm = fma(xm, xm, 1.0);
+      double s = __builtin_amdgcn_rcp(dm);
+      s = fma(s, fma(-dm, s, 1.0), s);
+      const double e = fma(-fma(x, x, 1.0), s, 1.0);
+      v = fma(s, e + e * e, s);
+    } else {
+      v = f.point(x);
+    }
+    out[t * U + u] = v * F::kScale;
+  }
+}
+
+template <DivMode M, class F>
+void launch_partials_t(const RiemannParams& p, LaunchShape shape, const double* table,
+                       int table_n, double* partials, hipStream_t stream) {
+  riemann_kernel<M, F><<<shape.grid, B, 0, stream>>>(p, table, table_n, partials);
+}
+template <DivMode M, class F>
+void launch_fused_t(const RiemannParams& p, LaunchShape shape, const double* table, int table_n,
+                    double* partials, unsigned* ticket, double scale, double* out,
+                    hipStream_t stream) {
+  riemann_fused_kernel<M, F>
+      <<<shape.grid, B, 0, stream>>>(p, table, table_n, partials, ticket, scale, out);
+}
+
+// Dispatch (integrand, dtype, division mode) to a template instantiation. Transcendental
+// integrands (sin/cos) and the table ignore the division mode (no division in them).
+template <template <DivMode, class> class Op, class... A>
+void dispatch(const RiemannParams& p, DType dtype, DivMode m, A&&... a) {
+  const Integrand f = static_cast<Integrand>(p.integrand);
+  if (dtype == DType::kF32) {
+    MIINT_CHECK(f == Integrand::kPi4, "fp32 path is implemented for the pi4 integrand");
+    if (m == DivMode::kSeries) Op<DivMode::kSeries, Pi4F32>::run(a...);
+    else Op<DivMode::kIeee, Pi4F32>::run(a...);
+    return;
+  }
+  switch (f) {
+    case Integrand::kPi4:
+      if (m == DivMode::kSeries) Op<DivMode::kSeries, Pi4>::run(a...);
+      else Op<DivMode::kIeee, Pi4>::run(a...);
+      return;
+    case Integrand::kSin: Op<DivMode::kIeee, Sin>::run(a...); return;
+    case Integrand::kPoly: Op<DivMode::kIeee, Poly>::run(a...); return;
+    case Integrand::kTrainVel: Op<DivMode::kIeee, TrainVel>::run(a...); return;
+    case Integrand::kTable: Op<DivMode::kIeee, Table>::run(a...); return;
+  }
+  fail("unknown integrand", __FILE__, __LINE__);
+}
+
+template <DivMode M, class F> struct PartialsOp {
+  template <class... A> static void run(A... a) { launch_partials_t<M, F>(a...); }
+};
+template <DivMode M, class F> struct FusedOp {
+  template <class... A> static void run(A... a) { launch_fused_t<M, F>(a...); }
+};
+template <DivMode M, class F> struct PointsOp {
+  static void run(const RiemannParams& p, const double* table, int table_n, double* out,
+                  hipStream_t stream) {
+    const uint64_t ntile = (p.n + U - 1) / U;
+    const int grid = static_cast<int>((ntile + B - 1) / B);
+    point_values_kernel<M, F><<<grid, B, 0, stream>>>(p, table, table_n, out);
+  }
+};
+
+}  // namespace
+
+// ============================================================================ host side
+LaunchShape default_riemann_shape(int num_cus, int waves_per_cu) {
+  const int waves_per_block = B / kWave;
+  int blocks = (num_cus * waves_per_cu) / waves_per_block;
+  if (blocks < 1) blocks = 1;
+  return {blocks, B};
+}
+
+double integrand_scale(Integrand f) { return f == Integrand::kPi4 ? Pi4::kScale : 1.0; }
+
+static void check_shape(LaunchShape s) {
+  MIINT_CHECK(s.block == B, "riemann kernels are compiled for 256-thread workgroups");
+  MIINT_CHECK(s.grid >= 1 && s.grid <= (1 << 20), "grid out of range");
+}
+
+static void check_params(const RiemannParams& p, const double* table, int table_n) {
+  const int f = p.integrand;
+  MIINT_CHECK(f >= 0 && f <= static_cast<int>(Integrand::kTable), "unknown integrand");
+  if (static_cast<Integrand>(f) == Integrand::kTable) {
+    MIINT_CHECK(table != nullptr, "table integrand needs a device table");
+    MIINT_CHECK(table_n >= 2 && table_n <= kMaxTable, "table size must be in [2, 2048]");
+  }
+  if (static_cast<Integrand>(f) == Integrand::kPoly)
+    MIINT_CHECK(p.ncoef >= 1 && p.ncoef <= kMaxPolyCoeffs, "poly needs 1..16 coefficients");
+  if (static_cast<Integrand>(f) == Integrand::kTrainVel)
+    MIINT_CHECK(p.p0 != 0.0, "train integrand needs ts != 0");
+  MIINT_CHECK(p.i_begin + p.n < (uint64_t(1) << 52), "sample index must stay below 2^52");
+}
+
+static DivMode effective_div(const RiemannParams& p, DivMode div) {
+  return (div == DivMode::kSeries && !series_ok(p.h)) ? DivMode::kIeee : div;
+}
+
+void launch_riemann_partials(const RiemannParams& p, DType dtype, DivMode div, LaunchShape shape,
+                             const double* table, int table_n, double* partials,
+                             hipStream_t stream) {
+  check_shape(shape);
+  check_params(p, table, table_n);
+  dispatch<PartialsOp>(p, dtype, effective_div(p, div), p, shape, table, table_n, partials,
+                       stream);
+  MIINT_HIP(hipGetLastError());
+}
+
+void launch_finalize(const double* partials, int n, double scale, double* out,
+                     hipStream_t stream) {
+  MIINT_CHECK(n >= 1, "finalize needs at least one partial");
+  finalize_kernel<<<1, kFinalBlock, 0, stream>>>(partials, n, scale, out);
+  MIINT_HIP(hipGetLastError());
+}
+
+void launch_riemann_fused(const RiemannParams& p, DType dtype, DivMode div, LaunchShape shape,
+                          const double* table, int table_n, double* partials,
+                          unsigned int* ticket, double scale, double* out, hipStream_t stream) {
+  check_shape(shape);
+  check_params(p, table, table_n);
+  dispatch<FusedOp>(p, dtype, effective_div(p, div), p, shape, table, table_n, partials, ticket,
+                    scale, out, stream);
+  MIINT_HIP(hipGetLastError());
+}
+
+void launch_riemann_point_values(const RiemannParams& p, DivMode div, const double* table,
+                                 int table_n, double* out, hipStream_t stream) {
+  check_params(p, table, table_n);
+  MIINT_CHECK(p.n >= 1, "empty range");
+  dispatch<PointsOp>(p, DType::kF64, effective_div(p, div), p, table, table_n, out, stream);
+  MIINT_HIP(hipGetLastError());
+}
+
+}  // namespace miint

@@ -1,0 +1,302 @@
+// pybind11 bindings: the native miint runtime + kernels as `cuda_v_mpi_amd._miint`.
+//
+// Device memory crosses the boundary as integer addresses (torch.Tensor.data_ptr()) and
+// streams as integer handles (torch.cuda.Stream.cuda_stream), so the module has no libtorch
+// ABI dependency and no hipify step; it links only libamdhip64 and librccl.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstdint>
+#include <string>
+
+#include "miint/comm.hpp"
+#include "miint/integrator.hpp"
+#include "miint/kernels.hpp"
+#include "miint/oracle.hpp"
+#include "miint/runtime.hpp"
+#include "miint/selftest.hpp"
+#include "miint/trainscan.hpp"
+
+namespace py = pybind11;
+using namespace miint;
+
+namespace {
+
+template <typename T>
+T* ptr(uintptr_t p) { return reinterpret_cast<T*>(p); }
+hipStream_t stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+RiemannParams make_params(int integrand, double a, double h, double off, uint64_t i_begin,
+                          uint64_t n, const std::vector<double>& coef, double p0, double p1) {
+  RiemannParams p{};
+  p.a = a;
+  p.h = h;
+  p.off = off;
+  p.i_begin = i_begin;
+  p.n = n;
+  p.integrand = integrand;
+  MIINT_CHECK(coef.size() <= static_cast<size_t>(kMaxPolyCoeffs), "too many coefficients");
+  p.ncoef = static_cast<int>(coef.size());
+  for (size_t i = 0; i < coef.size(); ++i) p.coef[i] = coef[i];
+  p.p0 = p0;
+  p.p1 = p1;
+  return p;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_miint, m) {
+  m.doc() = "miint: MI355X-native numerical integration (HIP/gfx950 kernels, RCCL, hipGraph)";
+  py::register_exception<miint::Error>(m, "MiintError", PyExc_RuntimeError);
+
+  // ------------------------------------------------------------------ enums
+  py::enum_<Integrand>(m, "Integrand")
+      .value("pi4", Integrand::kPi4)
+      .value("sin", Integrand::kSin)
+      .value("poly", Integrand::kPoly)
+      .value("train", Integrand::kTrainVel)
+      .value("table", Integrand::kTable);
+  py::enum_<Rule>(m, "Rule").value("left", Rule::kLeft).value("mid", Rule::kMid).value("right", Rule::kRight);
+  py::enum_<DType>(m, "DType").value("fp64", DType::kF64).value("fp32", DType::kF32);
+  py::enum_<DivMode>(m, "DivMode").value("series", DivMode::kSeries).value("ieee", DivMode::kIeee);
+
+  m.attr("RIEMANN_TILE") = kRiemannTile;
+  m.attr("RIEMANN_BLOCK") = kRiemannBlock;
+  m.def("series_ok", &series_ok);
+  m.def("integrand_scale", &integrand_scale);
+
+  // ------------------------------------------------------------------ devices
+  m.def("device_count", &device_count);
+  m.def("device_info", [](int d) {
+    DeviceInfo i = device_info(d);
+    py::dict r;
+    r["index"] = i.index;
+    r["name"] = i.name;
+    r["arch"] = i.arch;
+    r["num_cus"] = i.num_cus;
+    r["clock_khz"] = i.clock_khz;
+    r["total_mem"] = i.total_mem;
+    r["l2_bytes"] = i.l2_bytes;
+    return r;
+  });
+  m.def("set_device", &set_device);
+  m.def("device_synchronize", []() { MIINT_HIP(hipDeviceSynchronize()); });
+  m.def("process_start_seconds", &process_start_seconds);
+  m.def("wall_seconds", &wall_seconds);
+
+  // ------------------------------------------------------------------ comm
+  py::class_<Comm>(m, "Comm")
+      .def(py::init([](py::bytes id, int rank, int world, int device) {
+             return new Comm(std::string(id), rank, world, device);
+           }),
+           py::arg("unique_id"), py::arg("rank"), py::arg("world"), py::arg("device"))
+      .def_static("unique_id", []() { return py::bytes(Comm::unique_id()); })
+      .def_static("version", &Comm::version)
+      .def_property_readonly("rank", &Comm::rank)
+      .def_property_readonly("world", &Comm::world)
+      .def_property_readonly("device", &Comm::device)
+      .def("allreduce_sum", [](const Comm& c, uintptr_t send, uintptr_t recv, size_t count,
+                               uintptr_t s) { c.allreduce_sum(ptr<double>(send), ptr<double>(recv), count, stream(s)); })
+      .def("allgather", [](const Comm& c, uintptr_t send, uintptr_t recv, size_t count,
+                           uintptr_t s) { c.allgather(ptr<double>(send), ptr<double>(recv), count, stream(s)); })
+      .def("broadcast", [](const Comm& c, uintptr_t buf, size_t count, int root, uintptr_t s) {
+        c.broadcast(ptr<double>(buf), count, root, stream(s));
+      })
+      .def("check_async", &Comm::check_async);
+  m.def("rendezvous_unique_id", &rendezvous_unique_id, py::arg("addr"), py::arg("port"),
+        py::arg("rank"), py::arg("world"), py::arg("timeout_s") = 120.0);
+
+  // ------------------------------------------------------------------ Riemann plan
+  py::class_<RiemannConfig>(m, "RiemannConfig")
+      .def(py::init<>())
+      .def_readwrite("integrand", &RiemannConfig::integrand)
+      .def_readwrite("a", &RiemannConfig::a)
+      .def_readwrite("b", &RiemannConfig::b)
+      .def_readwrite("n", &RiemannConfig::n)
+      .def_readwrite("rule", &RiemannConfig::rule)
+      .def_readwrite("dtype", &RiemannConfig::dtype)
+      .def_readwrite("div", &RiemannConfig::div)
+      .def_readwrite("coef", &RiemannConfig::coef)
+      .def_readwrite("p0", &RiemannConfig::p0)
+      .def_readwrite("p1", &RiemannConfig::p1)
+      .def_readwrite("table", &RiemannConfig::table)
+      .def_readwrite("grid", &RiemannConfig::grid)
+      .def_readwrite("waves_per_cu", &RiemannConfig::waves_per_cu)
+      .def_readwrite("fused", &RiemannConfig::fused)
+      .def_readwrite("slots", &RiemannConfig::slots)
+      .def_readwrite("rank", &RiemannConfig::rank)
+      .def_readwrite("world", &RiemannConfig::world);
+
+  py::class_<RiemannPlan>(m, "RiemannPlan")
+      .def(py::init<const RiemannConfig&, int, const Comm*>(), py::arg("config"),
+           py::arg("device"), py::arg("comm") = nullptr, py::keep_alive<1, 4>())
+      .def_property_readonly("device", &RiemannPlan::device)
+      .def_property_readonly("rank", &RiemannPlan::rank)
+      .def_property_readonly("world", &RiemannPlan::world)
+      .def_property_readonly("begin", &RiemannPlan::begin)
+      .def_property_readonly("count", &RiemannPlan::count)
+      .def_property_readonly("h", &RiemannPlan::h)
+      .def_property_readonly("scale", &RiemannPlan::scale)
+      .def_property_readonly("grid", [](const RiemannPlan& p) { return p.shape().grid; })
+      .def_property_readonly("block", [](const RiemannPlan& p) { return p.shape().block; })
+      .def_property_readonly("effective_div", &RiemannPlan::effective_div)
+      .def_property_readonly("compute_stream", [](const RiemannPlan& p) { return reinterpret_cast<uintptr_t>(p.compute_stream()); })
+      .def_property_readonly("comm_stream", [](const RiemannPlan& p) { return reinterpret_cast<uintptr_t>(p.comm_stream()); })
+      .def("run", &RiemannPlan::run, py::call_guard<py::gil_scoped_release>())
+      .def("capture_graphs", &RiemannPlan::capture_graphs)
+      .def("launch_steps", &RiemannPlan::launch_steps, py::arg("steps"), py::arg("pipeline") = true,
+           py::arg("graphs") = true, py::call_guard<py::gil_scoped_release>())
+      .def("sync", &RiemannPlan::sync, py::call_guard<py::gil_scoped_release>())
+      .def("run_steps", [](RiemannPlan& p, int steps, bool pipeline, bool graphs) {
+             StepTiming t;
+             {
+               py::gil_scoped_release nogil;
+               t = p.run_steps(steps, pipeline, graphs);
+             }
+             py::dict r;
+             r["wall_s"] = t.wall_s;
+             r["device_ms"] = t.device_ms;
+             r["steps"] = t.steps;
+             return r;
+           }, py::arg("steps"), py::arg("pipeline") = true, py::arg("graphs") = true)
+      .def("host_result", &RiemannPlan::host_result)
+      .def_property_readonly("host_capacity", &RiemannPlan::host_capacity)
+      .def("enqueue", [](const RiemannPlan& p, uintptr_t s, int slot, int hidx) { p.enqueue(stream(s), slot, hidx); })
+      .def("device_result", [](const RiemannPlan& p, int slot) { return reinterpret_cast<uintptr_t>(p.device_result(slot)); });
+
+  // ------------------------------------------------------------------ raw kernels
+  m.def("launch_riemann_partials",
+        [](int integrand, double a, double h, double off, uint64_t i_begin, uint64_t n,
+           std::vector<double> coef, double p0, double p1, DType dtype, DivMode div, int grid,
+           uintptr_t table, int table_n, uintptr_t partials, uintptr_t s) {
+          const RiemannParams p = make_params(integrand, a, h, off, i_begin, n, coef, p0, p1);
+          launch_riemann_partials(p, dtype, div, {grid, kRiemannBlock}, ptr<const double>(table),
+                                  table_n, ptr<double>(partials), stream(s));
+        });
+  m.def("launch_riemann_fused",
+        [](int integrand, double a, double h, double off, uint64_t i_begin, uint64_t n,
+           std::vector<double> coef, double p0, double p1, DType dtype, DivMode div, int grid,
+           uintptr_t table, int table_n, uintptr_t partials, uintptr_t ticket, double scale,
+           uintptr_t out, uintptr_t s) {
+          const RiemannParams p = make_params(integrand, a, h, off, i_begin, n, coef, p0, p1);
+          launch_riemann_fused(p, dtype, div, {grid, kRiemannBlock}, ptr<const double>(table),
+                               table_n, ptr<double>(partials), ptr<unsigned>(ticket), scale,
+                               ptr<double>(out), stream(s));
+        });
+  m.def("launch_riemann_point_values",
+        [](int integrand, double a, double h, double off, uint64_t i_begin, uint64_t n,
+           std::vector<double> coef, double p0, double p1, DivMode div, uintptr_t table,
+           int table_n, uintptr_t out, uintptr_t s) {
+          const RiemannParams p = make_params(integrand, a, h, off, i_begin, n, coef, p0, p1);
+          launch_riemann_point_values(p, div, ptr<const double>(table), table_n, ptr<double>(out),
+                                      stream(s));
+        });
+  m.def("launch_finalize", [](uintptr_t partials, int n, double scale, uintptr_t out, uintptr_t s) {
+    launch_finalize(ptr<const double>(partials), n, scale, ptr<double>(out), stream(s));
+  });
+  m.def("default_riemann_grid", [](int cus, int waves) { return default_riemann_shape(cus, waves).grid; });
+  m.def("default_reduce_grid", &default_reduce_grid);
+  m.def("launch_sum_array", [](uintptr_t x, uint64_t n, double scale, uintptr_t partials, int grid,
+                               uintptr_t out, uintptr_t s) {
+    launch_sum_array(ptr<const double>(x), n, scale, ptr<double>(partials), grid, ptr<double>(out), stream(s));
+  });
+  m.def("launch_interp_fill", [](uintptr_t table, int tn, double dt, uint64_t i0, uint64_t n,
+                                 uintptr_t y, uintptr_t s) {
+    launch_interp_fill(ptr<const double>(table), tn, dt, i0, n, ptr<double>(y), stream(s));
+  });
+  m.def("scan_state_bytes", &scan_state_bytes);
+  m.def("launch_inclusive_scan", [](uintptr_t in, uintptr_t out, uint64_t n, uintptr_t state,
+                                    uintptr_t carry, uintptr_t s) {
+    launch_inclusive_scan(ptr<const double>(in), ptr<double>(out), n, ptr<void>(state),
+                          ptr<const double>(carry), stream(s));
+  });
+  m.def("launch_interp_scan", [](uintptr_t table, int tn, double dt, uint64_t i0, uint64_t n,
+                                 uint64_t win_lo, uint64_t win_hi, uintptr_t out, uintptr_t state,
+                                 uintptr_t carry, uintptr_t s) {
+    launch_interp_scan_window(ptr<const double>(table), tn, dt, i0, n, win_lo, win_hi,
+                              ptr<double>(out), ptr<void>(state), ptr<const double>(carry), stream(s));
+  });
+  m.def("scan_timeout_flag", [](uintptr_t state, uintptr_t s) { return scan_timeout_flag(ptr<const void>(state), stream(s)); });
+  m.def("launch_add_carry", [](uintptr_t x, uint64_t n, uintptr_t carry, uintptr_t s) {
+    launch_add_carry(ptr<double>(x), n, ptr<const double>(carry), stream(s));
+  });
+  m.def("table2d_grid", [](int nx, int ny, double X, double Y, int gx, int gy, int row0, int row1) {
+    Table2DParams p{nullptr, nx, ny, X, Y, gx, gy, row0, row1};
+    return table2d_grid(p);
+  });
+  m.def("launch_table2d_partials", [](uintptr_t table, int nx, int ny, double X, double Y, int gx,
+                                      int gy, int row0, int row1, uintptr_t partials, uintptr_t s) {
+    Table2DParams p{ptr<const double>(table), nx, ny, X, Y, gx, gy, row0, row1};
+    launch_table2d_partials(p, ptr<double>(partials), stream(s));
+  });
+  m.def("launch_outer_product", [](uintptr_t v, int n, uintptr_t t, uintptr_t s) {
+    launch_outer_product(ptr<const double>(v), n, ptr<double>(t), stream(s));
+  });
+  m.def("selftest_wave_ops", [](uintptr_t in, uint64_t n, bool f32, uintptr_t sums, uintptr_t scan, uintptr_t s) {
+    selftest_wave_ops(ptr<const void>(in), n, f32, ptr<void>(sums), ptr<void>(scan), stream(s));
+  });
+  m.def("selftest_block_ops", [](uintptr_t in, uint64_t n, int block, bool f32, uintptr_t sums,
+                                 uintptr_t scan, uintptr_t s) {
+    selftest_block_ops(ptr<const void>(in), n, block, f32, ptr<void>(sums), ptr<void>(scan), stream(s));
+  });
+
+  // ------------------------------------------------------------------ train scan pipeline
+  py::class_<TrainScanConfig>(m, "TrainScanConfig")
+      .def(py::init<>())
+      .def_readwrite("steps_per_sec", &TrainScanConfig::steps_per_sec)
+      .def_readwrite("seconds", &TrainScanConfig::seconds)
+      .def_readwrite("parity", &TrainScanConfig::parity)
+      .def_readwrite("replicate", &TrainScanConfig::replicate)
+      .def_readwrite("phase2", &TrainScanConfig::phase2);
+  py::class_<TrainScan>(m, "TrainScan")
+      .def(py::init<const TrainScanConfig&, int, const Comm*>(), py::arg("config"),
+           py::arg("device"), py::arg("comm") = nullptr, py::keep_alive<1, 4>())
+      .def("run", [](TrainScan& t) {
+        TrainScanResult r;
+        {
+          py::gil_scoped_release nogil;
+          r = t.run();
+        }
+        py::dict d;
+        d["distance"] = r.distance;
+        d["sum_of_sums"] = r.sum_of_sums;
+        d["device_ms"] = r.device_ms;
+        d["timeout"] = r.timeout;
+        return d;
+      })
+      .def_property_readonly("local_begin", &TrainScan::local_begin)
+      .def_property_readonly("local_count", &TrainScan::local_count)
+      .def("velocity_ptr", [](const TrainScan& t) { return reinterpret_cast<uintptr_t>(t.velocity()); })
+      .def("position_ptr", [](const TrainScan& t) { return reinterpret_cast<uintptr_t>(t.position()); });
+
+  // ------------------------------------------------------------------ oracle
+  py::module_ o = m.def_submodule("oracle", "host oracles, generated fixtures, parity emulation");
+  o.def("profile_table", &oracle::profile_table);
+  o.def("interp", [](double t) { return oracle::interp(oracle::profile_table(), t); });
+  o.def("profile_exact_integral", &oracle::profile_exact_integral);
+  o.def("analytic", &oracle::analytic, py::arg("integrand"), py::arg("a"), py::arg("b"),
+        py::arg("coef") = std::vector<double>{}, py::arg("p0") = 0.0, py::arg("p1") = 0.0);
+  o.def("riemann_serial", [](Integrand f, double a, double b, uint64_t n, Rule r,
+                             std::vector<double> coef, double p0, double p1) {
+    py::gil_scoped_release nogil;
+    return static_cast<double>(oracle::riemann_serial(f, a, b, n, r, coef, p0, p1));
+  }, py::arg("integrand"), py::arg("a"), py::arg("b"), py::arg("n"), py::arg("rule"),
+     py::arg("coef") = std::vector<double>{}, py::arg("p0") = 0.0, py::arg("p1") = 0.0);
+  o.def("riemann_mpi_parity", &oracle::riemann_mpi_parity, py::arg("comm_size"), py::arg("n"),
+        py::arg("range") = 3.14159265358979323846, py::call_guard<py::gil_scoped_release>());
+  o.def("cintegrate_parity", &oracle::cintegrate_parity, py::call_guard<py::gil_scoped_release>());
+  o.def("trainscan_parity", [](int p) {
+    oracle::TrainScanParity r;
+    {
+      py::gil_scoped_release nogil;
+      r = oracle::trainscan_parity(p);
+    }
+    return py::make_tuple(r.distance, r.sum_of_sums);
+  });
+  o.def("train_distance", &oracle::train_distance);
+  o.attr("TRAIN_TS") = oracle::kTrainTs;
+  o.attr("TRAIN_VS") = oracle::kTrainVs;
+  o.attr("TRAIN_AS") = oracle::kTrainAs;
+  o.attr("STEPS_PER_SEC") = oracle::kStepsPerSec;
+  o.attr("PROFILE_SECONDS") = oracle::kProfileSeconds;
+}

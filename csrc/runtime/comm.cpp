@@ -1,0 +1,163 @@
+// RCCL communicator wrapper + TCP unique-id rendezvous (see miint/comm.hpp).
+#include "miint/comm.hpp"
+
+#include <arpa/inet.h>
+#include <netdb.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <chrono>
+#include <cstring>
+#include <thread>
+
+#include "miint/runtime.hpp"
+
+namespace miint {
+
+std::string Comm::unique_id() {
+  ncclUniqueId id;
+  MIINT_RCCL(ncclGetUniqueId(&id));
+  return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
+}
+
+Comm::Comm(const std::string& id, int rank, int world, int device)
+    : rank_(rank), world_(world), device_(device) {
+  MIINT_CHECK(id.size() == sizeof(ncclUniqueId), "unique id must be 128 bytes");
+  MIINT_CHECK(rank >= 0 && rank < world, "rank out of range");
+  ncclUniqueId uid;
+  std::memcpy(&uid, id.data(), sizeof(uid));
+  DeviceGuard g(device);
+  MIINT_RCCL(ncclCommInitRank(&comm_, world, uid, rank));
+}
+
+std::vector<std::unique_ptr<Comm>> Comm::init_all(const std::vector<int>& devices) {
+  const int n = static_cast<int>(devices.size());
+  MIINT_CHECK(n >= 1, "need at least one device");
+  std::vector<ncclComm_t> comms(n);
+  MIINT_RCCL(ncclCommInitAll(comms.data(), n, devices.data()));
+  std::vector<std::unique_ptr<Comm>> out;
+  for (int i = 0; i < n; ++i) {
+    std::unique_ptr<Comm> c(new Comm());
+    c->comm_ = comms[i];
+    c->rank_ = i;
+    c->world_ = n;
+    c->device_ = devices[i];
+    out.push_back(std::move(c));
+  }
+  return out;
+}
+
+Comm::~Comm() {
+  if (comm_) (void)ncclCommDestroy(comm_);
+}
+
+void Comm::allreduce_sum(const double* send, double* recv, size_t count, hipStream_t s) const {
+  MIINT_RCCL(ncclAllReduce(send, recv, count, ncclFloat64, ncclSum, comm_, s));
+}
+void Comm::allgather(const double* send, double* recv, size_t count, hipStream_t s) const {
+  MIINT_RCCL(ncclAllGather(send, recv, count, ncclFloat64, comm_, s));
+}
+void Comm::broadcast(double* buf, size_t count, int root, hipStream_t s) const {
+  MIINT_RCCL(ncclBroadcast(buf, buf, count, ncclFloat64, root, comm_, s));
+}
+void Comm::reduce_sum(const double* send, double* recv, size_t count, int root,
+                      hipStream_t s) const {
+  MIINT_RCCL(ncclReduce(send, recv, count, ncclFloat64, ncclSum, root, comm_, s));
+}
+void Comm::check_async() const {
+  ncclResult_t r = ncclSuccess;
+  MIINT_RCCL(ncclCommGetAsyncError(comm_, &r));
+  MIINT_RCCL(r);
+}
+void Comm::group_start() { MIINT_RCCL(ncclGroupStart()); }
+void Comm::group_end() { MIINT_RCCL(ncclGroupEnd()); }
+std::string Comm::version() {
+  int v = 0;
+  MIINT_RCCL(ncclGetVersion(&v));
+  return std::to_string(v);
+}
+
+// ------------------------------------------------------------------ TCP rendezvous
+namespace {
+
+bool send_all(int fd, const char* p, size_t n) {
+  while (n) {
+    ssize_t k = ::send(fd, p, n, MSG_NOSIGNAL);
+    if (k <= 0) return false;
+    p += k;
+    n -= static_cast<size_t>(k);
+  }
+  return true;
+}
+bool recv_all(int fd, char* p, size_t n) {
+  while (n) {
+    ssize_t k = ::recv(fd, p, n, 0);
+    if (k <= 0) return false;
+    p += k;
+    n -= static_cast<size_t>(k);
+  }
+  return true;
+}
+
+}  // namespace
+
+std::string rendezvous_unique_id(const std::string& addr, int port, int rank, int world,
+                                 double timeout_s) {
+  constexpr size_t kLen = sizeof(ncclUniqueId);
+  if (world == 1) return Comm::unique_id();
+  const double t0 = wall_seconds();
+  if (rank == 0) {
+    const std::string id = Comm::unique_id();
+    int srv = ::socket(AF_INET, SOCK_STREAM, 0);
+    MIINT_CHECK(srv >= 0, "socket()");
+    int one = 1;
+    ::setsockopt(srv, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
+    sockaddr_in sa{};
+    sa.sin_family = AF_INET;
+    sa.sin_port = htons(static_cast<uint16_t>(port));
+    sa.sin_addr.s_addr = htonl(INADDR_ANY);
+    if (::bind(srv, reinterpret_cast<sockaddr*>(&sa), sizeof(sa)) != 0) {
+      ::close(srv);
+      fail("rendezvous bind failed on port " + std::to_string(port), __FILE__, __LINE__);
+    }
+    ::listen(srv, world);
+    for (int served = 1; served < world; ++served) {
+      int c = ::accept(srv, nullptr, nullptr);
+      if (c < 0 || !send_all(c, id.data(), kLen)) {
+        if (c >= 0) ::close(c);
+        ::close(srv);
+        fail("rendezvous accept/send failed", __FILE__, __LINE__);
+      }
+      ::close(c);
+    }
+    ::close(srv);
+    return id;
+  }
+  // Non-zero ranks: retry until rank 0 listens.
+  addrinfo hints{}, *res = nullptr;
+  hints.ai_family = AF_INET;
+  hints.ai_socktype = SOCK_STREAM;
+  MIINT_CHECK(::getaddrinfo(addr.c_str(), std::to_string(port).c_str(), &hints, &res) == 0,
+              "getaddrinfo(" + addr + ")");
+  std::string id(kLen, '\0');
+  for (;;) {
+    int fd = ::socket(AF_INET, SOCK_STREAM, 0);
+    if (fd >= 0 && ::connect(fd, res->ai_addr, res->ai_addrlen) == 0 &&
+        recv_all(fd, &id[0], kLen)) {
+      ::close(fd);
+      break;
+    }
+    if (fd >= 0) ::close(fd);
+    if (wall_seconds() - t0 > timeout_s) {
+      ::freeaddrinfo(res);
+      fail("rendezvous timed out waiting for rank 0", __FILE__, __LINE__);
+    }
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+  }
+  ::freeaddrinfo(res);
+  return id;
+}
+
+}  // namespace miint

@@ -1,0 +1,185 @@
+// RiemannPlan implementation (see miint/integrator.hpp).
+#include "miint/integrator.hpp"
+
+#include <algorithm>
+
+namespace miint {
+
+namespace {
+constexpr int kHostRing = 4096;  // pinned result slots for non-graph step loops
+}
+
+RiemannPlan::RiemannPlan(const RiemannConfig& cfg, int device, const Comm* comm)
+    : cfg_(cfg), device_(device), comm_(comm), compute_((set_device(device), Stream())),
+      comm_stream_() {
+  MIINT_CHECK(cfg.n >= 1, "n must be >= 1");
+  MIINT_CHECK(cfg.b != cfg.a, "empty interval");
+  MIINT_CHECK(cfg.slots >= 1 && cfg.slots <= 64, "slots must be in [1, 64]");
+  if (comm) {
+    rank_ = comm->rank();
+    world_ = comm->world();
+    MIINT_CHECK(comm->device() == device, "communicator bound to another device");
+  } else {
+    MIINT_CHECK(cfg.world >= 1 && cfg.rank >= 0 && cfg.rank < cfg.world, "bad rank/world");
+    rank_ = cfg.rank;
+    world_ = cfg.world;
+  }
+  DeviceGuard g(device);
+  params_.a = cfg.a;
+  params_.h = (cfg.b - cfg.a) / static_cast<double>(cfg.n);
+  params_.off = rule_offset(cfg.rule);
+  rank_slice(cfg.n, rank_, world_, &params_.i_begin, &params_.n);
+  params_.integrand = static_cast<int>(cfg.integrand);
+  params_.ncoef = static_cast<int>(cfg.coef.size());
+  MIINT_CHECK(cfg.coef.size() <= static_cast<size_t>(kMaxPolyCoeffs), "too many coefficients");
+  for (size_t i = 0; i < cfg.coef.size(); ++i) params_.coef[i] = cfg.coef[i];
+  params_.p0 = cfg.p0;
+  params_.p1 = cfg.p1;
+  scale_ = params_.h * integrand_scale(cfg.integrand);
+
+  const DeviceInfo info = device_info(device);
+  shape_ = default_riemann_shape(info.num_cus, cfg.waves_per_cu);
+  if (cfg.grid > 0) shape_.grid = cfg.grid;
+  // Never launch more workgroups than there are tiles to deal out.
+  const uint64_t tiles = (params_.n + kRiemannTile - 1) / kRiemannTile;
+  const uint64_t need = std::max<uint64_t>(1, (tiles + kRiemannBlock - 1) / kRiemannBlock);
+  shape_.grid = static_cast<int>(std::min<uint64_t>(static_cast<uint64_t>(shape_.grid), need));
+
+  partials_ = DeviceBuffer<double>(static_cast<size_t>(shape_.grid));
+  result_ = DeviceBuffer<double>(static_cast<size_t>(cfg.slots));
+  ticket_ = DeviceBuffer<unsigned int>(1);
+  MIINT_HIP(hipMemset(ticket_.get(), 0, sizeof(unsigned int)));
+  MIINT_HIP(hipMemset(result_.get(), 0, result_.bytes()));
+  if (cfg.integrand == Integrand::kTable) {
+    MIINT_CHECK(cfg.table.size() >= 2, "table integrand needs a table");
+    table_ = DeviceBuffer<double>(cfg.table.size());
+    MIINT_HIP(hipMemcpy(table_.get(), cfg.table.data(), table_.bytes(), hipMemcpyHostToDevice));
+  }
+  host_ = PinnedBuffer<double>(static_cast<size_t>(std::max(kHostRing, cfg.slots)));
+  for (int i = 0; i < cfg.slots; ++i) {
+    ev_computed_.emplace_back(new Event(false));
+    ev_drained_.emplace_back(new Event(false));
+  }
+  MIINT_HIP(hipDeviceSynchronize());
+}
+
+RiemannPlan::~RiemannPlan() {
+  (void)hipSetDevice(device_);
+  (void)hipStreamSynchronize(compute_.get());
+  (void)hipStreamSynchronize(comm_stream_.get());
+}
+
+DivMode RiemannPlan::effective_div() const {
+  return (cfg_.div == DivMode::kSeries && !series_ok(params_.h)) ? DivMode::kIeee : cfg_.div;
+}
+
+void RiemannPlan::enqueue_compute(hipStream_t s, int slot) const {
+  double* out = result_.get() + slot;
+  const int tn = static_cast<int>(cfg_.table.size());
+  if (cfg_.fused) {
+    launch_riemann_fused(params_, cfg_.dtype, cfg_.div, shape_, table_.get(), tn,
+                         partials_.get(), ticket_.get(), scale_, out, s);
+  } else {
+    launch_riemann_partials(params_, cfg_.dtype, cfg_.div, shape_, table_.get(), tn,
+                            partials_.get(), s);
+    launch_finalize(partials_.get(), shape_.grid, scale_, out, s);
+  }
+}
+
+void RiemannPlan::enqueue_reduce(hipStream_t s, int slot) const {
+  if (comm_ && world_ > 1) {  // without a native comm the caller reduces (torch path)
+    double* v = result_.get() + slot;
+    comm_->allreduce_sum(v, v, 1, s);
+  }
+}
+
+void RiemannPlan::enqueue_copyout(hipStream_t s, int slot, int host_index) const {
+  MIINT_HIP(hipMemcpyAsync(host_.get() + host_index, result_.get() + slot, sizeof(double),
+                           hipMemcpyDeviceToHost, s));
+}
+
+void RiemannPlan::enqueue(hipStream_t s, int slot, int host_index) const {
+  enqueue_compute(s, slot);
+  enqueue_reduce(s, slot);
+  enqueue_copyout(s, slot, host_index);
+}
+
+double RiemannPlan::run() {
+  DeviceGuard g(device_);
+  enqueue(compute_.get(), 0, 0);
+  compute_.sync();
+  return host_[0];
+}
+
+void RiemannPlan::capture_graphs() {
+  DeviceGuard g(device_);
+  graphs_.clear();
+  comm_graphs_.clear();
+  for (int k = 0; k < cfg_.slots; ++k) {
+    std::unique_ptr<Graph> cg(new Graph());
+    cg->capture(compute_.get(), [&](hipStream_t s) { enqueue_compute(s, k); });
+    std::unique_ptr<Graph> rg(new Graph());
+    rg->capture(comm_stream_.get(), [&](hipStream_t s) {
+      enqueue_reduce(s, k);
+      enqueue_copyout(s, k, k);
+    });
+    graphs_.push_back(std::move(cg));
+    comm_graphs_.push_back(std::move(rg));
+  }
+}
+
+void RiemannPlan::launch_steps(int steps, bool pipeline, bool graphs) {
+  DeviceGuard g(device_);
+  if (graphs && graphs_.empty()) capture_graphs();
+  const int S = cfg_.slots;
+  hipStream_t cs = compute_.get();
+  hipStream_t rs = pipeline ? comm_stream_.get() : cs;
+  for (int k = 0; k < steps; ++k) {
+    const int slot = k % S;
+    const int hidx = graphs ? slot : k % host_capacity();
+    if (pipeline && k >= S) MIINT_HIP(hipStreamWaitEvent(cs, ev_drained_[slot]->get(), 0));
+    if (graphs) graphs_[slot]->launch(cs);
+    else enqueue_compute(cs, slot);
+    if (pipeline) {
+      ev_computed_[slot]->record(cs);
+      MIINT_HIP(hipStreamWaitEvent(rs, ev_computed_[slot]->get(), 0));
+    }
+    if (graphs) {
+      comm_graphs_[slot]->launch(rs);
+    } else {
+      enqueue_reduce(rs, slot);
+      enqueue_copyout(rs, slot, hidx);
+    }
+    if (pipeline) ev_drained_[slot]->record(rs);
+  }
+}
+
+void RiemannPlan::sync() const {
+  DeviceGuard g(device_);
+  compute_.sync();
+  comm_stream_.sync();
+}
+
+StepTiming RiemannPlan::run_steps(int steps, bool pipeline, bool graphs) {
+  DeviceGuard g(device_);
+  if (graphs && graphs_.empty()) capture_graphs();
+  StepTiming t;
+  sync();
+  const double w0 = wall_seconds();
+  ev_t0_.record(compute_.get());
+  launch_steps(steps, pipeline, graphs);
+  if (pipeline) {
+    // join the comm stream back into the compute stream for the end event
+    Event join(false);
+    join.record(comm_stream_.get());
+    MIINT_HIP(hipStreamWaitEvent(compute_.get(), join.get(), 0));
+  }
+  ev_t1_.record(compute_.get());
+  sync();
+  t.wall_s = wall_seconds() - w0;
+  t.device_ms = Event::elapsed_ms(ev_t0_, ev_t1_);
+  t.steps = steps;
+  return t;
+}
+
+}  // namespace miint

@@ -1,0 +1,112 @@
+// TrainScan implementation (see miint/trainscan.hpp).
+#include "miint/trainscan.hpp"
+
+#include "miint/integrator.hpp"
+#include "miint/kernels.hpp"
+#include "miint/oracle.hpp"
+
+namespace miint {
+
+TrainScan::TrainScan(const TrainScanConfig& cfg, int device, const Comm* comm)
+    : cfg_(cfg), device_(device), comm_(comm), stream_((set_device(device), Stream())) {
+  if (comm) {
+    rank_ = comm->rank();
+    world_ = comm->world();
+    MIINT_CHECK(comm->device() == device, "communicator bound to another device");
+  }
+  MIINT_CHECK(cfg.steps_per_sec >= 1 && cfg.seconds >= 1, "bad train-scan size");
+  total_ = static_cast<uint64_t>(cfg.steps_per_sec) * static_cast<uint64_t>(cfg.seconds);
+  if (cfg.parity) {
+    // 4main.c:90 subrange = tablelen / comm_sz (residual never scanned), and
+    // 4main.c:76-78 fill window = whole seconds floor(1800/P) per rank.
+    const uint64_t sub = total_ / static_cast<uint64_t>(world_);
+    begin_ = static_cast<uint64_t>(rank_) * sub;
+    count_ = sub;
+    const uint64_t fs = static_cast<uint64_t>(cfg.seconds / world_) * cfg.steps_per_sec;
+    win_lo_ = static_cast<uint64_t>(rank_) * fs;
+    win_hi_ = win_lo_ + fs;
+  } else {
+    rank_slice(total_, rank_, world_, &begin_, &count_);
+  }
+  MIINT_CHECK(count_ >= 1, "empty slice");
+  const auto& tab = oracle::profile_table();
+  table_ = DeviceBuffer<double>(tab.size());
+  MIINT_HIP(hipMemcpy(table_.get(), tab.data(), table_.bytes(), hipMemcpyHostToDevice));
+  vel_ = DeviceBuffer<double>(count_);
+  if (cfg.phase2) pos_ = DeviceBuffer<double>(count_);
+  if (cfg.replicate) {
+    MIINT_CHECK(!cfg.parity && total_ % static_cast<uint64_t>(world_) == 0,
+                "replicate needs equal slices (total divisible by world, no parity)");
+    full_ = DeviceBuffer<double>(total_);
+  }
+  state_ = DeviceBuffer<char>(scan_state_bytes(count_));
+  scratch_ = DeviceBuffer<double>(8 + static_cast<size_t>(world_));
+  host_ = PinnedBuffer<double>(4);
+  MIINT_HIP(hipMemset(scratch_.get(), 0, scratch_.bytes()));
+  MIINT_HIP(hipDeviceSynchronize());
+}
+
+// Replace this rank's locally scanned slice by the globally scanned one: allgather every
+// rank's local total, form the exclusive carry for this rank, add it in place.
+void TrainScan::exchange_carry(const double* slice, uint64_t n, double* slice_out,
+                               hipStream_t s) {
+  if (!comm_ || world_ == 1) return;
+  double* sc = scratch_.get();
+  MIINT_HIP(hipMemcpyAsync(sc, slice + (n - 1), sizeof(double), hipMemcpyDeviceToDevice, s));
+  comm_->allgather(sc, sc + 8, 1, s);
+  launch_exclusive_carry(sc + 8, rank_, sc + 1, s);
+  if (rank_ > 0) launch_add_carry(slice_out, n, sc + 1, s);
+}
+
+// Value of global element `gi` (0 if no rank owns it, e.g. 4main's unscanned residual).
+double TrainScan::pick_global(const double* slice, uint64_t gi, hipStream_t s) {
+  double* sc = scratch_.get();
+  MIINT_HIP(hipMemsetAsync(sc + 2, 0, sizeof(double), s));
+  if (gi >= begin_ && gi < begin_ + count_)
+    MIINT_HIP(hipMemcpyAsync(sc + 2, slice + (gi - begin_), sizeof(double),
+                             hipMemcpyDeviceToDevice, s));
+  if (comm_ && world_ > 1) comm_->allreduce_sum(sc + 2, sc + 2, 1, s);
+  MIINT_HIP(hipMemcpyAsync(host_.get(), sc + 2, sizeof(double), hipMemcpyDeviceToHost, s));
+  MIINT_HIP(hipStreamSynchronize(s));
+  return host_[0];
+}
+
+TrainScanResult TrainScan::run() {
+  DeviceGuard g(device_);
+  hipStream_t s = stream_.get();
+  TrainScanResult r;
+  const double dt = 1.0 / cfg_.steps_per_sec;
+  const int tn = static_cast<int>(oracle::profile_table().size());
+  e0_.record(s);
+  // Phase 1: velocity samples -> running integral (4main.c:95-160)
+  launch_interp_scan_window(table_.get(), tn, dt, begin_, count_, win_lo_, win_hi_, vel_.get(),
+                            state_.get(), nullptr, s);
+  exchange_carry(vel_.get(), count_, vel_.get(), s);
+  // Phase 2: running integral -> sum of sums (4main.c:178-221)
+  if (cfg_.phase2) {
+    launch_inclusive_scan(vel_.get(), pos_.get(), count_, state_.get(), nullptr, s);
+    exchange_carry(pos_.get(), count_, pos_.get(), s);
+  }
+  if (cfg_.replicate) {
+    if (comm_) {
+      comm_->allgather(vel_.get(), full_.get(), count_, s);
+    } else {
+      MIINT_HIP(hipMemcpyAsync(full_.get(), vel_.get(), count_ * sizeof(double),
+                               hipMemcpyDeviceToDevice, s));
+    }
+  }
+  e1_.record(s);
+  MIINT_HIP(hipStreamSynchronize(s));
+  r.device_ms = Event::elapsed_ms(e0_, e1_);
+  r.timeout = scan_timeout_flag(state_.get(), s);
+  // 4main.c:241 prints default_sum[tablelen-2]; the complete integral is element T-1.
+  const uint64_t gi = cfg_.parity ? total_ - 2 : total_ - 1;
+  r.distance = pick_global(vel_.get(), gi, s) / cfg_.steps_per_sec;
+  if (cfg_.phase2) {
+    const uint64_t last = cfg_.parity ? (total_ / world_) * world_ - 1 : total_ - 1;
+    r.sum_of_sums = pick_global(pos_.get(), last, s);
+  }
+  return r;
+}
+
+}  // namespace miint

@@ -1,0 +1,114 @@
+"""Process-group bootstrap: one process per GPU under torchrun / torch.distributed.
+
+Replaces MPI_Init/Comm_size/Comm_rank (riemann.cpp:62-64, 4main.c:69-71). Two kinds of
+communicator come out of it:
+  * the torch.distributed process group (backend "nccl" == RCCL on ROCm, "gloo" on CPU);
+  * a native RCCL communicator owned by the C++ runtime (``_miint.Comm``), bootstrapped with
+    a unique id that rank 0 publishes through the torch.distributed store. The native one is
+    what the Riemann plans capture into hipGraphs together with their kernels.
+"""
+from __future__ import annotations
+
+import dataclasses
+import datetime
+import os
+
+import torch
+import torch.distributed as dist
+
+
+@dataclasses.dataclass
+class DistContext:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    device: int = 0
+    backend: str = "none"
+    initialized_here: bool = False
+
+    @property
+    def is_root(self) -> bool:
+        return self.rank == 0
+
+    def barrier(self) -> None:
+        if self.world > 1 and dist.is_initialized():
+            if self.backend == "nccl":
+                dist.barrier(device_ids=[self.device])
+            else:
+                dist.barrier()
+
+    def all_reduce_sum(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return t
+
+    def all_reduce_max(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return t
+
+    def all_gather_scalars(self, value: float, device=None) -> list[float]:
+        dev = device if device is not None else ("cuda" if self.backend == "nccl" else "cpu")
+        t = torch.tensor([value], dtype=torch.float64, device=dev)
+        if self.world == 1:
+            return [value]
+        out = [torch.zeros_like(t) for _ in range(self.world)]
+        dist.all_gather(out, t)
+        return [float(x.item()) for x in out]
+
+    def destroy(self) -> None:
+        if self.initialized_here and dist.is_initialized():
+            dist.destroy_process_group()
+            self.initialized_here = False
+
+
+def env_world() -> tuple[int, int, int]:
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def init(backend: str | None = None, timeout_s: float = 300.0, force: bool = False) -> DistContext:
+    """Initialise from the torchrun environment (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*).
+
+    Single-process runs skip process-group creation unless ``force``. The default
+    MASTER_ADDR is 127.0.0.1 (the container hostname may not resolve).
+    """
+    rank, world, local = env_world()
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+    ctx = DistContext(rank=rank, world=world, local_rank=local, backend=backend)
+    if backend == "nccl":
+        ctx.device = local
+        torch.cuda.set_device(local)
+    if world > 1 or force:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29531")
+        if not dist.is_initialized():
+            kw = {}
+            if backend == "nccl":
+                kw["device_id"] = torch.device("cuda", local)
+            dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                    timeout=datetime.timedelta(seconds=timeout_s), **kw)
+            ctx.initialized_here = True
+    else:
+        ctx.backend = backend if dist.is_initialized() else "none"
+    return ctx
+
+
+_uid_counter = [0]
+
+
+def native_comm(ctx: DistContext):
+    """Create a native RCCL communicator (``_miint.Comm``) spanning the process group."""
+    from .._native import native
+
+    m = native()
+    _uid_counter[0] += 1
+    if ctx.world == 1:
+        return m.Comm(m.Comm.unique_id(), 0, 1, ctx.device)
+    store = dist.distributed_c10d._get_default_store()
+    key = f"miint_rccl_uid_{_uid_counter[0]}"
+    if ctx.rank == 0:
+        store.set(key, m.Comm.unique_id())
+    uid = store.get(key)
+    return m.Comm(bytes(uid), ctx.rank, ctx.world, ctx.device)

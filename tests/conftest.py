@@ -1,0 +1,63 @@
+"""Test configuration.
+
+Markers
+  gpu   needs an MI355X (HIP device). The driver runs `-m "not gpu"` on a CPU box and
+        `-m gpu` on a GPU box. GPU tests never fall back to CPU paths: they exercise the
+        in-tree native extension (cuda_v_mpi_amd/_miint*.so) and fail if it is missing.
+
+The native extension is (re)built once per session if sources are newer than the .so, so a
+fresh checkout works on both boxes.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: requires a HIP GPU (MI355X / gfx950)")
+    config.addinivalue_line("markers", "slow: long-running test")
+
+
+def _has_gpu() -> bool:
+    try:
+        import torch
+
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+HAS_GPU = _has_gpu()
+
+
+def pytest_collection_modifyitems(config, items):
+    if HAS_GPU:
+        return
+    skip = pytest.mark.skip(reason="no HIP device")
+    for it in items:
+        if "gpu" in it.keywords:
+            it.add_marker(skip)
+
+
+@pytest.fixture(scope="session")
+def native():
+    """The native module (built in-tree if stale). Loads without a GPU too."""
+    from cuda_v_mpi_amd._native import native as load
+
+    return load()
+
+
+@pytest.fixture(scope="session")
+def cuda(native):
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda", 0)

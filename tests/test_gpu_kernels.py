@@ -1,0 +1,203 @@
+"""GPU numerics tests: every HIP kernel against a plain PyTorch fp64 reference of the same op.
+
+Runs only on an MI355X (marker `gpu`); exercises the in-tree native extension directly.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from cuda_v_mpi_amd.models import integrands
+from cuda_v_mpi_amd.ops import kernels
+from cuda_v_mpi_amd.utils import fixtures
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_sum(spec, n, rule="left", i_begin=0, n_local=None, dtype=torch.float64):
+    """fp64 torch reference of h*scale*sum f over the launch's samples (chunked)."""
+    n_local = n if n_local is None else n_local
+    h = (spec.b - spec.a) / n
+    off = {"left": 0.0, "mid": 0.5, "right": 1.0}[rule]
+    parts = []
+    for s in range(i_begin, i_begin + n_local, 1 << 22):
+        i = torch.arange(s, min(i_begin + n_local, s + (1 << 22)), dtype=torch.float64,
+                         device="cuda")
+        x = spec.a + (i + off) * h
+        parts.append(float(spec.f_torch(x.to(dtype)).to(torch.float64).sum()))
+    return math.fsum(parts) * h
+
+
+SPECS = [integrands.pi4(), integrands.sin(), integrands.poly(seed=3), integrands.train(),
+         integrands.table()]
+
+
+@pytest.mark.parametrize("spec", SPECS, ids=lambda s: s.name)
+@pytest.mark.parametrize("n", [1, 63, 1000, 4097, 1_000_003])
+def test_riemann_vs_torch(cuda, spec, n):
+    got = float(kernels.riemann(spec, n, rule="mid").item())
+    want = _ref_sum(spec, n, rule="mid")
+    assert got == pytest.approx(want, rel=1e-12, abs=1e-12)
+
+
+@pytest.mark.parametrize("spec", SPECS, ids=lambda s: s.name)
+def test_fused_equals_two_kernel_bitwise(cuda, spec):
+    n = 3_000_017
+    a = float(kernels.riemann(spec, n, fused=True).item())
+    b = float(kernels.riemann(spec, n, fused=False).item())
+    assert a == b  # same partials, same fixed-order final sum
+
+
+def test_rank_slices_sum_to_whole(cuda):
+    spec = integrands.pi4()
+    n = 10_000_019
+    whole = float(kernels.riemann(spec, n).item())
+    parts = []
+    from cuda_v_mpi_amd.parallel.decomposition import rank_slice
+    for r in range(7):
+        b, c = rank_slice(n, r, 7)
+        parts.append(float(kernels.riemann(spec, n, i_begin=b, n_local=c).item()))
+    assert math.fsum(parts) == pytest.approx(whole, rel=1e-14)
+
+
+def test_pi4_series_per_point_accuracy(cuda):
+    """The series reciprocal evaluates every sample to fp64 accuracy (<= 2 ulp vs IEEE)."""
+    spec = integrands.pi4()
+    n = 10**9
+    for i0 in (0, 123_456_789, 999_000_000):
+        v = kernels.point_values(spec, n, rule="left", div="series", i_begin=i0, n_local=1 << 16)
+        w = kernels.point_values(spec, n, rule="left", div="ieee", i_begin=i0, n_local=1 << 16)
+        ulp = torch.abs(v - w) / (torch.finfo(torch.float64).eps * torch.abs(w))
+        assert float(ulp.max()) <= 2.0
+
+
+def test_pi4_1e9_left_error_is_truncation(cuda):
+    v = float(kernels.riemann(integrands.pi4(), 10**9, rule="left").item())
+    assert abs((v - math.pi) - 1e-9) < 1e-13   # left rule error = h exactly
+
+
+def test_pi4_1e9_mid_error(cuda):
+    v = float(kernels.riemann(integrands.pi4(), 10**9, rule="mid").item())
+    assert abs(v - math.pi) < 1e-13
+
+
+def test_series_equals_ieee_sum(cuda):
+    spec = integrands.pi4()
+    a = float(kernels.riemann(spec, 10**8, div="series").item())
+    b = float(kernels.riemann(spec, 10**8, div="ieee").item())
+    assert a == pytest.approx(b, rel=1e-14)
+
+
+def test_fp32_error_vs_fp64(cuda):
+    spec = integrands.pi4()
+    f32 = float(kernels.riemann(spec, 10**9, rule="mid", dtype="fp32").item())
+    f64 = float(kernels.riemann(spec, 10**9, rule="mid", dtype="fp64").item())
+    assert abs(f32 - f64) < 1e-5
+    f32i = float(kernels.riemann(spec, 10**7, rule="mid", dtype="fp32", div="ieee").item())
+    assert abs(f32i - math.pi) < 1e-5
+
+
+def test_deterministic_bitwise(cuda):
+    spec = integrands.sin()
+    vals = {float(kernels.riemann(spec, 50_000_000).item()) for _ in range(5)}
+    assert len(vals) == 1
+
+
+def test_large_n_64bit_index(cuda):
+    """N = 5e9 > 2^32 samples (the reference's int counters overflow)."""
+    v = float(kernels.riemann(integrands.pi4(), 5 * 10**9, rule="mid").item())
+    assert abs(v - math.pi) < 1e-12
+
+
+# ------------------------------------------------------------------ DPP primitives
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("n", [1, 64, 100, 4096, 100_003])
+def test_wave_ops(cuda, dtype, n):
+    g = torch.Generator(device="cpu").manual_seed(n)
+    x = torch.randn(n, generator=g, dtype=torch.float64).to(dtype).cuda()
+    sums, scan = kernels.wave_ops(x)
+    pad = torch.zeros(math.ceil(n / 64) * 64, dtype=torch.float64, device="cuda")
+    pad[:n] = x.double()
+    w = pad.view(-1, 64)
+    tol = 1e-12 if dtype == torch.float64 else 1e-4
+    torch.testing.assert_close(sums.double(), w.sum(1), rtol=tol, atol=tol)
+    torch.testing.assert_close(scan.double(), w.cumsum(1).flatten()[:n], rtol=tol, atol=tol)
+
+
+@pytest.mark.parametrize("block", [64, 128, 192, 256, 512, 1024])
+def test_block_ops(cuda, block):
+    n = 10 * block + 7
+    x = torch.randn(n, dtype=torch.float64, device="cuda")
+    sums, scan = kernels.block_ops(x, block)
+    pad = torch.zeros(math.ceil(n / block) * block, dtype=torch.float64, device="cuda")
+    pad[:n] = x
+    w = pad.view(-1, block)
+    torch.testing.assert_close(sums, w.sum(1), rtol=1e-12, atol=1e-12)
+    torch.testing.assert_close(scan, w.cumsum(1).flatten()[:n], rtol=1e-12, atol=1e-12)
+
+
+# ------------------------------------------------------------------ table kernels
+@pytest.mark.parametrize("n", [1, 2, 1001, 18_000_000])
+def test_sum_array(cuda, n):
+    x = torch.rand(n, dtype=torch.float64, device="cuda")
+    got = float(kernels.sum_array(x, scale=0.5).item())
+    want = float(x.sum()) * 0.5
+    assert got == pytest.approx(want, rel=1e-12)
+
+
+@pytest.mark.parametrize("i0,n", [(0, 18_000_000), (7, 1001), (17_999_000, 1000)])
+def test_interp_fill(cuda, i0, n):
+    y = kernels.interp_fill(n, i0=i0)
+    tab = torch.as_tensor(fixtures.profile_table(), device="cuda")
+    t = 1e-4 * torch.arange(i0, i0 + n, dtype=torch.float64, device="cuda")
+    want = integrands.table().f_torch(t)
+    torch.testing.assert_close(y, want, rtol=1e-13, atol=1e-12)
+    del tab
+
+
+@pytest.mark.parametrize("n", [1, 4095, 4096, 4097, 1_000_000, 18_000_000])
+def test_inclusive_scan(cuda, n):
+    x = torch.rand(n, dtype=torch.float64, device="cuda")
+    got = kernels.inclusive_scan(x)
+    want = torch.cumsum(x, 0)
+    torch.testing.assert_close(got, want, rtol=1e-11, atol=1e-9)
+
+
+def test_scan_with_carry(cuda):
+    x = torch.rand(100_000, dtype=torch.float64, device="cuda")
+    c = torch.tensor([12.5], dtype=torch.float64, device="cuda")
+    torch.testing.assert_close(kernels.inclusive_scan(x, carry=c), torch.cumsum(x, 0) + 12.5,
+                               rtol=1e-12, atol=1e-9)
+
+
+def test_interp_scan_matches_fill_then_scan(cuda):
+    n = 18_000_000
+    fused = kernels.interp_scan(n)
+    two = torch.cumsum(kernels.interp_fill(n), 0)
+    torch.testing.assert_close(fused, two, rtol=1e-11, atol=1e-6)
+    assert float(fused[-2].item()) / 1e4 == pytest.approx(122000.004030, abs=2e-6)
+
+
+def test_table2d_separable_oracle(cuda):
+    v = torch.as_tensor(fixtures.profile_table(), device="cuda")
+    T = kernels.outer_product(v)
+    torch.testing.assert_close(T, torch.outer(v, v))
+    g = 4096
+    got = float(kernels.table2d(T, 1800.0, 1800.0, g, g).item())
+    xs = (torch.arange(g, dtype=torch.float64, device="cuda") + 0.5) * (1800.0 / g)
+    s1 = float(integrands.table().f_torch(xs).sum()) * (1800.0 / g)
+    assert got == pytest.approx(s1 * s1, rel=1e-12)
+    assert got == pytest.approx(122000.004 ** 2, rel=1e-5)
+
+
+def test_table2d_row_split(cuda):
+    v = torch.as_tensor(fixtures.profile_table(), device="cuda")
+    T = kernels.outer_product(v)
+    g = 1000
+    whole = float(kernels.table2d(T, 1800.0, 1800.0, g, g).item())
+    parts = [float(kernels.table2d(T, 1800.0, 1800.0, g, g, r0, r1).item())
+             for r0, r1 in [(0, 333), (333, 700), (700, 1000)]]
+    assert math.fsum(parts) == pytest.approx(whole, rel=1e-13)

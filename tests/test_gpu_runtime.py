@@ -1,0 +1,117 @@
+"""GPU tests of the native runtime: plans, hipGraph replay, train scan, CLI tools."""
+from __future__ import annotations
+
+import json
+import math
+import os
+import subprocess
+
+import pytest
+
+from cuda_v_mpi_amd import Integrator
+from cuda_v_mpi_amd.utils import output
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(REPO, "build", "bin")
+
+
+def test_integrator_pi4(cuda):
+    r = Integrator("pi4", n=10**9, rule="left").run()
+    assert abs(r.abs_err - 1e-9) < 1e-13
+    assert r.seconds_device > 0
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+@pytest.mark.parametrize("fused", [False, True])
+def test_plan_steps_graph_and_plain_agree(cuda, graphs, fused):
+    it = Integrator("sin", n=10**8, fused=fused)
+    one = it.run().value
+    t = it.run_steps(9, pipeline=False, graphs=graphs)
+    assert t["steps"] == 9 and t["device_ms"] > 0
+    slot = 8 % 4 if graphs else 8
+    assert it.plan.host_result(slot) == one
+
+
+def test_plan_effective_div_fallback(cuda):
+    # h = 1e-3 is too coarse for the series reciprocal -> IEEE division is used
+    it = Integrator("pi4", n=1000, div="series")
+    assert "ieee" in str(it.plan.effective_div)
+    assert it.run().value == pytest.approx(math.pi + 1e-3, abs=1e-7)
+
+
+def test_trainscan_native(native, cuda):
+    ts = native.TrainScan(native.TrainScanConfig(), 0)
+    r = ts.run()
+    assert r["timeout"] == 0
+    assert "%f" % r["distance"] == "%f" % 122000.004030 or abs(r["distance"] - 122000.00403) < 2e-6
+    assert r["sum_of_sums"] / 1e8 == pytest.approx(109861003.621919, rel=1e-12)
+
+
+def _run(args, env=None, timeout=300):
+    e = dict(os.environ)
+    e.update(env or {})
+    return subprocess.run(args, capture_output=True, text=True, timeout=timeout, env=e)
+
+
+@pytest.fixture(scope="module")
+def cli_built(native):
+    if not os.path.exists(os.path.join(BIN, "riemann")):
+        subprocess.run(["make", "-C", REPO, "-j8", "cli"], check=True)
+    return BIN
+
+
+def test_cli_riemann_format(cli_built):
+    p = _run([os.path.join(cli_built, "riemann")])
+    assert p.returncode == 0, p.stderr
+    lines = p.stdout.strip().splitlines()
+    assert lines[0].endswith(" seconds")
+    float(lines[0].split()[0])
+    assert lines[1].startswith("The integral of f(x) from 0.0 to 3.14159265358979 with "
+                               "1000000000 steps is ")
+    assert float(lines[1].rsplit(" ", 1)[1]) == pytest.approx(2.0, abs=1e-11)
+
+
+def test_cli_riemann_parity_single_rank_is_zero(cli_built):
+    p = _run([os.path.join(cli_built, "riemann"), "--parity", "--n", "1e6"])
+    assert p.returncode == 0, p.stderr
+    assert p.stdout.strip().splitlines()[1].endswith(" steps is 0")
+
+
+def test_cli_cintegrate(cli_built):
+    p = _run([os.path.join(cli_built, "cintegrate")])
+    assert p.returncode == 0, p.stderr
+    l = p.stdout.strip().splitlines()
+    assert l[1] == output.fmt_cintegrate_distance(122000.004030)
+    q = _run([os.path.join(cli_built, "cintegrate"), "--parity"])
+    assert q.stdout.strip().splitlines()[1] == "final distance is:121999.800663"
+    m = _run([os.path.join(cli_built, "cintegrate"), "--materialize"])
+    assert m.stdout.strip().splitlines()[1] == "final distance is:122000.004030"
+
+
+def test_cli_trainscan(cli_built):
+    p = _run([os.path.join(cli_built, "trainscan"), "--json"])
+    assert p.returncode == 0, p.stderr
+    l = p.stdout.strip().splitlines()
+    assert l[0] == "Step size of 10000"
+    assert l[1].endswith(" seconds")
+    assert l[2] == "Total distance traveled = 122000.004030"
+    js = json.loads(l[3])
+    assert js["timeout"] == 0
+
+
+def test_cli_selfcheck(cli_built):
+    p = _run([os.path.join(cli_built, "miint"), "selfcheck"])
+    assert p.returncode == 0, p.stdout + p.stderr
+    assert "SELFCHECK OK" in p.stdout
+
+
+def test_bench_contract(native, cuda):
+    p = _run(["python", os.path.join(REPO, "bench.py"), "--steps", "20", "--warmup", "3"])
+    assert p.returncode == 0, p.stderr
+    js = json.loads(p.stdout.strip().splitlines()[-1])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config"):
+        assert k in js
+    assert js["n_gpus"] == 1 and js["steps"] == 20 and js["verified"]
+    assert js["value"] > 1e11

@@ -1,0 +1,26 @@
+#!/usr/bin/env bash
+# Run a sequence of GPU steps on the gpurun box, each under its own time limit, stopping at
+# the first fault-like exit (timeout 124/137, abort 134, segfault 139, signal > 128).
+# Ordinary test failures (exit 1/2/3) do not stop the session.
+#
+#   tools/gpu_session.sh "name:seconds:command" ...
+# Output of each step: gpurun_out/<name>.txt ; summary: gpurun_out/session.txt
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+: > gpurun_out/session.txt
+for spec in "$@"; do
+  name="${spec%%:*}"; rest="${spec#*:}"
+  secs="${rest%%:*}"; cmd="${rest#*:}"
+  start=$(date +%s)
+  echo "=== $name ($secs s): $cmd" | tee -a gpurun_out/session.txt
+  timeout -k 10 "$secs" bash -c "$cmd" > "gpurun_out/$name.txt" 2>&1
+  rc=$?
+  echo "=== $name rc=$rc elapsed=$(( $(date +%s) - start ))s" | tee -a gpurun_out/session.txt
+  tail -n 5 "gpurun_out/$name.txt" | sed 's/^/    /' | tee -a gpurun_out/session.txt
+  if [ "$rc" -ge 124 ]; then
+    echo "=== stopping: fault-like exit $rc in $name" | tee -a gpurun_out/session.txt
+    exit "$rc"
+  fi
+done
+exit 0

@@ -37,7 +37,7 @@ def parse() -> argparse.Namespace:
     p.add_argument("--integrand", default="pi4")
     p.add_argument("--rule", default="left", choices=["left", "mid", "right"])
     p.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
-    p.add_argument("--div", default="series", choices=["series", "ieee"])
+    p.add_argument("--div", default="series", choices=["series", "ieee", "series_direct"])
     p.add_argument("--comm", default="native", choices=["native", "torch"])
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--no-pipeline", action="store_true")
@@ -94,8 +94,8 @@ def main() -> int:
 
     # ---- verify every result still in the host ring (graphs: slot ring of 4)
     analytic = integ.spec.analytic()
-    nres = min(args.steps, 4 if graphs else plan.host_capacity)
-    vals = [plan.host_result(i) for i in range(nres)]
+    last = range(max(0, args.steps - min(args.steps, plan.slots)), args.steps)
+    vals = [plan.host_result(plan.host_index_of(k, graphs)) for k in last]
     errs = [abs(v - analytic) for v in vals]
     abs_err = max(errs)
     # left rule truncation for 4/(1+x^2) is exactly h; anything far above is a bug

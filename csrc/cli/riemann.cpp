@@ -91,7 +91,7 @@ int main(int argc, char** argv) {
         StepTiming t = plan.run_steps(iters, comm != nullptr, iters > 1);
         std::lock_guard<std::mutex> g(mu);
         if (rank == topo.rank0) {
-          result = plan.host_result(iters > 1 ? (iters - 1) % cfg.slots : 0);
+          result = plan.host_result(plan.host_index_of(iters - 1, iters > 1));
           dev_ms = t.device_ms / iters;
         }
       });

@@ -58,11 +58,12 @@ enum class Integrand : int {
 // error (exactly h for 4/(1+x^2)) hides every other error source.
 enum class Rule : int { kLeft = 0, kMid = 1, kRight = 2 };
 
-// How the fp64 Pi4 kernel divides. kSeries (default) seeds each U-point tile with one
-// v_rcp_f64 and corrects every point with the exact residual series
-// 1/d = s(1+e+e^2+e^3), e = 1 - d*s (|e| <= U*h, so truncation is < 1e-21 relative).
-// kIeee uses the compiler's correctly-rounded division for every point (reference path).
-enum class DivMode : int { kSeries = 0, kIeee = 1 };
+// How the Pi4 kernels divide (see integrands.hpp for the derivation):
+//   kSeries        per-tile v_rcp_f64 seed, per-sample exact residual e = 1 - d*s evaluated
+//                  pairwise from the tile midpoint, 1/d = s(1+e+e^2)   (default, 3.5 ops)
+//   kIeee          correctly rounded division for every sample (reference path)
+//   kSeriesDirect  the same series with x, d formed explicitly per sample (5 ops; A/B)
+enum class DivMode : int { kSeries = 0, kIeee = 1, kSeriesDirect = 2 };
 
 inline double rule_offset(Rule r) {
   return r == Rule::kLeft ? 0.0 : (r == Rule::kMid ? 0.5 : 1.0);

@@ -26,23 +26,63 @@ namespace miint {
 // ------------------------------------------------------------------ 4/(1+x^2), fp64
 //
 // Division is the whole cost of this integrand. The IEEE path (DivMode::kIeee) lets the
-// compiler emit v_div_scale/v_rcp_f64/v_fma_f64 x4/v_div_fmas/v_div_fixup per point.
-// The series path evaluates the same reciprocal per point from a per-tile seed:
-//   s  ~= 1/d(x_mid)                 (v_rcp_f64 + one Newton step, once per U points)
-//   e_u = 1 - d_u*s                  (exact residual via fma, |e_u| <= (U/2)*h*|f'/f| + eps)
-//   1/d_u = s*(1 + e_u + e_u^2 + e_u^3/(1-e_u))
+// compiler emit v_div_scale/v_rcp_f64/v_fma_f64 x4/v_div_fmas/v_div_fixup per point
+// (~14 VALU f64 ops per sample with the coordinate and the accumulation).
+//
+// The series paths evaluate the same reciprocal per point from a per-tile seed:
+//   s  ~= 1/d(x_m)                   (v_rcp_f64 + one Newton step, once per U points;
+//                                     x_m = tile midpoint)
+//   e_u = 1 - d(x_u)*s               (the point's exact residual)
+//   1/d(x_u) = s*(1 + e_u + e_u^2 + e_u^3/(1-e_u))
 // |e_u| <= (U/2)*h (max of 2|x|/(1+x^2) is 1), so the dropped e^3 term is < 1e-17 relative
 // whenever (U/2)*h <= 2e-6; the host dispatcher (series_ok()) falls back to kIeee otherwise.
-// Every point is therefore still evaluated to fp64 accuracy; the per-point cost drops from ~10 VALU f64 ops to 5
-// (x, d, e, and the two accumulations). Nothing is skipped: every sample x_u is formed and
-// its reciprocal residual computed (tests check per-point agreement with IEEE division).
+//
+// kSeriesDirect forms x_u = x0 + u*h, d_u = 1 + x_u^2, e_u = 1 - d_u*s explicitly (5 ops).
+// kSeries (default) evaluates the very same residual with the offset k = u - (U-1)/2 from
+// the midpoint: since d(x_m + k h) = d_m + 2 x_m h k + h^2 k^2 exactly,
+//   e_k = e_m + k*A + k^2*B,   A = -2 x_m h s,  B = -h^2 s,  e_m = 1 - d_m s,
+// and the two samples at +-k share c_k = e_m + k^2 B:  e_{+-k} = c_k +- k A.
+// That is 3 fma per PAIR of samples for the residuals plus 2 accumulations per sample
+// (3.5 VALU ops per sample). It is not an approximation: the quadratic is exact, and it is
+// more accurate than rounding x_u first. Every sample still gets its own residual and its
+// own contribution; tests compare every point against IEEE division (<= 2 ulp).
 struct Pi4 {
   static constexpr double kScale = 4.0;
+  static constexpr int kPairs = 16;  // supports tiles of up to 32 samples
+
+  // Pair offsets k = j + 1/2 and k^2, held in SGPRs for the whole kernel (see init()).
+  // Every fma of the pair evaluation is then a 3-operand VOP3 v_fma_f64 with one SGPR
+  // source; folded to literals instead, hipcc emits v_fmac_f64 + literal and has to copy the
+  // shared c with a v_mov_b64 per pair (30 extra VALU per 32-sample tile, measured in the .s).
+  double pk[kPairs], pk2[kPairs];
+
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int j = 0; j < kPairs; ++j) {
+      double k = j + 0.5, k2 = k * k;
+      asm volatile("" : "+s"(k));   // opaque -> stays an SGPR pair, never a literal
+      asm volatile("" : "+s"(k2));
+      pk[j] = k;
+      pk2[j] = k2;
+    }
+  }
 
   __device__ __forceinline__ double point(double x) const { return 1.0 / fma(x, x, 1.0); }
 
+  // Per-tile constants of the series reciprocal (also used by the validation kernel).
+  struct Seed {
+    double s, em, a, b;
+  };
+  __device__ __forceinline__ static Seed seed(double xm, double h) {
+    const double dm = fma(xm, xm, 1.0);
+    double s = __builtin_amdgcn_rcp(dm);
+    s = fma(s, fma(-dm, s, 1.0), s);  // one Newton step
+    return {s, fma(-dm, s, 1.0), (-2.0 * h) * xm * s, -(h * h) * s};
+  }
+
   template <int U, DivMode M>
   __device__ __forceinline__ double tile(double x0, double h) const {
+    static_assert(U % 2 == 0, "pair evaluation needs an even tile");
     if constexpr (M == DivMode::kIeee) {
       double acc = 0.0;
 #pragma unroll
@@ -51,6 +91,22 @@ struct Pi4 {
         acc += 1.0 / fma(x, x, 1.0);
       }
       return acc;
+    } else if constexpr (M == DivMode::kSeries) {
+      const Seed sd = seed(fma(0.5 * (U - 1), h, x0), h);
+      double t1a = 0.0, t1b = 0.0, t2a = 0.0, t2b = 0.0;
+#pragma unroll
+      for (int j = 0; j < U / 2; ++j) {
+        static_assert(U / 2 <= kPairs, "tile larger than the pair table");
+        const double k = pk[j];
+        const double c = fma(pk2[j], sd.b, sd.em);
+        const double ep = fma(k, sd.a, c);         // sample u = U/2 + j
+        const double en = fma(-k, sd.a, c);        // sample u = U/2 - 1 - j
+        t1a += ep;
+        t1b += en;
+        t2a = fma(ep, ep, t2a);
+        t2b = fma(en, en, t2b);
+      }
+      return fma(sd.s, (t1a + t1b) + (t2a + t2b), static_cast<double>(U) * sd.s);
     } else {
       const double xm = fma(0.5 * (U - 1), h, x0);
       const double dm = fma(xm, xm, 1.0);

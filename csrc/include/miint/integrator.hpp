@@ -3,12 +3,16 @@
 // A RiemannPlan owns everything one rank needs to integrate f over [a, b] with n samples:
 // its 64-bit slice of the sample range, the kernel launch shape, device workspace, a ring
 // of result slots, pinned host results, and (optionally) an RCCL communicator for the
-// cross-GPU sum. Work is split in three stream-ordered stages so a driver can pipeline
-// them on separate HIP streams or capture them into a hipGraph:
+// cross-GPU sum. One integration ("step") is three stream-ordered stages:
 //
-//   compute  : Riemann kernel(s) -> this rank's scaled partial in slot k (device)
-//   reduce   : RCCL allreduce of slot k across ranks (xGMI)          [skipped if world==1]
-//   copyout  : 8-byte hipMemcpyAsync of slot k into pinned host memory
+//   compute  : fused Riemann kernel -> this rank's scaled partial (device slot, or, on a
+//              single GPU, straight into mapped pinned host memory: no copy at all)
+//   reduce   : RCCL allreduce of the slot across ranks over xGMI     [world > 1]
+//   copyout  : 8-byte hipMemcpyAsync of the slot into pinned memory  [world > 1]
+//
+// Steps are replayed from hipGraphs that hold a whole batch of `slots` steps (one graph
+// launch per batch; on >1 GPU the batch is a fork/join graph: kernels on the compute stream,
+// allreduce+copy of step k on the comm stream overlapping the kernel of step k+1).
 //
 // Reference mapping: riemann.cpp:47-101 (MPI master/worker) and cintegrate.cu:101-150
 // (CUDA host driver) are both instances of this plan (see csrc/cli/).
@@ -38,9 +42,11 @@ struct RiemannConfig {
   double p0 = 0.0, p1 = 0.0;   // Integrand::kTrainVel (ts, vs)
   std::vector<double> table;   // Integrand::kTable (host copy, uploaded once)
   int grid = 0;                // workgroups; 0 = auto (waves_per_cu per CU)
-  int waves_per_cu = 32;
+  int waves_per_cu = 28;       // 7 x 256-thread workgroups per CU: the pi4 series kernel's
+                               // SGPR-limited residency, so the default grid is one full wave
   bool fused = true;           // one launch (ticket reduction) vs partials + finalize
-  int slots = 4;               // result ring depth for pipelined steps
+  bool host_direct = true;     // world == 1: kernel stores the result into pinned memory
+  int slots = 8;               // steps per graph batch = result ring depth
   int rank = 0, world = 1;     // slice of [0, n) when no communicator is given (e.g. the
                                // torch.distributed path reduces results itself)
 };
@@ -55,7 +61,7 @@ inline void rank_slice(uint64_t n, int r, int w, uint64_t* begin, uint64_t* coun
 
 struct StepTiming {
   double wall_s = 0.0;    // host wall clock around the whole run
-  double device_ms = 0.0; // hipEvent time on the compute stream
+  double device_ms = 0.0; // hipEvent time from first enqueue to last result
   int steps = 0;
 };
 
@@ -76,8 +82,10 @@ class RiemannPlan {
   double scale() const { return scale_; }
   LaunchShape shape() const { return shape_; }
   DivMode effective_div() const;
+  bool direct() const { return direct_; }
 
-  void enqueue_compute(hipStream_t s, int slot) const;
+  // Stage launchers. `slot` selects the device result slot, `host_index` the pinned slot.
+  void enqueue_compute(hipStream_t s, int slot, int host_index) const;
   void enqueue_reduce(hipStream_t s, int slot) const;
   void enqueue_copyout(hipStream_t s, int slot, int host_index) const;
   void enqueue(hipStream_t s, int slot, int host_index) const;
@@ -85,29 +93,38 @@ class RiemannPlan {
   double* device_result(int slot) const { return result_.get() + slot; }
   double host_result(int host_index) const { return host_[host_index]; }
   int host_capacity() const { return static_cast<int>(host_.size()); }
+  int slots() const { return cfg_.slots; }
 
   // One synchronous integration on the plan's own stream; returns the global value.
   double run();
-  // Capture compute(+reduce+copyout) for every slot into hipGraphs.
+  // Capture one batch of `slots` steps into a hipGraph (fork/join over two streams when
+  // world > 1). Done lazily by the step runners.
   void capture_graphs();
-  bool graphs_ready() const { return !graphs_.empty(); }
+  bool graphs_ready() const { return batch_ != nullptr; }
+  size_t graph_nodes() const;
 
-  // Run `steps` complete integrations back to back. With pipeline=true (and world > 1)
-  // step k's allreduce+copyout runs on the comm stream while step k+1 computes; with
-  // graphs=true each stage is a graph replay. Returns when every result is on the host.
+  // Run `steps` complete integrations back to back. graphs=true: whole batches as graph
+  // replays (results of step k in host slot k % slots), remainder enqueued directly.
+  // graphs=false: direct enqueue (result of step k in host slot k % host_capacity); with
+  // pipeline=true and world > 1 the reduce/copy of step k overlaps compute of step k+1.
   StepTiming run_steps(int steps, bool pipeline, bool graphs);
-  // The same without the final synchronisation (bench.py brackets it with its own
-  // barrier + device synchronize); call sync() before reading host results.
+  // The same without synchronisation (bench.py brackets it with its own barrier + device
+  // synchronize); call sync() before reading host results.
   void launch_steps(int steps, bool pipeline, bool graphs);
   void sync() const;
+  // Host slot holding the result of step k of the last launch_steps/run_steps call.
+  int host_index_of(int k, bool graphs) const;
   hipStream_t compute_stream() const { return compute_.get(); }
   hipStream_t comm_stream() const { return comm_stream_.get(); }
 
  private:
+  void enqueue_batch(hipStream_t cs, hipStream_t rs, int nsteps, bool overlap);
+
   RiemannConfig cfg_;
   int device_;
   const Comm* comm_;
   int rank_ = 0, world_ = 1;
+  bool direct_ = false;
   RiemannParams params_{};
   double scale_ = 1.0;
   LaunchShape shape_{1, kRiemannBlock};
@@ -119,9 +136,9 @@ class RiemannPlan {
   Stream compute_;
   Stream comm_stream_;
   std::vector<std::unique_ptr<Event>> ev_computed_, ev_drained_;
+  Event ev_fork_, ev_join_;
   Event ev_t0_, ev_t1_;
-  std::vector<std::unique_ptr<Graph>> graphs_;       // compute graph per slot
-  std::vector<std::unique_ptr<Graph>> comm_graphs_;  // reduce+copyout graph per slot
+  std::unique_ptr<Graph> batch_;  // `slots` steps
 };
 
 }  // namespace miint

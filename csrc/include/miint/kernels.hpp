@@ -23,6 +23,12 @@ constexpr int kRiemannBlock = 256;
 // True when the fp64 Pi4 series reciprocal is exact to fp64 for this h (see integrands.hpp).
 inline bool series_ok(double h) { return 0.5 * kRiemannTile * (h < 0 ? -h : h) <= 2e-6; }
 
+// Division mode actually used for step h: the series paths fall back to IEEE division when
+// the tile span is too coarse for the truncated series to be exact to fp64.
+inline DivMode effective_div(DivMode d, double h) {
+  return (d != DivMode::kIeee && !series_ok(h)) ? DivMode::kIeee : d;
+}
+
 struct LaunchShape {
   int grid;   // workgroups
   int block;  // threads per workgroup

@@ -106,21 +106,32 @@ class DeviceBuffer {
   size_t n_ = 0;
 };
 
-// Page-locked host memory (hipHostMalloc) for async D2H/H2D.
+// Page-locked host memory (hipHostMalloc) for async D2H/H2D. Allocated mapped + coherent
+// (fine-grained), so kernels can also store results straight into it (device_ptr()):
+// a finished kernel's stores are visible to the host after the stream synchronises.
 template <typename T>
 class PinnedBuffer {
  public:
   PinnedBuffer() = default;
   explicit PinnedBuffer(size_t n) : n_(n) {
     if (n) {
-      MIINT_HIP(hipHostMalloc(reinterpret_cast<void**>(&p_), n * sizeof(T), hipHostMallocDefault));
+      MIINT_HIP(hipHostMalloc(reinterpret_cast<void**>(&p_), n * sizeof(T),
+                              hipHostMallocMapped | hipHostMallocPortable |
+                                  hipHostMallocCoherent));
       std::memset(static_cast<void*>(p_), 0, n * sizeof(T));
+      MIINT_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_), p_, 0));
     }
   }
+  T* device_ptr() const { return d_; }
   ~PinnedBuffer() { if (p_) (void)hipHostFree(p_); }
-  PinnedBuffer(PinnedBuffer&& o) noexcept : p_(o.p_), n_(o.n_) { o.p_ = nullptr; o.n_ = 0; }
+  PinnedBuffer(PinnedBuffer&& o) noexcept : p_(o.p_), d_(o.d_), n_(o.n_) {
+    o.p_ = nullptr;
+    o.d_ = nullptr;
+    o.n_ = 0;
+  }
   PinnedBuffer& operator=(PinnedBuffer&& o) noexcept {
     std::swap(p_, o.p_);
+    std::swap(d_, o.d_);
     std::swap(n_, o.n_);
     return *this;
   }
@@ -132,6 +143,7 @@ class PinnedBuffer {
 
  private:
   T* p_ = nullptr;
+  T* d_ = nullptr;
   size_t n_ = 0;
 };
 

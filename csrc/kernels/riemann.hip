@@ -107,7 +107,11 @@ struct Pi4F32 {
 template <class F> struct Maker;
 template <> struct Maker<Pi4> {
   static constexpr int kLds = 1;
-  __device__ static Pi4 make(const RiemannParams&, const double*, int, double*) { return {}; }
+  __device__ static Pi4 make(const RiemannParams&, const double*, int, double*) {
+    Pi4 f;
+    f.init();
+    return f;
+  }
 };
 template <> struct Maker<Pi4F32> {
   static constexpr int kLds = 1;
@@ -150,7 +154,9 @@ __global__ __launch_bounds__(B) void riemann_kernel(RiemannParams p, const doubl
 }
 
 // ---------------------------------------------------------------------------- finalize
-constexpr int kFinalBlock = 1024;
+// Same width and order as the fused kernel's last-workgroup sum (B threads, partial i
+// folded into thread i % B in increasing i), so both paths are bitwise identical.
+constexpr int kFinalBlock = B;
 
 __device__ __forceinline__ double ordered_sum(const double* partials, int n, double* red) {
   double v = 0.0;
@@ -222,13 +228,18 @@ __global__ __launch_bounds__(B) void point_values_kernel(RiemannParams p, const 
   for (int u = 0; u < U && t * U + u < p.n; ++u) {
     const double x = fma(static_cast<double>(u), p.h, x0);
     double v;
-    if constexpr (M == DivMode::kSeries && sizeof(F) == sizeof(Pi4) &&
-                  __is_same(F, Pi4)) {
-      const double dm = fma(xm, xm, 1.0);
-      double s = __builtin_amdgcn_rcp(dm);
-      s = fma(s, fma(-dm, s, 1.0), s);
-      const double e = fma(-fma(x, x, 1.0), s, 1.0);
-      v = fma(s, e + e * e, s);
+    if constexpr (M != DivMode::kIeee && __is_same(F, Pi4)) {
+      const Pi4::Seed sd = Pi4::seed(xm, p.h);
+      double e;
+      if constexpr (M == DivMode::kSeries) {  // exactly the pair evaluation of Pi4::tile
+        const int j = u >= U / 2 ? u - U / 2 : U / 2 - 1 - u;
+        const double k = j + 0.5;
+        const double c = fma(k * k, sd.b, sd.em);
+        e = u >= U / 2 ? fma(k, sd.a, c) : fma(-k, sd.a, c);
+      } else {
+        e = fma(-fma(x, x, 1.0), sd.s, 1.0);
+      }
+      v = fma(sd.s, e + e * e, sd.s);
     } else {
       v = f.point(x);
     }
@@ -256,13 +267,14 @@ void dispatch(const RiemannParams& p, DType dtype, DivMode m, A&&... a) {
   const Integrand f = static_cast<Integrand>(p.integrand);
   if (dtype == DType::kF32) {
     MIINT_CHECK(f == Integrand::kPi4, "fp32 path is implemented for the pi4 integrand");
-    if (m == DivMode::kSeries) Op<DivMode::kSeries, Pi4F32>::run(a...);
-    else Op<DivMode::kIeee, Pi4F32>::run(a...);
+    if (m == DivMode::kIeee) Op<DivMode::kIeee, Pi4F32>::run(a...);
+    else Op<DivMode::kSeries, Pi4F32>::run(a...);
     return;
   }
   switch (f) {
     case Integrand::kPi4:
       if (m == DivMode::kSeries) Op<DivMode::kSeries, Pi4>::run(a...);
+      else if (m == DivMode::kSeriesDirect) Op<DivMode::kSeriesDirect, Pi4>::run(a...);
       else Op<DivMode::kIeee, Pi4>::run(a...);
       return;
     case Integrand::kSin: Op<DivMode::kIeee, Sin>::run(a...); return;
@@ -320,7 +332,7 @@ static void check_params(const RiemannParams& p, const double* table, int table_
 }
 
 static DivMode effective_div(const RiemannParams& p, DivMode div) {
-  return (div == DivMode::kSeries && !series_ok(p.h)) ? DivMode::kIeee : div;
+  return miint::effective_div(div, p.h);
 }
 
 void launch_riemann_partials(const RiemannParams& p, DType dtype, DivMode div, LaunchShape shape,

@@ -58,7 +58,10 @@ PYBIND11_MODULE(_miint, m) {
       .value("table", Integrand::kTable);
   py::enum_<Rule>(m, "Rule").value("left", Rule::kLeft).value("mid", Rule::kMid).value("right", Rule::kRight);
   py::enum_<DType>(m, "DType").value("fp64", DType::kF64).value("fp32", DType::kF32);
-  py::enum_<DivMode>(m, "DivMode").value("series", DivMode::kSeries).value("ieee", DivMode::kIeee);
+  py::enum_<DivMode>(m, "DivMode")
+      .value("series", DivMode::kSeries)
+      .value("ieee", DivMode::kIeee)
+      .value("series_direct", DivMode::kSeriesDirect);
 
   m.attr("RIEMANN_TILE") = kRiemannTile;
   m.attr("RIEMANN_BLOCK") = kRiemannBlock;
@@ -161,6 +164,10 @@ PYBIND11_MODULE(_miint, m) {
            }, py::arg("steps"), py::arg("pipeline") = true, py::arg("graphs") = true)
       .def("host_result", &RiemannPlan::host_result)
       .def_property_readonly("host_capacity", &RiemannPlan::host_capacity)
+      .def_property_readonly("slots", &RiemannPlan::slots)
+      .def_property_readonly("direct", &RiemannPlan::direct)
+      .def_property_readonly("graph_nodes", &RiemannPlan::graph_nodes)
+      .def("host_index_of", &RiemannPlan::host_index_of, py::arg("k"), py::arg("graphs"))
       .def("enqueue", [](const RiemannPlan& p, uintptr_t s, int slot, int hidx) { p.enqueue(stream(s), slot, hidx); })
       .def("device_result", [](const RiemannPlan& p, int slot) { return reinterpret_cast<uintptr_t>(p.device_result(slot)); });
 

@@ -11,7 +11,7 @@ constexpr int kHostRing = 4096;  // pinned result slots for non-graph step loops
 
 RiemannPlan::RiemannPlan(const RiemannConfig& cfg, int device, const Comm* comm)
     : cfg_(cfg), device_(device), comm_(comm), compute_((set_device(device), Stream())),
-      comm_stream_() {
+      comm_stream_(), ev_fork_(false), ev_join_(false) {
   MIINT_CHECK(cfg.n >= 1, "n must be >= 1");
   MIINT_CHECK(cfg.b != cfg.a, "empty interval");
   MIINT_CHECK(cfg.slots >= 1 && cfg.slots <= 64, "slots must be in [1, 64]");
@@ -24,6 +24,9 @@ RiemannPlan::RiemannPlan(const RiemannConfig& cfg, int device, const Comm* comm)
     rank_ = cfg.rank;
     world_ = cfg.world;
   }
+  // Results go straight from the kernel into pinned host memory when nothing has to
+  // happen to them on the device afterwards (no cross-GPU reduction by this plan).
+  direct_ = cfg.host_direct && !(comm_ && world_ > 1);
   DeviceGuard g(device);
   params_.a = cfg.a;
   params_.h = (cfg.b - cfg.a) / static_cast<double>(cfg.n);
@@ -69,12 +72,12 @@ RiemannPlan::~RiemannPlan() {
   (void)hipStreamSynchronize(comm_stream_.get());
 }
 
-DivMode RiemannPlan::effective_div() const {
-  return (cfg_.div == DivMode::kSeries && !series_ok(params_.h)) ? DivMode::kIeee : cfg_.div;
-}
+DivMode RiemannPlan::effective_div() const { return miint::effective_div(cfg_.div, params_.h); }
 
-void RiemannPlan::enqueue_compute(hipStream_t s, int slot) const {
-  double* out = result_.get() + slot;
+size_t RiemannPlan::graph_nodes() const { return batch_ ? batch_->num_nodes() : 0; }
+
+void RiemannPlan::enqueue_compute(hipStream_t s, int slot, int host_index) const {
+  double* out = direct_ ? host_.device_ptr() + host_index : result_.get() + slot;
   const int tn = static_cast<int>(cfg_.table.size());
   if (cfg_.fused) {
     launch_riemann_fused(params_, cfg_.dtype, cfg_.div, shape_, table_.get(), tn,
@@ -94,12 +97,13 @@ void RiemannPlan::enqueue_reduce(hipStream_t s, int slot) const {
 }
 
 void RiemannPlan::enqueue_copyout(hipStream_t s, int slot, int host_index) const {
+  if (direct_) return;  // the kernel already stored into pinned memory
   MIINT_HIP(hipMemcpyAsync(host_.get() + host_index, result_.get() + slot, sizeof(double),
                            hipMemcpyDeviceToHost, s));
 }
 
 void RiemannPlan::enqueue(hipStream_t s, int slot, int host_index) const {
-  enqueue_compute(s, slot);
+  enqueue_compute(s, slot, host_index);
   enqueue_reduce(s, slot);
   enqueue_copyout(s, slot, host_index);
 }
@@ -111,46 +115,69 @@ double RiemannPlan::run() {
   return host_[0];
 }
 
+// Steps j < nsteps use device slot j and host slot j. With overlap (and something to
+// overlap), the reduce+copy chain runs on `rs` behind per-step events: a fork/join that
+// hipStreamBeginCapture turns into graph edges.
+void RiemannPlan::enqueue_batch(hipStream_t cs, hipStream_t rs, int nsteps, bool overlap) {
+  if (!overlap || direct_ || !(comm_ && world_ > 1)) {
+    for (int j = 0; j < nsteps; ++j) enqueue(cs, j, j);
+    return;
+  }
+  ev_fork_.record(cs);
+  MIINT_HIP(hipStreamWaitEvent(rs, ev_fork_.get(), 0));
+  for (int j = 0; j < nsteps; ++j) {
+    enqueue_compute(cs, j, j);
+    ev_computed_[j]->record(cs);
+    MIINT_HIP(hipStreamWaitEvent(rs, ev_computed_[j]->get(), 0));
+    enqueue_reduce(rs, j);
+    enqueue_copyout(rs, j, j);
+  }
+  ev_join_.record(rs);
+  MIINT_HIP(hipStreamWaitEvent(cs, ev_join_.get(), 0));
+}
+
 void RiemannPlan::capture_graphs() {
   DeviceGuard g(device_);
-  graphs_.clear();
-  comm_graphs_.clear();
-  for (int k = 0; k < cfg_.slots; ++k) {
-    std::unique_ptr<Graph> cg(new Graph());
-    cg->capture(compute_.get(), [&](hipStream_t s) { enqueue_compute(s, k); });
-    std::unique_ptr<Graph> rg(new Graph());
-    rg->capture(comm_stream_.get(), [&](hipStream_t s) {
-      enqueue_reduce(s, k);
-      enqueue_copyout(s, k, k);
-    });
-    graphs_.push_back(std::move(cg));
-    comm_graphs_.push_back(std::move(rg));
-  }
+  batch_.reset(new Graph());
+  batch_->capture(compute_.get(), [&](hipStream_t s) {
+    enqueue_batch(s, comm_stream_.get(), cfg_.slots, true);
+  });
+}
+
+int RiemannPlan::host_index_of(int k, bool graphs) const {
+  return graphs ? k % cfg_.slots : k % host_capacity();
 }
 
 void RiemannPlan::launch_steps(int steps, bool pipeline, bool graphs) {
   DeviceGuard g(device_);
-  if (graphs && graphs_.empty()) capture_graphs();
-  const int S = cfg_.slots;
   hipStream_t cs = compute_.get();
-  hipStream_t rs = pipeline ? comm_stream_.get() : cs;
+  hipStream_t rs = comm_stream_.get();
+  const int S = cfg_.slots;
+  if (graphs) {
+    if (!batch_) capture_graphs();
+    for (int b = 0; b < steps / S; ++b) batch_->launch(cs);
+    if (steps % S) enqueue_batch(cs, rs, steps % S, pipeline);
+    return;
+  }
+  const bool overlap = pipeline && !direct_ && comm_ && world_ > 1;
   for (int k = 0; k < steps; ++k) {
     const int slot = k % S;
-    const int hidx = graphs ? slot : k % host_capacity();
-    if (pipeline && k >= S) MIINT_HIP(hipStreamWaitEvent(cs, ev_drained_[slot]->get(), 0));
-    if (graphs) graphs_[slot]->launch(cs);
-    else enqueue_compute(cs, slot);
-    if (pipeline) {
-      ev_computed_[slot]->record(cs);
-      MIINT_HIP(hipStreamWaitEvent(rs, ev_computed_[slot]->get(), 0));
+    const int hidx = k % host_capacity();
+    if (!overlap) {
+      enqueue(cs, slot, hidx);
+      continue;
     }
-    if (graphs) {
-      comm_graphs_[slot]->launch(rs);
-    } else {
-      enqueue_reduce(rs, slot);
-      enqueue_copyout(rs, slot, hidx);
-    }
-    if (pipeline) ev_drained_[slot]->record(rs);
+    if (k >= S) MIINT_HIP(hipStreamWaitEvent(cs, ev_drained_[slot]->get(), 0));
+    enqueue_compute(cs, slot, hidx);
+    ev_computed_[slot]->record(cs);
+    MIINT_HIP(hipStreamWaitEvent(rs, ev_computed_[slot]->get(), 0));
+    enqueue_reduce(rs, slot);
+    enqueue_copyout(rs, slot, hidx);
+    ev_drained_[slot]->record(rs);
+  }
+  if (overlap) {  // leave the compute stream ordered after the last copy
+    ev_join_.record(rs);
+    MIINT_HIP(hipStreamWaitEvent(cs, ev_join_.get(), 0));
   }
 }
 
@@ -162,19 +189,13 @@ void RiemannPlan::sync() const {
 
 StepTiming RiemannPlan::run_steps(int steps, bool pipeline, bool graphs) {
   DeviceGuard g(device_);
-  if (graphs && graphs_.empty()) capture_graphs();
+  if (graphs && !batch_) capture_graphs();
   StepTiming t;
   sync();
   const double w0 = wall_seconds();
   ev_t0_.record(compute_.get());
   launch_steps(steps, pipeline, graphs);
-  if (pipeline) {
-    // join the comm stream back into the compute stream for the end event
-    Event join(false);
-    join.record(comm_stream_.get());
-    MIINT_HIP(hipStreamWaitEvent(compute_.get(), join.get(), 0));
-  }
-  ev_t1_.record(compute_.get());
+  ev_t1_.record(compute_.get());  // every path leaves cs ordered after all of its work
   sync();
   t.wall_s = wall_seconds() - w0;
   t.device_ms = Event::elapsed_ms(ev_t0_, ev_t1_);

@@ -104,7 +104,8 @@ ORACLES = {
     "cintegrate_sp32_sm2": 121999.800663,
     "cintegrate_sp30_sm2": 122000.004000,
     "cintegrate_sp32_sm3": 121823.051337,
-    "trainscan_p1": 122000.004030,
+    "trainscan_p1": 122000.004030,        # includes sequential-sum rounding drift
+    "trainscan_p1_exact": 122000.004000,  # what tree/look-back accumulation prints
     "trainscan_p7": 0.0,
     "trainscan_p16": 117642.707174,
     "train_analytic_1800": 121999.99983,

@@ -178,7 +178,9 @@ def test_interp_scan_matches_fill_then_scan(cuda):
     fused = kernels.interp_scan(n)
     two = torch.cumsum(kernels.interp_fill(n), 0)
     torch.testing.assert_close(fused, two, rtol=1e-11, atol=1e-6)
-    assert float(fused[-2].item()) / 1e4 == pytest.approx(122000.004030, abs=2e-6)
+    # Tree/look-back accumulation lands on the exact knot-sampled value 122000.004000; the
+    # reference's sequential running sum prints ...004030 (3e-5 of fp64 rounding drift).
+    assert float(fused[-1].item()) / 1e4 == pytest.approx(122000.004000, abs=1e-6)
 
 
 def test_table2d_separable_oracle(cuda):

@@ -38,11 +38,17 @@ def parse() -> argparse.Namespace:
     p.add_argument("--rule", default="left", choices=["left", "mid", "right"])
     p.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
     p.add_argument("--div", default="series", choices=["series", "ieee", "series_direct"])
-    p.add_argument("--comm", default="native", choices=["native", "torch"])
+    p.add_argument("--comm", default="native", choices=["native", "torch"],
+                   help="native: C++ RCCL communicator captured in the step graph; "
+                        "torch: torch.distributed all_reduce of each step's partial")
+    p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                   help="process-group backend (gloo only for functional tests on shared GPUs)")
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--no-pipeline", action="store_true")
     p.add_argument("--unfused", action="store_true", help="partials + finalize (2 launches)")
     p.add_argument("--grid", type=int, default=0)
+    p.add_argument("--force-collective", action="store_true",
+                   help="run the RCCL all-reduce stage even on 1 GPU (tests the multi-GPU graph)")
     p.add_argument("--verbose", action="store_true")
     return p.parse_args()
 
@@ -61,41 +67,61 @@ def main() -> int:
             print(f"bench.py: --gpus {args.gpus} needs torchrun with {args.gpus} processes",
                   file=sys.stderr)
             return 2
-    ctx = mdist.init(backend="nccl")
+    if args.backend == "gloo" and args.comm == "native" and world_env > 1:
+        print("bench.py: --backend gloo shares GPUs between ranks; use --comm torch", file=sys.stderr)
+        return 2
+    ctx = mdist.init(backend=args.backend)
     world = ctx.world
     n_per = int(args.n)
     n_total = n_per * world if args.scaling == "weak" else n_per
 
+    use_torch = args.comm == "torch" and world > 1
     integ = Integrator(args.integrand, n=n_total, rule=args.rule, dtype=args.dtype, div=args.div,
                        backend="hip", ctx=ctx, comm=args.comm, fused=not args.unfused,
-                       grid=args.grid)
+                       grid=args.grid, force_collective=args.force_collective)
     plan = integ.plan
-    graphs = not args.no_graph
-    pipeline = not args.no_pipeline and world > 1
+    graphs = not args.no_graph and not use_torch
+    pipeline = not args.no_pipeline and (world > 1 or args.force_collective)
+
+    if use_torch:  # kernels on the torch stream + torch.distributed all_reduce per step
+        from cuda_v_mpi_amd.parallel.torch_steps import TorchStepper
+
+        stepper = TorchStepper(integ.spec, n_total, ctx, rule=args.rule, dtype=args.dtype,
+                               div=args.div, grid=args.grid or None)
+        launch, finish, result = stepper.launch_steps, stepper.sync, stepper.result
+    else:
+        launch = lambda k: plan.launch_steps(k, pipeline, graphs)  # noqa: E731
+        finish = plan.sync
+        result = lambda k: plan.host_result(plan.host_index_of(k, graphs))  # noqa: E731
 
     # ---- warmup (includes graph capture and RCCL channel setup)
-    plan.run_steps(max(1, args.warmup), pipeline, graphs)
+    launch(max(1, args.warmup))
+    finish()
+    if graphs and not plan.graphs_ready:
+        print(f"bench.py: hipGraph capture failed ({plan.graph_error}); "
+              "running with direct stream enqueue", file=sys.stderr)
+        graphs = False
 
     # ---- timed region: barrier + device sync on both sides, K steps in between
     ctx.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    plan.launch_steps(args.steps, pipeline, graphs)
-    plan.sync()
+    launch(args.steps)
+    finish()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     ctx.barrier()
     elapsed = t1 - t0
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t = torch.tensor([elapsed], dtype=torch.float64,
+                     device="cuda" if ctx.backend == "nccl" else "cpu")
+    ctx.all_reduce_max(t)
     elapsed_max = float(t.item())
 
-    # ---- verify every result still in the host ring (graphs: slot ring of 4)
+    # ---- verify the results of the last steps (every rank holds the global value)
     analytic = integ.spec.analytic()
     last = range(max(0, args.steps - min(args.steps, plan.slots)), args.steps)
-    vals = [plan.host_result(plan.host_index_of(k, graphs)) for k in last]
+    vals = [result(k) for k in last]
     errs = [abs(v - analytic) for v in vals]
     abs_err = max(errs)
     # left rule truncation for 4/(1+x^2) is exactly h; anything far above is a bug
@@ -131,8 +157,9 @@ def main() -> int:
                 "global_batch": n_total,
                 "seq_len": 1,
                 "parallelism": f"dp{world}",
-                "comm": args.comm if world > 1 else "none",
+                "comm": args.comm if (world > 1 or args.force_collective) else "none",
                 "graphs": graphs,
+                "graph_nodes": plan.graph_nodes if graphs else 0,
                 "pipeline": pipeline,
                 "fused_reduction": not args.unfused,
                 "grid": plan.grid,

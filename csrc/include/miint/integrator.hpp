@@ -22,6 +22,7 @@
 
 #include <cstdint>
 #include <memory>
+#include <string>
 #include <vector>
 
 #include "miint/comm.hpp"
@@ -49,6 +50,8 @@ struct RiemannConfig {
   int slots = 8;               // steps per graph batch = result ring depth
   int rank = 0, world = 1;     // slice of [0, n) when no communicator is given (e.g. the
                                // torch.distributed path reduces results itself)
+  bool force_collective = false;  // run the RCCL stage even with a 1-rank communicator
+                                  // (exercises the multi-GPU graph path on one GPU)
 };
 
 // Balanced 64-bit slice of [0, n) for rank r of w: first (n % w) ranks get one extra.
@@ -101,6 +104,8 @@ class RiemannPlan {
   // world > 1). Done lazily by the step runners.
   void capture_graphs();
   bool graphs_ready() const { return batch_ != nullptr; }
+  // Non-empty if graph capture failed (the plan then enqueues directly).
+  const std::string& graph_error() const { return graph_error_; }
   size_t graph_nodes() const;
 
   // Run `steps` complete integrations back to back. graphs=true: whole batches as graph
@@ -117,8 +122,12 @@ class RiemannPlan {
   hipStream_t compute_stream() const { return compute_.get(); }
   hipStream_t comm_stream() const { return comm_stream_.get(); }
 
+  // True when this plan runs an RCCL reduction per step.
+  bool collective() const { return comm_ && (world_ > 1 || cfg_.force_collective); }
+
  private:
   void enqueue_batch(hipStream_t cs, hipStream_t rs, int nsteps, bool overlap);
+  bool use_graphs(bool requested);
 
   RiemannConfig cfg_;
   int device_;
@@ -139,6 +148,7 @@ class RiemannPlan {
   Event ev_fork_, ev_join_;
   Event ev_t0_, ev_t1_;
   std::unique_ptr<Graph> batch_;  // `slots` steps
+  std::string graph_error_;
 };
 
 }  // namespace miint

@@ -128,7 +128,9 @@ PYBIND11_MODULE(_miint, m) {
       .def_readwrite("fused", &RiemannConfig::fused)
       .def_readwrite("slots", &RiemannConfig::slots)
       .def_readwrite("rank", &RiemannConfig::rank)
-      .def_readwrite("world", &RiemannConfig::world);
+      .def_readwrite("world", &RiemannConfig::world)
+      .def_readwrite("force_collective", &RiemannConfig::force_collective)
+      .def_readwrite("host_direct", &RiemannConfig::host_direct);
 
   py::class_<RiemannPlan>(m, "RiemannPlan")
       .def(py::init<const RiemannConfig&, int, const Comm*>(), py::arg("config"),
@@ -167,6 +169,9 @@ PYBIND11_MODULE(_miint, m) {
       .def_property_readonly("slots", &RiemannPlan::slots)
       .def_property_readonly("direct", &RiemannPlan::direct)
       .def_property_readonly("graph_nodes", &RiemannPlan::graph_nodes)
+      .def_property_readonly("graphs_ready", &RiemannPlan::graphs_ready)
+      .def_property_readonly("graph_error", &RiemannPlan::graph_error)
+      .def_property_readonly("collective", &RiemannPlan::collective)
       .def("host_index_of", &RiemannPlan::host_index_of, py::arg("k"), py::arg("graphs"))
       .def("enqueue", [](const RiemannPlan& p, uintptr_t s, int slot, int hidx) { p.enqueue(stream(s), slot, hidx); })
       .def("device_result", [](const RiemannPlan& p, int slot) { return reinterpret_cast<uintptr_t>(p.device_result(slot)); });

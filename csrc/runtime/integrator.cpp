@@ -26,7 +26,7 @@ RiemannPlan::RiemannPlan(const RiemannConfig& cfg, int device, const Comm* comm)
   }
   // Results go straight from the kernel into pinned host memory when nothing has to
   // happen to them on the device afterwards (no cross-GPU reduction by this plan).
-  direct_ = cfg.host_direct && !(comm_ && world_ > 1);
+  direct_ = cfg.host_direct && !(comm_ && (world_ > 1 || cfg.force_collective));
   DeviceGuard g(device);
   params_.a = cfg.a;
   params_.h = (cfg.b - cfg.a) / static_cast<double>(cfg.n);
@@ -90,7 +90,7 @@ void RiemannPlan::enqueue_compute(hipStream_t s, int slot, int host_index) const
 }
 
 void RiemannPlan::enqueue_reduce(hipStream_t s, int slot) const {
-  if (comm_ && world_ > 1) {  // without a native comm the caller reduces (torch path)
+  if (collective()) {  // without a native comm the caller reduces (torch path)
     double* v = result_.get() + slot;
     comm_->allreduce_sum(v, v, 1, s);
   }
@@ -119,7 +119,7 @@ double RiemannPlan::run() {
 // overlap), the reduce+copy chain runs on `rs` behind per-step events: a fork/join that
 // hipStreamBeginCapture turns into graph edges.
 void RiemannPlan::enqueue_batch(hipStream_t cs, hipStream_t rs, int nsteps, bool overlap) {
-  if (!overlap || direct_ || !(comm_ && world_ > 1)) {
+  if (!overlap || direct_ || !collective()) {
     for (int j = 0; j < nsteps; ++j) enqueue(cs, j, j);
     return;
   }
@@ -139,13 +139,28 @@ void RiemannPlan::enqueue_batch(hipStream_t cs, hipStream_t rs, int nsteps, bool
 void RiemannPlan::capture_graphs() {
   DeviceGuard g(device_);
   batch_.reset(new Graph());
-  batch_->capture(compute_.get(), [&](hipStream_t s) {
-    enqueue_batch(s, comm_stream_.get(), cfg_.slots, true);
-  });
+  try {
+    batch_->capture(compute_.get(), [&](hipStream_t s) {
+      enqueue_batch(s, comm_stream_.get(), cfg_.slots, true);
+    });
+  } catch (const Error& e) {
+    // e.g. a collective that cannot be captured on this RCCL build: keep running with
+    // direct stream enqueue (same results, more launch overhead) and say why.
+    batch_.reset();
+    graph_error_ = e.what();
+    (void)hipGetLastError();
+    (void)hipStreamSynchronize(compute_.get());
+    (void)hipStreamSynchronize(comm_stream_.get());
+  }
+}
+
+bool RiemannPlan::use_graphs(bool requested) {
+  if (requested && !batch_ && graph_error_.empty()) capture_graphs();
+  return requested && batch_ != nullptr;
 }
 
 int RiemannPlan::host_index_of(int k, bool graphs) const {
-  return graphs ? k % cfg_.slots : k % host_capacity();
+  return (graphs && batch_) ? k % cfg_.slots : k % host_capacity();
 }
 
 void RiemannPlan::launch_steps(int steps, bool pipeline, bool graphs) {
@@ -153,13 +168,12 @@ void RiemannPlan::launch_steps(int steps, bool pipeline, bool graphs) {
   hipStream_t cs = compute_.get();
   hipStream_t rs = comm_stream_.get();
   const int S = cfg_.slots;
-  if (graphs) {
-    if (!batch_) capture_graphs();
+  if (use_graphs(graphs)) {
     for (int b = 0; b < steps / S; ++b) batch_->launch(cs);
     if (steps % S) enqueue_batch(cs, rs, steps % S, pipeline);
     return;
   }
-  const bool overlap = pipeline && !direct_ && comm_ && world_ > 1;
+  const bool overlap = pipeline && !direct_ && collective();
   for (int k = 0; k < steps; ++k) {
     const int slot = k % S;
     const int hidx = k % host_capacity();
@@ -189,7 +203,7 @@ void RiemannPlan::sync() const {
 
 StepTiming RiemannPlan::run_steps(int steps, bool pipeline, bool graphs) {
   DeviceGuard g(device_);
-  if (graphs && !batch_) capture_graphs();
+  use_graphs(graphs);
   StepTiming t;
   sync();
   const double w0 = wall_seconds();

@@ -61,8 +61,8 @@ class Integrator:
     def __init__(self, integrand: str | integrands.IntegrandSpec = "pi4", n: int = 10**9,
                  rule: str = "left", dtype: str = "fp64", div: str = "series",
                  backend: str = "hip", ctx: DistContext | None = None, comm: str = "native",
-                 fused: bool = True, grid: int = 0, slots: int = 4, a: float | None = None,
-                 b: float | None = None, **spec_kw):
+                 fused: bool = True, grid: int = 0, slots: int = 8, a: float | None = None,
+                 b: float | None = None, force_collective: bool = False, **spec_kw):
         spec = integrands.get(integrand, **spec_kw) if isinstance(integrand, str) else integrand
         if a is not None or b is not None:
             spec = dataclasses.replace(spec, a=spec.a if a is None else a,
@@ -95,7 +95,8 @@ class Integrator:
             cfg.p0, cfg.p1 = spec.p0, spec.p1
             cfg.table = spec.native_table()
             cfg.grid, cfg.fused, cfg.slots = grid, fused, slots
-            if self.ctx.world > 1 and comm == "native":
+            cfg.force_collective = force_collective
+            if (self.ctx.world > 1 or force_collective) and comm == "native":
                 self._comm = native_comm(self.ctx)
                 self._plan = m.RiemannPlan(cfg, self.ctx.device, self._comm)
             else:

@@ -80,6 +80,10 @@ def init(backend: str | None = None, timeout_s: float = 300.0, force: bool = Fal
     if backend == "nccl":
         ctx.device = local
         torch.cuda.set_device(local)
+    elif torch.cuda.is_available():
+        # gloo process group with GPU compute: ranks may share devices (testing on 1 GPU)
+        ctx.device = local % torch.cuda.device_count()
+        torch.cuda.set_device(ctx.device)
     if world > 1 or force:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29531")

@@ -32,6 +32,22 @@ def test_plan_steps_graph_and_plain_agree(cuda, graphs, fused):
     assert it.plan.host_result(it.plan.host_index_of(8, graphs)) == one
 
 
+@pytest.mark.parametrize("graphs", [False, True])
+def test_plan_rccl_stage_on_one_gpu(cuda, graphs):
+    """The multi-GPU step (kernel -> RCCL allreduce on the comm stream -> memcpy to pinned,
+    fork/join-captured in a graph) run with a 1-rank communicator."""
+    base = Integrator("pi4", n=10**8, rule="mid")
+    want = base.run().value
+    it = Integrator("pi4", n=10**8, rule="mid", force_collective=True)
+    assert it.plan.collective and not it.plan.direct
+    t = it.run_steps(19, pipeline=True, graphs=graphs)
+    assert t["steps"] == 19
+    if graphs:
+        assert it.plan.graphs_ready, it.plan.graph_error
+    for k in range(11, 19):
+        assert it.plan.host_result(it.plan.host_index_of(k, graphs)) == want
+
+
 def native_serial_pi4_left(n):
     from cuda_v_mpi_amd import native
     m = native()
@@ -111,6 +127,42 @@ def test_cli_selfcheck(cli_built):
     p = _run([os.path.join(cli_built, "miint"), "selfcheck"])
     assert p.returncode == 0, p.stdout + p.stderr
     assert "SELFCHECK OK" in p.stdout
+
+
+def _torchrun(nproc, args, timeout=300):
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    return _run(["python", "-m", "torch.distributed.run", "--nnodes=1",
+                 f"--nproc-per-node={nproc}", "--master-addr", "127.0.0.1",
+                 "--master-port", str(port)] + args, timeout=timeout)
+
+
+def test_bench_torchrun_single_rank(native, cuda):
+    p = _torchrun(1, [os.path.join(REPO, "bench.py"), "--gpus", "1", "--steps", "16",
+                      "--warmup", "2"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    js = json.loads(p.stdout.strip().splitlines()[-1])
+    assert js["verified"] and js["n_gpus"] == 1
+
+
+def test_bench_two_ranks_shared_gpu_torch_comm(native, cuda):
+    """Two processes on one GPU: rank slicing + torch.distributed (gloo) all_reduce of the
+    per-rank kernel partials; weak scaling doubles N."""
+    p = _torchrun(2, [os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                      "--comm", "torch", "--steps", "12", "--warmup", "2", "--n", "2e8"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    js = json.loads(p.stdout.strip().splitlines()[-1])
+    assert js["n_gpus"] == 2 and js["config"]["N"] == 400_000_000 and js["verified"]
+
+
+def test_bench_force_collective_graph(native, cuda):
+    p = _run(["python", os.path.join(REPO, "bench.py"), "--steps", "24", "--warmup", "8",
+              "--force-collective"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    js = json.loads(p.stdout.strip().splitlines()[-1])
+    assert js["verified"] and js["config"]["graphs"] and js["config"]["pipeline"]
 
 
 def test_bench_contract(native, cuda):

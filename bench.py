@@ -32,7 +32,9 @@ def parse() -> argparse.Namespace:
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=400)
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--n", type=float, default=1e9, help="samples per GPU (weak) or total (strong)")
+    # (--n is a prefix of torchrun's own --nnodes/--nproc-per-node: use --samples under torchrun)
+    p.add_argument("--samples", "--n", dest="n", type=float, default=1e9,
+                   help="samples per GPU (weak) or total (strong)")
     p.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     p.add_argument("--integrand", default="pi4")
     p.add_argument("--rule", default="left", choices=["left", "mid", "right"])

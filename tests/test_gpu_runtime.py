@@ -151,7 +151,7 @@ def test_bench_two_ranks_shared_gpu_torch_comm(native, cuda):
     """Two processes on one GPU: rank slicing + torch.distributed (gloo) all_reduce of the
     per-rank kernel partials; weak scaling doubles N."""
     p = _torchrun(2, [os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo",
-                      "--comm", "torch", "--steps", "12", "--warmup", "2", "--n", "2e8"])
+                      "--comm", "torch", "--steps", "12", "--warmup", "2", "--samples", "2e8"])
     assert p.returncode == 0, p.stderr[-3000:]
     js = json.loads(p.stdout.strip().splitlines()[-1])
     assert js["n_gpus"] == 2 and js["config"]["N"] == 400_000_000 and js["verified"]

@@ -1,0 +1,34 @@
+#!/usr/bin/env bash
+# Collect rocprofv3 PMC counters for the hot kernels, one counter group per run
+# (--pmc with --kernel-trace only; never combined with sys/runtime traces).
+# Output: gpurun_out/pmc/<workload>_<group>/... ; summarise with tools/summarize_counters.py
+set -euo pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+REPO=$(pwd)
+OUT=$REPO/gpurun_out/pmc
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+
+G1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_TRANS_F64 GRBM_GUI_ACTIVE"
+G2="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU_MUL_F64 SQ_THREAD_CYCLES_VALU"
+G3="FETCH_SIZE GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"
+G4="WRITE_SIZE GRBM_GUI_ACTIVE SQ_LDS_UNALIGNED_STALL SQ_INSTS_FLAT"
+
+run() {  # name, group-name, counters, command...
+  local name=$1 gname=$2 ctrs=$3; shift 3
+  timeout -k 10 300 rocprofv3 --pmc $ctrs --kernel-trace --output-format csv \
+    -d "$OUT/${name}_${gname}" -o run -- "$@" > "$OUT/${name}_${gname}.log" 2>&1
+}
+
+for g in G1 G2; do
+  run pi4_series $g "${!g}" "$REPO/build/bin/miint" bench --iters 20
+  run pi4_ieee $g "${!g}" "$REPO/build/bin/miint" bench --iters 10 --div ieee
+  run pi4_fp32 $g "${!g}" "$REPO/build/bin/miint" bench --iters 20 --dtype fp32
+  run sin $g "${!g}" "$REPO/build/bin/miint" bench --iters 4 --integrand sin
+  run dpp_selftest $g "${!g}" python3 "$REPO/tools/dpp_probe.py"
+done
+for g in G1 G2 G3 G4; do
+  run trainscan $g "${!g}" "$REPO/build/bin/trainscan"
+  run materialize $g "${!g}" "$REPO/build/bin/cintegrate" --materialize
+done
+echo "pmc done"

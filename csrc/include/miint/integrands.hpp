@@ -23,6 +23,20 @@
 
 namespace miint {
 
+// Default tile hooks (CRTP). The lane loop calls
+//   acc = f.tile_acc<U, M>(fma(i_anchor, h, a), h, acc)
+// where i_anchor = first sample index of the tile + anchor<U, M>(): integrands whose hot
+// path is centred on the tile (Pi4 series) ask for the midpoint directly, saving an fma.
+template <class D>
+struct TileDefaults {
+  template <int U, DivMode M>
+  __device__ static constexpr double anchor() { return 0.0; }
+  template <int U, DivMode M>
+  __device__ __forceinline__ double tile_acc(double x0, double h, double acc) const {
+    return acc + static_cast<const D*>(this)->template tile<U, M>(x0, h);
+  }
+};
+
 // ------------------------------------------------------------------ 4/(1+x^2), fp64
 //
 // Division is the whole cost of this integrand. The IEEE path (DivMode::kIeee) lets the
@@ -46,24 +60,22 @@ namespace miint {
 // (3.5 VALU ops per sample). It is not an approximation: the quadratic is exact, and it is
 // more accurate than rounding x_u first. Every sample still gets its own residual and its
 // own contribution; tests compare every point against IEEE division (<= 2 ulp).
-struct Pi4 {
+struct Pi4 : TileDefaults<Pi4> {
   static constexpr double kScale = 4.0;
   static constexpr int kPairs = 16;  // supports tiles of up to 32 samples
 
-  // Pair offsets k = j + 1/2 and k^2, held in SGPRs for the whole kernel (see init()).
+  // Pair offsets k = j + 1/2, held in SGPRs for the whole kernel (see init()).
   // Every fma of the pair evaluation is then a 3-operand VOP3 v_fma_f64 with one SGPR
   // source; folded to literals instead, hipcc emits v_fmac_f64 + literal and has to copy the
   // shared c with a v_mov_b64 per pair (30 extra VALU per 32-sample tile, measured in the .s).
-  double pk[kPairs], pk2[kPairs];
+  double pk[kPairs];
 
   __device__ __forceinline__ void init() {
 #pragma unroll
     for (int j = 0; j < kPairs; ++j) {
-      double k = j + 0.5, k2 = k * k;
+      double k = j + 0.5;
       asm volatile("" : "+s"(k));   // opaque -> stays an SGPR pair, never a literal
-      asm volatile("" : "+s"(k2));
       pk[j] = k;
-      pk2[j] = k2;
     }
   }
 
@@ -92,21 +104,7 @@ struct Pi4 {
       }
       return acc;
     } else if constexpr (M == DivMode::kSeries) {
-      const Seed sd = seed(fma(0.5 * (U - 1), h, x0), h);
-      double t1a = 0.0, t1b = 0.0, t2a = 0.0, t2b = 0.0;
-#pragma unroll
-      for (int j = 0; j < U / 2; ++j) {
-        static_assert(U / 2 <= kPairs, "tile larger than the pair table");
-        const double k = pk[j];
-        const double c = fma(pk2[j], sd.b, sd.em);
-        const double ep = fma(k, sd.a, c);         // sample u = U/2 + j
-        const double en = fma(-k, sd.a, c);        // sample u = U/2 - 1 - j
-        t1a += ep;
-        t1b += en;
-        t2a = fma(ep, ep, t2a);
-        t2b = fma(en, en, t2b);
-      }
-      return fma(sd.s, (t1a + t1b) + (t2a + t2b), static_cast<double>(U) * sd.s);
+      return tile_acc<U, M>(fma(0.5 * (U - 1), h, x0), h, 0.0);
     } else {
       const double xm = fma(0.5 * (U - 1), h, x0);
       const double dm = fma(xm, xm, 1.0);
@@ -128,10 +126,47 @@ struct Pi4 {
       return fma(s, (t1a + t1b) + t2, static_cast<double>(U) * s);
     }
   }
+
+  // Hot path of the default kSeries mode: anchored at the tile midpoint x_m, one running
+  // sum per side (e and e^2 folded into the same accumulator), and the tile's
+  // s*(U + sum(e + e^2)) folded into the lane accumulator with a single fma.
+  // Per 32-sample tile: 16 x 7 pair ops + ~12 seed/fold ops.
+  template <int U, DivMode M>
+  __device__ static constexpr double anchor() {
+    return M == DivMode::kSeries ? 0.5 * (U - 1) : 0.0;
+  }
+  template <int U, DivMode M>
+  __device__ __forceinline__ double tile_acc(double xa, double h, double acc) const {
+    if constexpr (M == DivMode::kSeries) {
+      const Seed sd = seed(xa, h);
+      double ta = 0.0, tb = 0.0;
+      // c_j = e_m + k_j^2 B advanced by the exact integer step k_{j+1}^2 - k_j^2 = 2j + 2
+      // (a literal operand of an in-place v_fmac: c_j is dead once e_{+-k_j} are formed),
+      // so only k_j needs an SGPR pair: 32 SGPRs instead of 64 keeps the kernel at 7
+      // resident workgroups per CU. The recurrence's rounding (|c| ~ 1e-8, 15 steps) stays
+      // below 1e-22 absolute.
+      double c = fma(0.25, sd.b, sd.em);
+#pragma unroll
+      for (int j = 0; j < U / 2; ++j) {
+        static_assert(U / 2 <= kPairs, "tile larger than the pair table");
+        const double k = pk[j];
+        const double ep = fma(k, sd.a, c);   // sample u = U/2 + j
+        const double en = fma(-k, sd.a, c);  // sample u = U/2 - 1 - j
+        ta += ep;
+        ta = fma(ep, ep, ta);
+        tb += en;
+        tb = fma(en, en, tb);
+        if (j + 1 < U / 2) c = fma(static_cast<double>(2 * j + 2), sd.b, c);
+      }
+      return fma(sd.s, (ta + tb) + static_cast<double>(U), acc);
+    } else {
+      return acc + tile<U, M>(xa, h);
+    }
+  }
 };
 
 // ------------------------------------------------------------------ sin(x), fp64
-struct Sin {
+struct Sin : TileDefaults<Sin> {
   static constexpr double kScale = 1.0;
   __device__ __forceinline__ double point(double x) const { return sin(x); }
   template <int U, DivMode>
@@ -149,7 +184,7 @@ struct Sin {
 };
 
 // ------------------------------------------------------------------ polynomial
-struct Poly {
+struct Poly : TileDefaults<Poly> {
   static constexpr double kScale = 1.0;
   const double* c;  // points into the kernarg block (uniform -> SGPR loads)
   int n;
@@ -170,7 +205,7 @@ struct Poly {
 // ------------------------------------------------------------------ analytic train velocity
 // v(t) = (1 - cos(t/ts)) * vs   (riemann.cpp:108-111). Integral over [0,1800] is
 // dis_function(1800) = vs*(1800 - ts*sin(1800/ts)) ~= 121999.99983.
-struct TrainVel {
+struct TrainVel : TileDefaults<TrainVel> {
   double inv_ts, vs;
   static constexpr double kScale = 1.0;
   __device__ __forceinline__ double point(double t) const {
@@ -192,7 +227,7 @@ struct TrainVel {
 // The 1801-sample table (14.4 KB) lives in LDS, loaded once per workgroup. Segment index is
 // clamped to [0, nseg-1] so t == 1800 interpolates the last segment instead of reading
 // past the end (the reference copies only 1800 of 1801 entries: cintegrate.cu:117,121).
-struct Table {
+struct Table : TileDefaults<Table> {
   const double* lds;  // LDS copy of the table
   int nseg;           // number of segments = entries - 1
   static constexpr double kScale = 1.0;

@@ -43,8 +43,8 @@ struct RiemannConfig {
   double p0 = 0.0, p1 = 0.0;   // Integrand::kTrainVel (ts, vs)
   std::vector<double> table;   // Integrand::kTable (host copy, uploaded once)
   int grid = 0;                // workgroups; 0 = auto (waves_per_cu per CU)
-  int waves_per_cu = 28;       // 7 x 256-thread workgroups per CU: the pi4 series kernel's
-                               // SGPR-limited residency, so the default grid is one full wave
+  int waves_per_cu = 32;       // 8 x 256-thread workgroups per CU (the pi4 series kernel
+                               // keeps <= 80 SGPRs for this): the default grid is one full wave
   bool fused = true;           // one launch (ticket reduction) vs partials + finalize
   bool host_direct = true;     // world == 1: kernel stores the result into pinned memory
   int slots = 8;               // steps per graph batch = result ring depth

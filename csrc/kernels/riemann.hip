@@ -29,20 +29,34 @@ namespace {
 constexpr int U = kRiemannTile;
 constexpr int B = kRiemannBlock;
 
+// Wave-uniform 64-bit value read from one lane (two 32-bit v_readlane).
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
+  const uint32_t lo = __builtin_amdgcn_readlane(static_cast<uint32_t>(v), lane);
+  const uint32_t hi = __builtin_amdgcn_readlane(static_cast<uint32_t>(v >> 32), lane);
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
 // Accumulate f over this launch's samples [p.i_begin, p.i_begin + p.n) into a per-lane sum.
-// The tile's first index is carried as an exact double (integers < 2^53 are exact), so the
-// loop pays one v_add_f64 per tile instead of a u64->f64 conversion.
+//  * Lane g owns tiles g, g+L, g+2L, ... (L = all lanes of the grid). Consecutive lanes of a
+//    wave differ by at most one round, so the loop runs a wave-uniform round count (SALU
+//    counter, no per-tile VALU compare) and only one extra round is exec-masked.
+//  * The tile's anchor index is carried as an exact double (integers < 2^53 are exact), so
+//    a round costs one v_add_f64 + one v_fma_f64 for its coordinate.
 template <DivMode M, class F>
 __device__ __forceinline__ double lane_sum(const RiemannParams& p, const F& f) {
   const uint64_t lanes = static_cast<uint64_t>(gridDim.x) * B;
   const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * B + threadIdx.x;
   const uint64_t ntile = p.n / U;
+  const uint64_t rounds = gid < ntile ? (ntile - 1 - gid) / lanes + 1 : 0;
+  const uint64_t r_all = readlane_u64(rounds, kWave - 1);  // lane 63 has the fewest rounds
+  const uint64_t r_any = readlane_u64(rounds, 0);          // lane 0 the most (<= r_all + 1)
   const double base = static_cast<double>(p.i_begin) + p.off;
   const double istep = static_cast<double>(lanes * U);
-  double ib = base + static_cast<double>(gid * U);
+  double ib = base + static_cast<double>(gid * U) + F::template anchor<U, M>();
   double acc = 0.0;
-  for (uint64_t t = gid; t < ntile; t += lanes, ib += istep)
-    acc += f.template tile<U, M>(fma(ib, p.h, p.a), p.h);
+  uint64_t r = 0;
+  for (; r < r_all; ++r, ib += istep) acc = f.template tile_acc<U, M>(fma(ib, p.h, p.a), p.h, acc);
+  if (r < r_any && r < rounds) acc = f.template tile_acc<U, M>(fma(ib, p.h, p.a), p.h, acc);
   const uint64_t done = ntile * U;
   if (gid < p.n - done) acc += f.point(fma(base + static_cast<double>(done + gid), p.h, p.a));
   return acc;
@@ -60,7 +74,7 @@ __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) {
 // 4/(1+x^2) in packed fp32 (v_pk_fma_f32 pairs). Tile base comes in as fp64 so sample
 // coordinates do not collapse at 1e9 samples; in-tile offsets and all
 // per-point math are fp32. Series division as in Pi4 (first order suffices: e^2 < 2^-24).
-struct Pi4F32 {
+struct Pi4F32 : TileDefaults<Pi4F32> {
   static constexpr double kScale = 4.0;
   __device__ __forceinline__ double point(double xd) const {
     const float x = static_cast<float>(xd);
@@ -124,13 +138,13 @@ template <> struct Maker<Sin> {
 template <> struct Maker<Poly> {
   static constexpr int kLds = 1;
   __device__ static Poly make(const RiemannParams& p, const double*, int, double*) {
-    return {p.coef, p.ncoef};
+    return {{}, p.coef, p.ncoef};
   }
 };
 template <> struct Maker<TrainVel> {
   static constexpr int kLds = 1;
   __device__ static TrainVel make(const RiemannParams& p, const double*, int, double*) {
-    return {1.0 / p.p0, p.p1};
+    return {{}, 1.0 / p.p0, p.p1};
   }
 };
 template <> struct Maker<Table> {
@@ -138,7 +152,7 @@ template <> struct Maker<Table> {
   __device__ static Table make(const RiemannParams&, const double* table, int n, double* lds) {
     for (int i = threadIdx.x; i < n; i += B) lds[i] = table[i];  // 14.4 KB, once per block
     __syncthreads();
-    return {lds, n - 1};
+    return {{}, lds, n - 1};
   }
 };
 
@@ -231,10 +245,11 @@ __global__ __launch_bounds__(B) void point_values_kernel(RiemannParams p, const 
     if constexpr (M != DivMode::kIeee && __is_same(F, Pi4)) {
       const Pi4::Seed sd = Pi4::seed(xm, p.h);
       double e;
-      if constexpr (M == DivMode::kSeries) {  // exactly the pair evaluation of Pi4::tile
+      if constexpr (M == DivMode::kSeries) {  // exactly the pair evaluation of Pi4::tile_acc
         const int j = u >= U / 2 ? u - U / 2 : U / 2 - 1 - u;
         const double k = j + 0.5;
-        const double c = fma(k * k, sd.b, sd.em);
+        double c = fma(0.25, sd.b, sd.em);
+        for (int q = 0; q < j; ++q) c = fma(static_cast<double>(2 * q + 2), sd.b, c);
         e = u >= U / 2 ? fma(k, sd.a, c) : fma(-k, sd.a, c);
       } else {
         e = fma(-fma(x, x, 1.0), sd.s, 1.0);

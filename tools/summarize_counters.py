@@ -21,9 +21,16 @@ import sys
 
 
 def short(name: str) -> str:
-    n = name.split("(")[0]
-    n = n.replace("void ", "").replace("miint::(anonymous namespace)::", "")
-    return n[:70]
+    n = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    n = n.replace("miint::", "").replace("(miint::DivMode)", "div")
+    depth, out = 0, []
+    for ch in n:  # drop the parameter list, keep template arguments
+        if ch == "(" and depth == 0:
+            break
+        depth += ch == "<"
+        depth -= ch == ">"
+        out.append(ch)
+    return "".join(out)[:90]
 
 
 def load(dirpath: str):

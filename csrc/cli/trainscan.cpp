@@ -10,7 +10,8 @@
 // printed element (P=7 -> 0.000000, P=16 -> 117642.707174). --replicate allgathers the full
 // table to every rank like 4main.c:157.
 //
-//   ./trainscan [--gpus G] [--parity] [--replicate] [--no-phase2] [--json]
+//   ./trainscan [--gpus G] [--parity] [--replicate] [--no-phase2] [--algo fused|lookback]
+//               [--iters K] [--json]
 #include <cstdio>
 
 #include "cli_common.hpp"
@@ -28,6 +29,8 @@ int main(int argc, char** argv) {
     cfg.parity = a.flag("parity");
     cfg.replicate = a.flag("replicate");
     cfg.phase2 = !a.flag("no-phase2");
+    cfg.algo = a.str("algo", "fused") == "lookback" ? ScanAlgo::kLookback : ScanAlgo::kFused;
+    const int iters = static_cast<int>(a.integer("iters", 1));
     if (topo.rank0 == 0)  // 4main.c:72-74 (tablelen/1800)
       std::printf("Step size of %ld\n", static_cast<long>(cfg.steps_per_sec));
     TrainScanResult res;
@@ -35,6 +38,11 @@ int main(int argc, char** argv) {
     cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
       TrainScan ts(cfg, dev, comm);
       TrainScanResult r = ts.run();
+      for (int i = 1; i < iters; ++i) {  // --iters K: report the best device time
+        const TrainScanResult q = ts.run();
+        if (q.device_ms < r.device_ms) r.device_ms = q.device_ms;
+        r.timeout |= q.timeout;
+      }
       std::lock_guard<std::mutex> lk(mu);
       if (rank == topo.rank0) res = r;
     });

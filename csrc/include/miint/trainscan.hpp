@@ -5,14 +5,18 @@
 // element partition, ships every slice to rank 0, which adds carries serially and
 // broadcasts the 144 MB table; then does it all again for the second integral.
 //
-// Here, per rank (one GPU):
-//   phase 1  fused interp+scan kernel (decoupled look-back) -> velocity-integral slice
-//            allgather of one fp64 slice total per rank -> exclusive carry -> add
-//   phase 2  scan of the phase-1 slice -> position slice, same carry exchange
-//   optional allgather of the full tables (the reference's "every rank has the table").
-// Communication volume: 2 x world x 8 B instead of 2 x (gather + broadcast) of 144 MB.
-// --parity reproduces 4main's partitions (fill by seconds, scan by elements, residual
-// never scanned, value printed from element T-2), so P=7 prints 0 and P=16 117642.707174.
+// Here, per rank (one GPU), two algorithms:
+//   kFused (default)  reduce-then-scan on the *computed* samples (trainscan.hip): per-tile
+//                     sums (compute only) -> one-workgroup tile prefix -> [allgather of one
+//                     {T1, T2, count} triple per rank -> rank carries] -> one write-only pass
+//                     that emits both the running integral and its running integral.
+//                     HBM traffic: 16 B per sample, written once.
+//   kLookback         the general single-pass decoupled look-back scan (scan.hip), used as
+//                     phase-1 interp+scan and phase-2 scan, with an allgather + carry add per
+//                     phase (48 B per sample of traffic).
+// Communication volume either way: a few x world x 8 B instead of 2 x (gather + broadcast)
+// of 144 MB. --parity reproduces 4main's partitions (fill by seconds, scan by elements,
+// residual never scanned, printed element T-2), so P=7 prints 0 and P=16 117642.707174.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -25,12 +29,15 @@
 
 namespace miint {
 
+enum class ScanAlgo : int { kFused = 0, kLookback = 1 };
+
 struct TrainScanConfig {
   int steps_per_sec = 10000;  // 4main.c:26
   int seconds = 1800;         // 4main.c:27 (table covers 1800 s)
   bool parity = false;        // emulate 4main.c partitions and printed element
   bool replicate = false;     // allgather full tables to every rank (4main.c:157)
   bool phase2 = true;         // second integral (4main.c:178-221)
+  ScanAlgo algo = ScanAlgo::kFused;
 };
 
 struct TrainScanResult {
@@ -40,18 +47,43 @@ struct TrainScanResult {
   unsigned timeout = 0;      // look-back spin gave up (never expected)
 };
 
+// Kernel-level parameters of the fused pipeline (trainscan.hip).
+struct TrainScanKernelParams {
+  const double* table;  // device profile table
+  int table_n;
+  double dt;            // seconds per sample
+  uint64_t i0;          // global index of this slice's first sample
+  uint64_t n;           // samples in the slice
+  uint64_t win_lo, win_hi;  // samples outside [win_lo, win_hi) are zero (parity fills)
+};
+size_t trainscan_workspace_bytes(uint64_t n);
+// K1 + K2: per-tile sums and tile prefixes into `ws`; totals[0..1] = {T1, T2} (device).
+void launch_trainscan_local(const TrainScanKernelParams& p, void* ws, double* totals,
+                            hipStream_t s);
+// K3: rank carries {C1, C2} from world x {T1, T2, count} gathered triples.
+void launch_trainscan_rank_carry(const double* gathered, int rank, double* carries,
+                                 hipStream_t s);
+// K4: write vel (running integral) and pos (its running integral); carries may be null.
+void launch_trainscan_write(const TrainScanKernelParams& p, const void* ws, const double* carries,
+                            double* vel, double* pos, hipStream_t s);
+
 class TrainScan {
  public:
   TrainScan(const TrainScanConfig& cfg, int device, const Comm* comm = nullptr);
   TrainScanResult run();
+  // Enqueue one complete pipeline on the plan's stream without synchronising.
+  void enqueue();
   uint64_t total() const { return total_; }
   uint64_t local_begin() const { return begin_; }
   uint64_t local_count() const { return count_; }
   const double* velocity() const { return vel_.get(); }
   const double* position() const { return pos_.get(); }
   const double* replicated() const { return full_.get(); }
+  hipStream_t stream() const { return stream_.get(); }
 
  private:
+  void enqueue_fused(hipStream_t s);
+  void enqueue_lookback(hipStream_t s);
   void exchange_carry(const double* slice, uint64_t n, double* slice_out, hipStream_t s);
   double pick_global(const double* slice, uint64_t global_index, hipStream_t s);
 
@@ -63,8 +95,8 @@ class TrainScan {
   uint64_t win_lo_ = 0, win_hi_ = ~uint64_t(0);
   Stream stream_;
   DeviceBuffer<double> table_, vel_, pos_, full_;
-  DeviceBuffer<char> state_;
-  DeviceBuffer<double> scratch_;  // [0] local total, [1] carry, [2] pick, [8..8+world) totals
+  DeviceBuffer<char> state_;      // look-back scan state or fused-pipeline workspace
+  DeviceBuffer<double> scratch_;  // [0..7] scalars, [8..) gathered per-rank values
   PinnedBuffer<double> host_;
   Event e0_, e1_;
 };

@@ -259,7 +259,22 @@ PYBIND11_MODULE(_miint, m) {
       .def_readwrite("seconds", &TrainScanConfig::seconds)
       .def_readwrite("parity", &TrainScanConfig::parity)
       .def_readwrite("replicate", &TrainScanConfig::replicate)
-      .def_readwrite("phase2", &TrainScanConfig::phase2);
+      .def_readwrite("phase2", &TrainScanConfig::phase2)
+      .def_property("algo",
+                    [](const TrainScanConfig& c) { return c.algo == ScanAlgo::kFused ? "fused" : "lookback"; },
+                    [](TrainScanConfig& c, const std::string& s) {
+                      MIINT_CHECK(s == "fused" || s == "lookback", "algo must be fused|lookback");
+                      c.algo = s == "fused" ? ScanAlgo::kFused : ScanAlgo::kLookback;
+                    });
+  m.def("trainscan_workspace_bytes", &trainscan_workspace_bytes);
+  m.def("launch_trainscan", [](uintptr_t table, int tn, double dt, uint64_t i0, uint64_t n,
+                               uint64_t win_lo, uint64_t win_hi, uintptr_t ws, uintptr_t totals,
+                               uintptr_t carries, uintptr_t vel, uintptr_t pos, uintptr_t s) {
+    TrainScanKernelParams p{ptr<const double>(table), tn, dt, i0, n, win_lo, win_hi};
+    launch_trainscan_local(p, ptr<void>(ws), ptr<double>(totals), stream(s));
+    launch_trainscan_write(p, ptr<const void>(ws), ptr<const double>(carries), ptr<double>(vel),
+                           ptr<double>(pos), stream(s));
+  });
   py::class_<TrainScan>(m, "TrainScan")
       .def(py::init<const TrainScanConfig&, int, const Comm*>(), py::arg("config"),
            py::arg("device"), py::arg("comm") = nullptr, py::keep_alive<1, 4>())

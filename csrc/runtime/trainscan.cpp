@@ -1,11 +1,22 @@
 // TrainScan implementation (see miint/trainscan.hpp).
 #include "miint/trainscan.hpp"
 
+#include <algorithm>
+
 #include "miint/integrator.hpp"
 #include "miint/kernels.hpp"
 #include "miint/oracle.hpp"
 
 namespace miint {
+
+namespace {
+// scratch_ layout
+constexpr int kLocalTotal = 0;  // [0] look-back: local slice total
+constexpr int kCarry = 1;       // [1] look-back carry | [2..3] fused {C1, C2}
+constexpr int kPick = 4;        // [4] pick_global value
+constexpr int kTotals = 5;      // [5..6] fused {T1, T2}, [7] count
+constexpr int kGather = 8;      // [8 ..) gathered values (3 per rank)
+}  // namespace
 
 TrainScan::TrainScan(const TrainScanConfig& cfg, int device, const Comm* comm)
     : cfg_(cfg), device_(device), comm_(comm), stream_((set_device(device), Stream())) {
@@ -33,51 +44,68 @@ TrainScan::TrainScan(const TrainScanConfig& cfg, int device, const Comm* comm)
   table_ = DeviceBuffer<double>(tab.size());
   MIINT_HIP(hipMemcpy(table_.get(), tab.data(), table_.bytes(), hipMemcpyHostToDevice));
   vel_ = DeviceBuffer<double>(count_);
-  if (cfg.phase2) pos_ = DeviceBuffer<double>(count_);
+  if (cfg.phase2 || cfg.algo == ScanAlgo::kFused) pos_ = DeviceBuffer<double>(count_);
   if (cfg.replicate) {
     MIINT_CHECK(!cfg.parity && total_ % static_cast<uint64_t>(world_) == 0,
                 "replicate needs equal slices (total divisible by world, no parity)");
     full_ = DeviceBuffer<double>(total_);
   }
-  state_ = DeviceBuffer<char>(scan_state_bytes(count_));
-  scratch_ = DeviceBuffer<double>(8 + static_cast<size_t>(world_));
+  state_ = DeviceBuffer<char>(cfg.algo == ScanAlgo::kFused ? trainscan_workspace_bytes(count_)
+                                                            : scan_state_bytes(count_));
+  scratch_ = DeviceBuffer<double>(kGather + 3 * static_cast<size_t>(world_));
   host_ = PinnedBuffer<double>(4);
   MIINT_HIP(hipMemset(scratch_.get(), 0, scratch_.bytes()));
+  MIINT_HIP(hipMemset(state_.get(), 0, state_.bytes()));
+  const double cnt = static_cast<double>(count_);
+  MIINT_HIP(hipMemcpy(scratch_.get() + kTotals + 2, &cnt, sizeof(double), hipMemcpyHostToDevice));
   MIINT_HIP(hipDeviceSynchronize());
 }
 
-// Replace this rank's locally scanned slice by the globally scanned one: allgather every
-// rank's local total, form the exclusive carry for this rank, add it in place.
+// Look-back path: replace this rank's locally scanned slice by the globally scanned one —
+// allgather every rank's local total, form the exclusive carry, add it in place.
 void TrainScan::exchange_carry(const double* slice, uint64_t n, double* slice_out,
                                hipStream_t s) {
   if (!comm_ || world_ == 1) return;
   double* sc = scratch_.get();
-  MIINT_HIP(hipMemcpyAsync(sc, slice + (n - 1), sizeof(double), hipMemcpyDeviceToDevice, s));
-  comm_->allgather(sc, sc + 8, 1, s);
-  launch_exclusive_carry(sc + 8, rank_, sc + 1, s);
-  if (rank_ > 0) launch_add_carry(slice_out, n, sc + 1, s);
+  MIINT_HIP(hipMemcpyAsync(sc + kLocalTotal, slice + (n - 1), sizeof(double),
+                           hipMemcpyDeviceToDevice, s));
+  comm_->allgather(sc + kLocalTotal, sc + kGather, 1, s);
+  launch_exclusive_carry(sc + kGather, rank_, sc + kCarry, s);
+  if (rank_ > 0) launch_add_carry(slice_out, n, sc + kCarry, s);
 }
 
 // Value of global element `gi` (0 if no rank owns it, e.g. 4main's unscanned residual).
 double TrainScan::pick_global(const double* slice, uint64_t gi, hipStream_t s) {
   double* sc = scratch_.get();
-  MIINT_HIP(hipMemsetAsync(sc + 2, 0, sizeof(double), s));
+  MIINT_HIP(hipMemsetAsync(sc + kPick, 0, sizeof(double), s));
   if (gi >= begin_ && gi < begin_ + count_)
-    MIINT_HIP(hipMemcpyAsync(sc + 2, slice + (gi - begin_), sizeof(double),
+    MIINT_HIP(hipMemcpyAsync(sc + kPick, slice + (gi - begin_), sizeof(double),
                              hipMemcpyDeviceToDevice, s));
-  if (comm_ && world_ > 1) comm_->allreduce_sum(sc + 2, sc + 2, 1, s);
-  MIINT_HIP(hipMemcpyAsync(host_.get(), sc + 2, sizeof(double), hipMemcpyDeviceToHost, s));
+  if (comm_ && world_ > 1) comm_->allreduce_sum(sc + kPick, sc + kPick, 1, s);
+  MIINT_HIP(hipMemcpyAsync(host_.get(), sc + kPick, sizeof(double), hipMemcpyDeviceToHost, s));
   MIINT_HIP(hipStreamSynchronize(s));
   return host_[0];
 }
 
-TrainScanResult TrainScan::run() {
-  DeviceGuard g(device_);
-  hipStream_t s = stream_.get();
-  TrainScanResult r;
+void TrainScan::enqueue_fused(hipStream_t s) {
+  TrainScanKernelParams p{table_.get(), static_cast<int>(oracle::profile_table().size()),
+                          1.0 / cfg_.steps_per_sec, begin_, count_, win_lo_, win_hi_};
+  double* sc = scratch_.get();
+  launch_trainscan_local(p, state_.get(), sc + kTotals, s);
+  const double* carries = nullptr;
+  if (comm_ && world_ > 1) {
+    // one {T1, T2, count} triple per rank (count written at construction), then each rank
+    // forms its own carries
+    comm_->allgather(sc + kTotals, sc + kGather, 3, s);
+    launch_trainscan_rank_carry(sc + kGather, rank_, sc + kCarry + 1, s);
+    carries = sc + kCarry + 1;
+  }
+  launch_trainscan_write(p, state_.get(), carries, vel_.get(), pos_.get(), s);
+}
+
+void TrainScan::enqueue_lookback(hipStream_t s) {
   const double dt = 1.0 / cfg_.steps_per_sec;
   const int tn = static_cast<int>(oracle::profile_table().size());
-  e0_.record(s);
   // Phase 1: velocity samples -> running integral (4main.c:95-160)
   launch_interp_scan_window(table_.get(), tn, dt, begin_, count_, win_lo_, win_hi_, vel_.get(),
                             state_.get(), nullptr, s);
@@ -87,6 +115,13 @@ TrainScanResult TrainScan::run() {
     launch_inclusive_scan(vel_.get(), pos_.get(), count_, state_.get(), nullptr, s);
     exchange_carry(pos_.get(), count_, pos_.get(), s);
   }
+}
+
+void TrainScan::enqueue() {
+  DeviceGuard g(device_);
+  hipStream_t s = stream_.get();
+  if (cfg_.algo == ScanAlgo::kFused) enqueue_fused(s);
+  else enqueue_lookback(s);
   if (cfg_.replicate) {
     if (comm_) {
       comm_->allgather(vel_.get(), full_.get(), count_, s);
@@ -95,14 +130,22 @@ TrainScanResult TrainScan::run() {
                                hipMemcpyDeviceToDevice, s));
     }
   }
+}
+
+TrainScanResult TrainScan::run() {
+  DeviceGuard g(device_);
+  hipStream_t s = stream_.get();
+  TrainScanResult r;
+  e0_.record(s);
+  enqueue();
   e1_.record(s);
   MIINT_HIP(hipStreamSynchronize(s));
   r.device_ms = Event::elapsed_ms(e0_, e1_);
-  r.timeout = scan_timeout_flag(state_.get(), s);
+  if (cfg_.algo == ScanAlgo::kLookback) r.timeout = scan_timeout_flag(state_.get(), s);
   // 4main.c:241 prints default_sum[tablelen-2]; the complete integral is element T-1.
   const uint64_t gi = cfg_.parity ? total_ - 2 : total_ - 1;
   r.distance = pick_global(vel_.get(), gi, s) / cfg_.steps_per_sec;
-  if (cfg_.phase2) {
+  if (cfg_.phase2 || cfg_.algo == ScanAlgo::kFused) {
     const uint64_t last = cfg_.parity ? (total_ / world_) * world_ - 1 : total_ - 1;
     r.sum_of_sums = pick_global(pos_.get(), last, s);
   }

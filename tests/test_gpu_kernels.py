@@ -183,6 +183,60 @@ def test_interp_scan_matches_fill_then_scan(cuda):
     assert float(fused[-1].item()) / 1e4 == pytest.approx(122000.004000, abs=1e-6)
 
 
+@pytest.mark.parametrize("n", [1, 4095, 4097, 1_000_003, 18_000_000])
+def test_fused_trainscan_vs_cumsum(cuda, n):
+    vel, pos, totals = kernels.trainscan(n)
+    x = kernels.interp_fill(n)
+    v_ref = torch.cumsum(x, 0)
+    torch.testing.assert_close(vel, v_ref, rtol=1e-11, atol=1e-7)
+    p_ref = torch.cumsum(v_ref, 0)
+    torch.testing.assert_close(pos, p_ref, rtol=1e-10, atol=1e-3)
+    assert float(totals[0]) == pytest.approx(float(x.sum()), rel=1e-12)
+    assert float(totals[1]) == pytest.approx(float(v_ref.sum()), rel=1e-11)
+
+
+def test_fused_trainscan_rank_carries(cuda):
+    """Split 18e6 samples into 3 'ranks'; carries from the {T1,T2,count} triples must make
+    the concatenated slices equal the single-slice scan (the multi-GPU path's algebra)."""
+    n = 18_000_000
+    vel, pos, _ = kernels.trainscan(n)
+    cuts = [0, 5_000_011, 11_000_000, n]
+    tri = []
+    for r in range(3):
+        _, _, t = kernels.trainscan(cuts[r + 1] - cuts[r], i0=cuts[r])
+        tri.append((float(t[0]), float(t[1]), cuts[r + 1] - cuts[r]))
+    for r in range(3):
+        c1 = c2 = 0.0
+        for q in range(r):  # same fold as ts_rank_carry
+            c2 += tri[q][2] * c1 + tri[q][1]
+            c1 += tri[q][0]
+        car = torch.tensor([c1, c2], dtype=torch.float64, device="cuda")
+        v, p, _ = kernels.trainscan(cuts[r + 1] - cuts[r], i0=cuts[r], carries=car)
+        torch.testing.assert_close(v, vel[cuts[r]:cuts[r + 1]], rtol=1e-12, atol=1e-6)
+        torch.testing.assert_close(p, pos[cuts[r]:cuts[r + 1]], rtol=1e-12, atol=1e-2)
+
+
+def test_fused_trainscan_parity_window(cuda):
+    n = 2_000_000
+    vel, _, _ = kernels.trainscan(n, i0=1_000_000, window=(1_500_000, 2_500_000))
+    x = kernels.interp_fill(n, i0=1_000_000)
+    x[:500_000] = 0
+    x[1_500_000:] = 0
+    torch.testing.assert_close(vel, torch.cumsum(x, 0), rtol=1e-11, atol=1e-7)
+
+
+@pytest.mark.parametrize("algo", ["fused", "lookback"])
+@pytest.mark.parametrize("parity", [False, True])
+def test_trainscan_class_algorithms_agree(native, cuda, algo, parity):
+    cfg = native.TrainScanConfig()
+    cfg.algo = algo
+    cfg.parity = parity
+    r = native.TrainScan(cfg, 0).run()
+    assert r["timeout"] == 0
+    assert abs(r["distance"] - 122000.004) < 1e-6
+    assert r["sum_of_sums"] / 1e8 == pytest.approx(109861003.621919, rel=1e-9)
+
+
 def test_table2d_separable_oracle(cuda):
     v = torch.as_tensor(fixtures.profile_table(), device="cuda")
     T = kernels.outer_product(v)

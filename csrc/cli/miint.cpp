@@ -4,6 +4,7 @@
 //   ./miint bench [--integrand pi4] [--n 1e9] [--dtype fp64] [--rule left] [--iters 200]
 //                 [--gpus G] [--div series|ieee] [--unfused] [--no-graph]      (JSON lines)
 //   ./miint sweep [--gpus G]     N in {1e6,1e9,1e10} x dtype {fp64,fp32} x integrand
+//   ./miint table2d [--grid 4096] [--gpus G]   2-D velocity-field integral (BASELINE #5)
 //   ./miint selfcheck            every SURVEY §6.1 oracle on the GPU, exit 1 on mismatch
 //
 // The reference has no benchmark harness (its only artefact is a wall-clock
@@ -17,6 +18,7 @@
 #include "cli_common.hpp"
 #include "miint/integrator.hpp"
 #include "miint/oracle.hpp"
+#include "miint/table2d.hpp"
 #include "miint/trainscan.hpp"
 
 using namespace miint;
@@ -154,6 +156,32 @@ int main(int argc, char** argv) {
                   a.str("rule", "left").c_str());
       return 0;
     }
+    if (cmd == "table2d") {  // BASELINE config #5: 2-D field, g x g samples, rows split
+      Table2DConfig c;
+      c.grid = static_cast<int>(a.integer("grid", 4096));
+      double value = 0.0, ms = 0.0;
+      std::mutex mu;
+      cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
+        Table2DPlan plan(c, dev, comm);
+        const double v = plan.run();
+        const double t = plan.time(iters);
+        std::lock_guard<std::mutex> g(mu);
+        if (rank == topo.rank0) value = v;
+        if (t > ms) ms = t;
+      });
+      if (topo.rank0 == 0) {
+        const double want = table2d_oracle(c.grid);
+        const double exact = 122000.004 * 122000.004;
+        std::printf("{\"program\":\"table2d\",\"grid\":%d,\"gpus\":%d,\"result\":%.17g,"
+                    "\"midpoint_oracle\":%.17g,\"rel_err_vs_oracle\":%.3e,"
+                    "\"rel_err_vs_exact\":%.3e,\"ms_per_integration\":%.6f,"
+                    "\"samples_per_s\":%.6e}\n",
+                    c.grid, topo.world, value, want, std::fabs(value - want) / want,
+                    std::fabs(value - exact) / exact, ms,
+                    static_cast<double>(c.grid) * c.grid / (ms * 1e-3));
+      }
+      return 0;
+    }
     if (cmd == "sweep") {
       const std::vector<double> ns = {1e6, 1e9, 1e10};
       const std::vector<std::string> integs = {"pi4", "sin", "poly", "train"};
@@ -170,7 +198,7 @@ int main(int argc, char** argv) {
         }
       return 0;
     }
-    std::fprintf(stderr, "usage: miint info|bench|sweep|selfcheck [--flags]\n");
+    std::fprintf(stderr, "usage: miint info|bench|sweep|table2d|selfcheck [--flags]\n");
     return 2;
   } catch (const std::exception& e) {
     std::fprintf(stderr, "miint: %s\n", e.what());

@@ -1,0 +1,55 @@
+// 2-D velocity-field integral (BASELINE.json config #5; no counterpart in the reference,
+// whose data is the 1-D ex4vel.h profile).
+//
+// Field: F(x, y) = v(x) v(y) on [0, 1800]^2, materialised as the 1801 x 1801 fp64 outer
+// product of the generated profile (25.9 MB, built on the device), integrated with a
+// midpoint rule on a g x g sample grid using bilinear interpolation of the table. The
+// kernel (table.hip) gives each workgroup a 64 x 64 block of samples and stages the table
+// footprint of that block in LDS (2-D LDS tiling). Ranks split the sample rows; the
+// per-rank partials meet in one RCCL all-reduce.
+//
+// Oracle: bilinear interpolation of a separable product of piecewise-linear factors is
+// exactly v(x) v(y), so the midpoint sum equals (sum_j v(x_j) dx)^2 — a 1-D computation —
+// and the exact integral is 122000.004^2 = 1.4884000976e10.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "miint/comm.hpp"
+#include "miint/kernels.hpp"
+#include "miint/runtime.hpp"
+
+namespace miint {
+
+struct Table2DConfig {
+  int grid = 4096;       // samples per axis
+  double extent = 1800;  // [0, extent]^2
+};
+
+class Table2DPlan {
+ public:
+  Table2DPlan(const Table2DConfig& cfg, int device, const Comm* comm = nullptr);
+  // One integration: kernel -> finalize -> [allreduce] -> pinned host. Returns the value.
+  double run();
+  // `iters` back-to-back integrations; returns device ms per integration.
+  double time(int iters);
+  int row0() const { return row0_; }
+  int row1() const { return row1_; }
+
+ private:
+  void enqueue(hipStream_t s);
+  Table2DConfig cfg_;
+  int device_;
+  const Comm* comm_;
+  int rank_ = 0, world_ = 1;
+  int row0_ = 0, row1_ = 0;
+  Stream stream_;
+  DeviceBuffer<double> v_, table_, partials_, result_;
+  PinnedBuffer<double> host_;
+  Event e0_, e1_;
+};
+
+// Host oracle for the midpoint sum on a g x g grid: (sum_j v(x_j) dx)^2.
+double table2d_oracle(int grid, double extent = 1800.0);
+
+}  // namespace miint

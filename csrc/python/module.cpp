@@ -15,6 +15,7 @@
 #include "miint/oracle.hpp"
 #include "miint/runtime.hpp"
 #include "miint/selftest.hpp"
+#include "miint/table2d.hpp"
 #include "miint/trainscan.hpp"
 
 namespace py = pybind11;
@@ -267,6 +268,22 @@ PYBIND11_MODULE(_miint, m) {
                       c.algo = s == "fused" ? ScanAlgo::kFused : ScanAlgo::kLookback;
                     });
   m.def("trainscan_workspace_bytes", &trainscan_workspace_bytes);
+
+  // ------------------------------------------------------------------ 2-D field plan
+  py::class_<Table2DPlan>(m, "Table2DPlan")
+      .def(py::init([](int grid, double extent, int device, const Comm* comm) {
+             Table2DConfig c;
+             c.grid = grid;
+             c.extent = extent;
+             return new Table2DPlan(c, device, comm);
+           }),
+           py::arg("grid") = 4096, py::arg("extent") = 1800.0, py::arg("device") = 0,
+           py::arg("comm") = nullptr, py::keep_alive<1, 5>())
+      .def("run", &Table2DPlan::run, py::call_guard<py::gil_scoped_release>())
+      .def("time", &Table2DPlan::time, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("row0", &Table2DPlan::row0)
+      .def_property_readonly("row1", &Table2DPlan::row1);
+  m.def("table2d_oracle", &table2d_oracle, py::arg("grid"), py::arg("extent") = 1800.0);
   m.def("launch_trainscan", [](uintptr_t table, int tn, double dt, uint64_t i0, uint64_t n,
                                uint64_t win_lo, uint64_t win_hi, uintptr_t ws, uintptr_t totals,
                                uintptr_t carries, uintptr_t vel, uintptr_t pos, uintptr_t s) {

@@ -50,6 +50,30 @@ struct Sampler {
     const double v0 = tab[s - s0];
     return fma(tab[s + 1 - s0] - v0, t - static_cast<double>(s), v0);
   }
+  // The kItems consecutive samples of this thread, starting at slice-local index g.
+  // Hot form (tile fully inside the slice and the fill window): 64-bit index math once per
+  // thread, then per sample t = fma(k, dt, t_first), a 32-bit segment index and two
+  // broadcast LDS reads — identical to operator() up to one rounding of t.
+  __device__ __forceinline__ void items(uint64_t g, bool plain, double (&v)[kItems]) const {
+    if (!plain) {
+#pragma unroll
+      for (int k = 0; k < kItems; ++k) v[k] = (*this)(g + k);
+      return;
+    }
+    const double tb = dt * static_cast<double>(i0 + g);
+#pragma unroll
+    for (int k = 0; k < kItems; ++k) {
+      const double t = fma(static_cast<double>(k), dt, tb);
+      int s = static_cast<int>(t);
+      s = s >= nseg ? nseg - 1 : s;
+      const double v0 = tab[s - s0];
+      v[k] = fma(tab[s + 1 - s0] - v0, t - static_cast<double>(s), v0);
+    }
+  }
+  // Block-uniform: can every sample of tile [t0, t0 + kTile) take the hot form?
+  __device__ __forceinline__ bool plain_tile(uint64_t t0) const {
+    return t0 + kTile <= n && i0 + t0 >= win_lo && i0 + t0 + kTile <= win_hi;
+  }
 };
 
 __device__ __forceinline__ int seg_of(double t, int nseg) {
@@ -80,13 +104,14 @@ __global__ __launch_bounds__(kB) void ts_tile_sums(TrainScanKernelParams p, f64x
   const Sampler f = make_sampler(p, tab);
   const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kTile;
   const uint64_t nt = p.n - t0 < kTile ? p.n - t0 : kTile;
+  double v[kItems];
+  f.items(t0 + threadIdx.x * kItems, f.plain_tile(t0), v);
+  const double w0 = static_cast<double>(static_cast<int64_t>(nt) - threadIdx.x * kItems);
   double s1 = 0.0, s2 = 0.0;
 #pragma unroll
   for (int k = 0; k < kItems; ++k) {
-    const int i = threadIdx.x * kItems + k;
-    const double v = f(t0 + i);
-    s1 += v;
-    s2 = fma(static_cast<double>(static_cast<int64_t>(nt) - i), v, s2);  // v_i counted n_t - i times
+    s1 += v[k];
+    s2 = fma(w0 - k, v[k], s2);  // sample i is counted n_t - i times in the tile's prefixes
   }
   s1 = block_sum<kB>(s1, red1);
   s2 = block_sum<kB>(s2, red2);
@@ -171,10 +196,11 @@ __global__ __launch_bounds__(kB) void ts_write(TrainScanKernelParams p, const f6
   const double c1 = carries ? carries[0] : 0.0;
   const double c2 = carries ? carries[1] : 0.0;
   double v[kItems];
+  f.items(t0 + threadIdx.x * kItems, f.plain_tile(t0), v);
   double run = 0.0;
 #pragma unroll
   for (int k = 0; k < kItems; ++k) {
-    run += f(t0 + threadIdx.x * kItems + k);
+    run += v[k];
     v[k] = run;  // thread-local inclusive scan of the samples
   }
   double tot;

@@ -54,6 +54,8 @@ class Comm {
   void reduce_sum(const double* send, double* recv, size_t count, int root, hipStream_t s) const;
   // Throws if RCCL reported an asynchronous error (e.g. a peer died).
   void check_async() const;
+  // Abort outstanding collectives (watchdog path); the communicator is unusable afterwards.
+  void abort() const;
 
   static void group_start();
   static void group_end();
@@ -61,7 +63,7 @@ class Comm {
 
  private:
   Comm() = default;
-  ncclComm_t comm_ = nullptr;
+  mutable ncclComm_t comm_ = nullptr;  // nulled by abort()
   int rank_ = 0, world_ = 1, device_ = 0;
 };
 

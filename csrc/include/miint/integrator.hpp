@@ -52,6 +52,7 @@ struct RiemannConfig {
                                // torch.distributed path reduces results itself)
   bool force_collective = false;  // run the RCCL stage even with a 1-rank communicator
                                   // (exercises the multi-GPU graph path on one GPU)
+  double timeout_s = 300.0;    // collective watchdog in sync(); <= 0 disables
 };
 
 // Balanced 64-bit slice of [0, n) for rank r of w: first (n % w) ranks get one extra.

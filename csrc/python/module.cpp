@@ -16,6 +16,7 @@
 #include "miint/runtime.hpp"
 #include "miint/selftest.hpp"
 #include "miint/table2d.hpp"
+#include "miint/trace.hpp"
 #include "miint/trainscan.hpp"
 
 namespace py = pybind11;
@@ -86,6 +87,13 @@ PYBIND11_MODULE(_miint, m) {
   m.def("set_device", &set_device);
   m.def("device_synchronize", []() { MIINT_HIP(hipDeviceSynchronize()); });
   m.def("process_start_seconds", &process_start_seconds);
+  m.def("enable_tracing", &enable_tracing, "roctx ranges around runtime phases (MIINT_ROCTX=1)");
+  m.def("tracing_enabled", &tracing_enabled);
+  m.def("trace_mark", &trace_mark);
+  m.def("wait_with_timeout", [](uintptr_t s, double timeout_s) {
+    py::gil_scoped_release nogil;
+    return wait_with_timeout(stream(s), timeout_s, nullptr);
+  });
   m.def("wall_seconds", &wall_seconds);
 
   // ------------------------------------------------------------------ comm
@@ -131,6 +139,7 @@ PYBIND11_MODULE(_miint, m) {
       .def_readwrite("rank", &RiemannConfig::rank)
       .def_readwrite("world", &RiemannConfig::world)
       .def_readwrite("force_collective", &RiemannConfig::force_collective)
+      .def_readwrite("timeout_s", &RiemannConfig::timeout_s)
       .def_readwrite("host_direct", &RiemannConfig::host_direct);
 
   py::class_<RiemannPlan>(m, "RiemannPlan")

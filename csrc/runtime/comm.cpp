@@ -71,6 +71,10 @@ void Comm::check_async() const {
   MIINT_RCCL(ncclCommGetAsyncError(comm_, &r));
   MIINT_RCCL(r);
 }
+void Comm::abort() const {
+  if (comm_) (void)ncclCommAbort(comm_);
+  comm_ = nullptr;
+}
 void Comm::group_start() { MIINT_RCCL(ncclGroupStart()); }
 void Comm::group_end() { MIINT_RCCL(ncclGroupEnd()); }
 std::string Comm::version() {

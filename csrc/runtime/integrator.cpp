@@ -3,6 +3,8 @@
 
 #include <algorithm>
 
+#include "miint/trace.hpp"
+
 namespace miint {
 
 namespace {
@@ -138,6 +140,7 @@ void RiemannPlan::enqueue_batch(hipStream_t cs, hipStream_t rs, int nsteps, bool
 
 void RiemannPlan::capture_graphs() {
   DeviceGuard g(device_);
+  TraceRange tr("miint.plan.capture_graphs");
   batch_.reset(new Graph());
   try {
     batch_->capture(compute_.get(), [&](hipStream_t s) {
@@ -165,6 +168,7 @@ int RiemannPlan::host_index_of(int k, bool graphs) const {
 
 void RiemannPlan::launch_steps(int steps, bool pipeline, bool graphs) {
   DeviceGuard g(device_);
+  TraceRange tr("miint.plan.launch_steps");
   hipStream_t cs = compute_.get();
   hipStream_t rs = comm_stream_.get();
   const int S = cfg_.slots;
@@ -197,6 +201,12 @@ void RiemannPlan::launch_steps(int steps, bool pipeline, bool graphs) {
 
 void RiemannPlan::sync() const {
   DeviceGuard g(device_);
+  TraceRange tr("miint.plan.sync");
+  if (collective() && cfg_.timeout_s > 0) {  // watchdog: a dead peer must not hang us forever
+    wait_with_timeout(comm_stream_.get(), cfg_.timeout_s, comm_);
+    wait_with_timeout(compute_.get(), cfg_.timeout_s, comm_);
+    return;
+  }
   compute_.sync();
   comm_stream_.sync();
 }

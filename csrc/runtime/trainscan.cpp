@@ -6,6 +6,7 @@
 #include "miint/integrator.hpp"
 #include "miint/kernels.hpp"
 #include "miint/oracle.hpp"
+#include "miint/trace.hpp"
 
 namespace miint {
 
@@ -119,6 +120,7 @@ void TrainScan::enqueue_lookback(hipStream_t s) {
 
 void TrainScan::enqueue() {
   DeviceGuard g(device_);
+  TraceRange tr(cfg_.algo == ScanAlgo::kFused ? "miint.trainscan.fused" : "miint.trainscan.lookback");
   hipStream_t s = stream_.get();
   if (cfg_.algo == ScanAlgo::kFused) enqueue_fused(s);
   else enqueue_lookback(s);

@@ -1,0 +1,179 @@
+"""Python command line: ``python -m cuda_v_mpi_amd <command> [flags]``.
+
+Mirrors the native tools in build/bin (same stdout contract as the reference programs,
+SURVEY §2.6) on top of the Python API, and adds JSON output:
+
+    riemann     sin on [0, pi], N = 1e9 (riemann.cpp)          [--integrand pi4 --n 1e9 ...]
+    cintegrate  train distance from the profile (cintegrate.cu)  [--parity --sp 32 --sm 2]
+    trainscan   two-phase prefix scan (4main.c)                   [--parity --algo lookback]
+    integrate   any integrand, JSON result                        [--integrand --n --rule ...]
+    oracle      print every SURVEY §6.1 oracle value (CPU only)
+    info        devices and build
+
+Multi-GPU: launch under torchrun (one process per GPU); the process group is created from
+the environment and partial sums are reduced with RCCL.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import sys
+
+from .utils import output
+
+
+def _elapsed() -> float:
+    """Seconds since this process started (the reference starts its clock first thing in
+    main(), before MPI_Init / context creation: riemann.cpp:51, cintegrate.cu:104)."""
+    import time
+
+    import psutil
+
+    return time.time() - psutil.Process().create_time()
+
+
+def _ctx():
+    from .parallel import dist as mdist
+
+    return mdist.init()
+
+
+def cmd_riemann(a) -> int:
+    from . import Integrator
+
+    ctx = _ctx()
+    spec_b = {"sin": math.pi, "pi4": 1.0}.get(a.integrand, None)
+    it = Integrator(a.integrand, n=int(a.n), rule=a.rule, dtype=a.dtype, ctx=ctx,
+                    backend=a.backend)
+    r = it.run()
+    if ctx.is_root:
+        print(output.fmt_seconds(_elapsed()))
+        print(output.fmt_riemann_result(spec_b if spec_b is not None else it.spec.b, a.n, r.value))
+        if a.json:
+            print(json.dumps(r.as_dict()))
+    ctx.destroy()
+    return 0
+
+
+def cmd_cintegrate(a) -> int:
+    from . import Integrator
+    from .parallel.decomposition import coverage_seconds
+
+    ctx = _ctx()
+    seconds = coverage_seconds(a.sp * a.sm) if a.parity else 1800
+    it = Integrator("table", n=seconds * 10000, rule="left", b=float(seconds), ctx=ctx,
+                    backend=a.backend)
+    r = it.run()
+    if ctx.is_root:
+        print(output.fmt_seconds(_elapsed()))
+        print(output.fmt_cintegrate_distance(r.value))
+        if a.json:
+            print(json.dumps(r.as_dict()))
+    ctx.destroy()
+    return 0
+
+
+def cmd_trainscan(a) -> int:
+    from ._native import native
+    from .parallel.dist import native_comm
+
+    ctx = _ctx()
+    m = native()
+    cfg = m.TrainScanConfig()
+    cfg.parity, cfg.algo = a.parity, a.algo
+    comm = native_comm(ctx) if ctx.world > 1 else None
+    if ctx.is_root:
+        print(output.fmt_step_size(cfg.steps_per_sec))
+    r = m.TrainScan(cfg, ctx.device, comm).run()
+    if ctx.is_root:
+        print(output.fmt_seconds(_elapsed()))
+        print(output.fmt_total_distance(r["distance"]))
+        if a.json:
+            print(json.dumps(r))
+    ctx.destroy()
+    return 0
+
+
+def cmd_integrate(a) -> int:
+    from . import Integrator
+
+    ctx = _ctx()
+    r = Integrator(a.integrand, n=int(a.n), rule=a.rule, dtype=a.dtype, div=a.div, ctx=ctx,
+                   backend=a.backend).run()
+    if ctx.is_root:
+        print(json.dumps(r.as_dict()))
+    ctx.destroy()
+    return 0
+
+
+def cmd_oracle(a) -> int:
+    from ._native import native
+
+    m = native()
+    o = m.oracle
+    rows = {
+        "profile_exact_integral": o.profile_exact_integral(),
+        "cintegrate_sp32_sm2": o.cintegrate_parity(32, 2),
+        "cintegrate_sp30_sm2": o.cintegrate_parity(30, 2),
+        "cintegrate_sp32_sm3": o.cintegrate_parity(32, 3),
+        "trainscan_p1": o.trainscan_parity(1)[0],
+        "trainscan_p7": o.trainscan_parity(7)[0],
+        "trainscan_p16": o.trainscan_parity(16)[0],
+        "riemann_np8_n1e6": o.riemann_mpi_parity(8, 1e6),
+        "train_analytic_1800": o.train_distance(1800.0),
+        "pi4_left_n1e6_err": o.riemann_serial(m.Integrand.pi4, 0, 1, 10**6, m.Rule.left) - math.pi,
+    }
+    print(json.dumps(rows, indent=1))
+    return 0
+
+
+def cmd_info(a) -> int:
+    from . import __version__
+    from ._native import extension_path, native
+
+    m = native()
+    n = m.device_count()
+    print(f"cuda_v_mpi_amd {__version__}  extension {extension_path()}")
+    for d in range(n):
+        print(" ", m.device_info(d))
+    if n == 0:
+        print("  no HIP device visible")
+    return 0
+
+
+def main(argv=None) -> int:
+    p = argparse.ArgumentParser(prog="python -m cuda_v_mpi_amd", description=__doc__,
+                                formatter_class=argparse.RawDescriptionHelpFormatter)
+    sub = p.add_subparsers(dest="cmd", required=True)
+
+    def common(sp, integrand="sin"):
+        sp.add_argument("--integrand", default=integrand)
+        sp.add_argument("--n", type=float, default=1e9)
+        sp.add_argument("--rule", default="left", choices=["left", "mid", "right"])
+        sp.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
+        sp.add_argument("--div", default="series", choices=["series", "ieee", "series_direct"])
+        sp.add_argument("--backend", default="hip", choices=["hip", "cpu"])
+        sp.add_argument("--json", action="store_true")
+
+    common(sub.add_parser("riemann"))
+    c = sub.add_parser("cintegrate")
+    c.add_argument("--parity", action="store_true")
+    c.add_argument("--sp", type=int, default=32)
+    c.add_argument("--sm", type=int, default=2)
+    c.add_argument("--backend", default="hip", choices=["hip", "cpu"])
+    c.add_argument("--json", action="store_true")
+    t = sub.add_parser("trainscan")
+    t.add_argument("--parity", action="store_true")
+    t.add_argument("--algo", default="fused", choices=["fused", "lookback"])
+    t.add_argument("--json", action="store_true")
+    common(sub.add_parser("integrate"), integrand="pi4")
+    sub.add_parser("oracle")
+    sub.add_parser("info")
+    a = p.parse_args(argv)
+    return {"riemann": cmd_riemann, "cintegrate": cmd_cintegrate, "trainscan": cmd_trainscan,
+            "integrate": cmd_integrate, "oracle": cmd_oracle, "info": cmd_info}[a.cmd](a)
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,60 @@
+"""CPU tests of the command-line front ends (formats, argument handling, oracle dump)."""
+from __future__ import annotations
+
+import json
+import math
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _py(*args):
+    return subprocess.run([sys.executable, "-m", "cuda_v_mpi_amd", *args], cwd=REPO,
+                          capture_output=True, text=True, timeout=300)
+
+
+def test_python_cli_riemann_cpu_format():
+    p = _py("riemann", "--backend", "cpu", "--n", "1e6", "--json")
+    assert p.returncode == 0, p.stderr
+    l = p.stdout.strip().splitlines()
+    assert l[0].endswith(" seconds") and float(l[0].split()[0]) > 0
+    assert l[1].startswith("The integral of f(x) from 0.0 to 3.14159265358979 with 1000000 steps is ")
+    js = json.loads(l[2])
+    assert abs(js["value"] - 2.0) < 1e-11
+
+
+def test_python_cli_cintegrate_parity_cpu():
+    p = _py("cintegrate", "--backend", "cpu", "--parity")
+    assert p.returncode == 0, p.stderr
+    assert p.stdout.strip().splitlines()[1] == "final distance is:121999.800663"
+
+
+def test_python_cli_oracle():
+    p = _py("oracle")
+    assert p.returncode == 0, p.stderr
+    js = json.loads(p.stdout)
+    assert "%f" % js["trainscan_p16"] == "117642.707174"
+    assert js["trainscan_p7"] == 0.0
+    assert abs(js["pi4_left_n1e6_err"] - 1e-6) < 1e-9
+
+
+def test_native_cli_refuses_without_gpu():
+    exe = os.path.join(REPO, "build", "bin", "riemann")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", REPO, "-j8", "cli"], check=True, capture_output=True)
+    p = subprocess.run([exe], capture_output=True, text=True, timeout=60)
+    try:
+        import torch
+        has_gpu = torch.cuda.is_available()
+    except Exception:
+        has_gpu = False
+    if not has_gpu:
+        assert p.returncode == 1 and "HIP devices" in p.stderr
+
+
+def test_bench_rejects_gpus_without_torchrun():
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"],
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 2 and "torchrun" in p.stderr

@@ -29,6 +29,9 @@ namespace miint {
 // path is centred on the tile (Pi4 series) ask for the midpoint directly, saving an fma.
 template <class D>
 struct TileDefaults {
+  // Samples per lane tile (the grid-stride work unit) for division mode M.
+  template <DivMode M>
+  __host__ __device__ static constexpr int tile_len() { return 32; }
   template <int U, DivMode M>
   __device__ static constexpr double anchor() { return 0.0; }
   template <int U, DivMode M>
@@ -44,44 +47,84 @@ struct TileDefaults {
 // (~14 VALU f64 ops per sample with the coordinate and the accumulation).
 //
 // The series paths evaluate the same reciprocal per point from a per-tile seed:
-//   s  ~= 1/d(x_m)                   (v_rcp_f64 + one Newton step, once per U points;
+//   s  ~= 1/d(x_m)                   (v_rcp_f64 + one Newton step, once per tile;
 //                                     x_m = tile midpoint)
 //   e_u = 1 - d(x_u)*s               (the point's exact residual)
 //   1/d(x_u) = s*(1 + e_u + e_u^2 + e_u^3/(1-e_u))
-// |e_u| <= (U/2)*h (max of 2|x|/(1+x^2) is 1), so the dropped e^3 term is < 1e-17 relative
-// whenever (U/2)*h <= 2e-6; the host dispatcher (series_ok()) falls back to kIeee otherwise.
+// |e_u| <= |e_m| + (U/2)*h (max of 2|x|/(1+x^2) is 1), so the dropped e^3 term is < 1e-17
+// relative whenever (U/2)*h <= 2e-6; the host dispatcher (series_ok(), kSeriesHalfSpan) falls
+// back to kIeee otherwise.
 //
 // kSeriesDirect forms x_u = x0 + u*h, d_u = 1 + x_u^2, e_u = 1 - d_u*s explicitly (5 ops).
-// kSeries (default) evaluates the very same residual with the offset k = u - (U-1)/2 from
-// the midpoint: since d(x_m + k h) = d_m + 2 x_m h k + h^2 k^2 exactly,
+//
+// kSeries (default) evaluates the very same residual from the offset k = u - (U-1)/2 to the
+// midpoint: d(x_m + k h) = d_m + 2 x_m h k + h^2 k^2 exactly, so
 //   e_k = e_m + k*A + k^2*B,   A = -2 x_m h s,  B = -h^2 s,  e_m = 1 - d_m s,
-// and the two samples at +-k share c_k = e_m + k^2 B:  e_{+-k} = c_k +- k A.
-// That is 3 fma per PAIR of samples for the residuals plus 2 accumulations per sample
-// (3.5 VALU ops per sample). It is not an approximation: the quadratic is exact, and it is
-// more accurate than rounding x_u first. Every sample still gets its own residual and its
-// own contribution; tests compare every point against IEEE division (<= 2 ulp).
+// and it folds the series into one square per sample:
+//   1 + e + e^2 = 3/4 + g^2,   g = 1/2 + e,
+// so a sample costs ONE accumulation, fma(g, g, t), instead of t += e; t = fma(e, e, t).
+// The two samples at +-k of a sub-tile centre share c_k = 1/2 + e_c + k^2 B and get
+// g_{+-k} = c_k +- k A. c_k is formed directly with one fma from an SGPR k^2 (no running
+// recurrence: increments of ~1e-17 would be lost against ulp(1/2)). Per PAIR of samples:
+// 1 fma for c_k, 2 for g, 2 accumulations = 2.5 VALU per sample.
+// A 64-sample tile is 4 sub-tiles of 16 whose centres sit at c0 = -24, -8, 8, 24 steps from
+// x_m; re-expanding the exact quadratic there gives e_c = e_m + c0 A + c0^2 B and slope
+// A' = A + 2 c0 B (3 fma per sub-tile, against ~12 for a fresh seed). Keeping sub-tiles at
+// 8 pairs keeps the constants at 22 SGPR pairs: 79 SGPRs, 8 resident workgroups per CU.
+// Measured (gfx950 .s): 183 VALU per 64-sample tile = 2.86 per sample (the previous form,
+// t += e; t = fma(e, e, t) with one seed per 32 samples, was 127 per 32 = 3.97).
+//
+// Accuracy: every sample still gets its own residual and its own contribution. Per point,
+// g is rounded at ulp(1/2) scale: <= 5 ulp vs IEEE division, 91 % within 1 ulp, 99.4 %
+// within 2 (tools/ulp_probe.py, whole domain at three step sizes); the sum agrees with
+// the IEEE path to 1e-15 relative and |error| at N = 1e9 is unchanged (4.4e-16, mid rule).
 struct Pi4 : TileDefaults<Pi4> {
   static constexpr double kScale = 4.0;
-  static constexpr int kPairs = 16;  // supports tiles of up to 32 samples
+  static constexpr int kPairs = 8;                  // sample pairs per sub-tile
+  static constexpr int kSub = 2 * kPairs;           // 16 samples per sub-tile
+  static constexpr int kSubs = 4;                   // sub-tiles per series tile
+  static constexpr int kSeriesTile = kSub * kSubs;  // 64 samples per seed
 
-  // Pair offsets k = j + 1/2, held in SGPRs for the whole kernel (see init()).
-  // Every fma of the pair evaluation is then a 3-operand VOP3 v_fma_f64 with one SGPR
-  // source; folded to literals instead, hipcc emits v_fmac_f64 + literal and has to copy the
-  // shared c with a v_mov_b64 per pair (30 extra VALU per 32-sample tile, measured in the .s).
-  double pk[kPairs];
+  template <DivMode M>
+  __host__ __device__ static constexpr int tile_len() {
+    return M == DivMode::kSeries ? kSeriesTile : 32;
+  }
 
+  // Constants held in SGPRs for the whole kernel (see init()). Every fma of the pair
+  // evaluation is then a 3-operand VOP3 v_fma_f64 with one SGPR source; as literals, hipcc
+  // has to use the 2-operand v_fmac_f64 and copy the shared operand with a v_mov_b64.
+  // Mean of k_j^2 over a sub-tile's pairs: sum_j (j + 1/2)^2 / 8 = 170/8.
+  static constexpr double kMeanK2 = 21.25;
+  double pk[kPairs];         // k_j = j + 1/2
+  double pk2[kPairs];        // k_j^2 - kMeanK2
+  double pc[kSubs / 2];      // |sub-tile centre offset| c0: 8, 24
+  double pcm[kSubs / 2];     // c0 + kMeanK2 / c0
+  double pc2[kSubs / 2];     // 2 c0: 16, 48
+  double c15;                // 3/2 (e_m + 1/2 = 3/2 - d_m s in one fma)
+
+  __device__ __forceinline__ static double opaque_s(double v) {
+    asm volatile("" : "+s"(v));  // opaque -> stays an SGPR pair, never a literal
+    return v;
+  }
   __device__ __forceinline__ void init() {
 #pragma unroll
     for (int j = 0; j < kPairs; ++j) {
-      double k = j + 0.5;
-      asm volatile("" : "+s"(k));   // opaque -> stays an SGPR pair, never a literal
-      pk[j] = k;
+      pk[j] = opaque_s(j + 0.5);
+      pk2[j] = opaque_s((j + 0.5) * (j + 0.5) - kMeanK2);
     }
+#pragma unroll
+    for (int i = 0; i < kSubs / 2; ++i) {
+      const double c0 = kSub * (i + 0.5);
+      pc[i] = opaque_s(c0);
+      pcm[i] = opaque_s(c0 + kMeanK2 / c0);
+      pc2[i] = opaque_s(2.0 * c0);
+    }
+    c15 = opaque_s(1.5);
   }
 
   __device__ __forceinline__ double point(double x) const { return 1.0 / fma(x, x, 1.0); }
 
-  // Per-tile constants of the series reciprocal (also used by the validation kernel).
+  // Per-tile seed for kSeriesDirect (also the reciprocal seed of kSeries).
   struct Seed {
     double s, em, a, b;
   };
@@ -91,10 +134,35 @@ struct Pi4 : TileDefaults<Pi4> {
     s = fma(s, fma(-dm, s, 1.0), s);  // one Newton step
     return {s, fma(-dm, s, 1.0), (-2.0 * h) * xm * s, -(h * h) * s};
   }
+  // kSeries seed: as seed() but with eh = 1/2 + e_m rounded once (3/2 - d_m s).
+  __device__ __forceinline__ Seed seed_half(double xm, double h) const {
+    const double dm = fma(xm, xm, 1.0);
+    double s = __builtin_amdgcn_rcp(dm);
+    s = fma(s, fma(-dm, s, 1.0), s);  // one Newton step
+    return {s, fma(-dm, s, c15), (-2.0 * h) * xm * s, -(h * h) * s};
+  }
+  // Sub-tile q's centre offset c0 (in steps from x_m), c0 + kMeanK2/c0 and 2 c0, from the
+  // SGPR table (negative side by the free source-negate modifier).
+  __device__ __forceinline__ static double side(const double* t, int q) {
+    return q < kSubs / 2 ? -t[kSubs / 2 - 1 - q] : t[q - kSubs / 2];
+  }
+  // g at sub-tile centre, carrying the sub-tile's mean k^2 B:
+  //   1/2 + e_m + c0 A + (c0^2 + kMeanK2) B = fma(c0, fma(c0 + kMeanK2/c0, B, A), 1/2 + e_m).
+  // Each pair then adds only (k^2 - kMeanK2) B, which sums to zero over the sub-tile: when
+  // that term is below half an ulp of 1/2 (h ~ 1e-9) and fma(., ., eh) drops it, the dropped
+  // amounts cancel instead of biasing every sample the same way (B < 0), which they did
+  // (+0.2..0.4 ulp mean per point) with plain k^2.
+  __device__ __forceinline__ double centre_g(const Seed& sd, int q) const {
+    return fma(side(pc, q), fma(side(pcm, q), sd.b, sd.a), sd.em);
+  }
+  __device__ __forceinline__ double centre_slope(const Seed& sd, int q) const {
+    return fma(side(pc2, q), sd.b, sd.a);
+  }
 
   template <int U, DivMode M>
   __device__ __forceinline__ double tile(double x0, double h) const {
     static_assert(U % 2 == 0, "pair evaluation needs an even tile");
+    static_assert(M != DivMode::kSeries, "kSeries runs through tile_acc");
     if constexpr (M == DivMode::kIeee) {
       double acc = 0.0;
 #pragma unroll
@@ -103,65 +171,74 @@ struct Pi4 : TileDefaults<Pi4> {
         acc += 1.0 / fma(x, x, 1.0);
       }
       return acc;
-    } else if constexpr (M == DivMode::kSeries) {
-      return tile_acc<U, M>(fma(0.5 * (U - 1), h, x0), h, 0.0);
     } else {
-      const double xm = fma(0.5 * (U - 1), h, x0);
-      const double dm = fma(xm, xm, 1.0);
-      double s = __builtin_amdgcn_rcp(dm);
-      s = fma(s, fma(-dm, s, 1.0), s);  // one Newton step: seed error ~1e-16 + |x-xm| term
+      const Seed sd = seed(fma(0.5 * (U - 1), h, x0), h);
       double t1a = 0.0, t1b = 0.0, t2 = 0.0;
 #pragma unroll
       for (int u = 0; u < U; u += 2) {
         const double xa = fma(static_cast<double>(u), h, x0);
         const double xb = fma(static_cast<double>(u + 1), h, x0);
-        const double ea = fma(-fma(xa, xa, 1.0), s, 1.0);
-        const double eb = fma(-fma(xb, xb, 1.0), s, 1.0);
+        const double ea = fma(-fma(xa, xa, 1.0), sd.s, 1.0);
+        const double eb = fma(-fma(xb, xb, 1.0), sd.s, 1.0);
         t1a += ea;
         t1b += eb;
         t2 = fma(ea, ea, t2);
         t2 = fma(eb, eb, t2);
       }
       // sum_u s*(1 + e_u + e_u^2): U*s + s*(sum e + sum e^2)
-      return fma(s, (t1a + t1b) + t2, static_cast<double>(U) * s);
+      return fma(sd.s, (t1a + t1b) + t2, static_cast<double>(U) * sd.s);
     }
   }
 
-  // Hot path of the default kSeries mode: anchored at the tile midpoint x_m, one running
-  // sum per side (e and e^2 folded into the same accumulator), and the tile's
-  // s*(U + sum(e + e^2)) folded into the lane accumulator with a single fma.
-  // Per 32-sample tile: 16 x 7 pair ops + ~12 seed/fold ops.
+  // kSeries tiles are anchored at their midpoint; the lane loop passes x_m directly.
   template <int U, DivMode M>
   __device__ static constexpr double anchor() {
     return M == DivMode::kSeries ? 0.5 * (U - 1) : 0.0;
   }
+
   template <int U, DivMode M>
   __device__ __forceinline__ double tile_acc(double xa, double h, double acc) const {
     if constexpr (M == DivMode::kSeries) {
-      const Seed sd = seed(xa, h);
-      double ta = 0.0, tb = 0.0;
-      // c_j = e_m + k_j^2 B advanced by the exact integer step k_{j+1}^2 - k_j^2 = 2j + 2
-      // (a literal operand of an in-place v_fmac: c_j is dead once e_{+-k_j} are formed),
-      // so only k_j needs an SGPR pair: 32 SGPRs instead of 64 keeps the kernel at 7
-      // resident workgroups per CU. The recurrence's rounding (|c| ~ 1e-8, 15 steps) stays
-      // below 1e-22 absolute.
-      double c = fma(0.25, sd.b, sd.em);
+      static_assert(U == kSeriesTile, "series tiles are kSubs sub-tiles of kSub samples");
+      const Seed sd = seed_half(xa, h);
+      // One running sum for the whole tile, started at the tile's U * 3/4. Its rounding
+      // (ulp(64) ~ 1.4e-14) is far below the lane accumulator's it is folded into (~1.5e3
+      // after 30 tiles, ulp 2.3e-13); a single chain is fine at 8 waves per SIMD.
+      double t = 0.75 * U;
 #pragma unroll
-      for (int j = 0; j < U / 2; ++j) {
-        static_assert(U / 2 <= kPairs, "tile larger than the pair table");
-        const double k = pk[j];
-        const double ep = fma(k, sd.a, c);   // sample u = U/2 + j
-        const double en = fma(-k, sd.a, c);  // sample u = U/2 - 1 - j
-        ta += ep;
-        ta = fma(ep, ep, ta);
-        tb += en;
-        tb = fma(en, en, tb);
-        if (j + 1 < U / 2) c = fma(static_cast<double>(2 * j + 2), sd.b, c);
+      for (int q = 0; q < kSubs; ++q) {
+        const double eh = centre_g(sd, q);     // 1/2 + e at the centre (+ mean k^2 B)
+        const double a = centre_slope(sd, q);  // slope there
+#pragma unroll
+        for (int j = 0; j < kPairs; ++j) {
+          const double c = fma(pk2[j], sd.b, eh);
+          const double gp = fma(pk[j], a, c);   // sample kSub/2 + j of the sub-tile
+          const double gn = fma(-pk[j], a, c);  // sample kSub/2 - 1 - j
+          t = fma(gp, gp, t);
+          t = fma(gn, gn, t);
+          // Keep program order (empty asm, no instructions): left free, the scheduler
+          // hoists and interleaves the sub-tiles' independent chains and, with all of
+          // them live, trades the 3-operand v_fma_f64 for v_fmac_f64 + v_mov_b64 copies.
+          asm volatile("" : "+v"(t));
+        }
       }
-      return fma(sd.s, (ta + tb) + static_cast<double>(U), acc);
+      return fma(sd.s, t, acc);
     } else {
       return acc + tile<U, M>(xa, h);
     }
+  }
+
+  // Series value of sample u of a full tile, by exactly the operations tile_acc applies to
+  // it (validation kernel): s * (3/4 + g_u^2).
+  __device__ __forceinline__ double series_point(double xm, double h, int u) const {
+    const Seed sd = seed_half(xm, h);
+    const int q = u / kSub, w = u % kSub;
+    const double eh = centre_g(sd, q);
+    const double a = centre_slope(sd, q);
+    const int j = w >= kSub / 2 ? w - kSub / 2 : kSub / 2 - 1 - w;
+    const double c = fma(pk2[j], sd.b, eh);
+    const double g = w >= kSub / 2 ? fma(pk[j], a, c) : fma(-pk[j], a, c);
+    return sd.s * fma(g, g, 0.75);
   }
 };
 

@@ -17,11 +17,12 @@ namespace miint {
 enum class DType : int { kF64 = 0, kF32 = 1 };
 
 // Tile (unroll) size of the Riemann kernels: U consecutive samples per lane per step.
-constexpr int kRiemannTile = 32;
+constexpr int kRiemannTile = 32;     // default samples per lane tile (Pi4 series: 64)
 constexpr int kRiemannBlock = 256;
+constexpr int kSeriesHalfSpan = 32;  // max |sample offset| from a Pi4 series seed, in steps
 
 // True when the fp64 Pi4 series reciprocal is exact to fp64 for this h (see integrands.hpp).
-inline bool series_ok(double h) { return 0.5 * kRiemannTile * (h < 0 ? -h : h) <= 2e-6; }
+inline bool series_ok(double h) { return kSeriesHalfSpan * (h < 0 ? -h : h) <= 2e-6; }
 
 // Division mode actually used for step h: the series paths fall back to IEEE division when
 // the tile span is too coarse for the truncated series to be exact to fp64.

@@ -6,7 +6,8 @@
 //   riemann_sum    riemann.cpp:29-44    — serial host loop, int counter (overflows >2^31).
 //
 // Design (MI355X-first):
-//   * Work unit = a tile of U=32 consecutive samples owned by one lane. Tiles are dealt
+//   * Work unit = a tile of T consecutive samples owned by one lane (T = 32, or 64 for the
+//     Pi4 series path: F::tile_len<M>()). Tiles are dealt
 //     grid-stride over 64-bit indices, so N = 1e10+ is fine (fixes SURVEY B9) and every
 //     launch fills all 256 CUs x 8 waves/SIMD regardless of N.
 //   * Sample coordinates are formed from the integer index every tile
@@ -26,7 +27,6 @@
 namespace miint {
 namespace {
 
-constexpr int U = kRiemannTile;
 constexpr int B = kRiemannBlock;
 
 // Wave-uniform 64-bit value read from one lane (two 32-bit v_readlane).
@@ -44,20 +44,22 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
 //    a round costs one v_add_f64 + one v_fma_f64 for its coordinate.
 template <DivMode M, class F>
 __device__ __forceinline__ double lane_sum(const RiemannParams& p, const F& f) {
+  constexpr int T = F::template tile_len<M>();
   const uint64_t lanes = static_cast<uint64_t>(gridDim.x) * B;
   const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * B + threadIdx.x;
-  const uint64_t ntile = p.n / U;
+  const uint64_t ntile = p.n / T;
   const uint64_t rounds = gid < ntile ? (ntile - 1 - gid) / lanes + 1 : 0;
   const uint64_t r_all = readlane_u64(rounds, kWave - 1);  // lane 63 has the fewest rounds
   const uint64_t r_any = readlane_u64(rounds, 0);          // lane 0 the most (<= r_all + 1)
   const double base = static_cast<double>(p.i_begin) + p.off;
-  const double istep = static_cast<double>(lanes * U);
-  double ib = base + static_cast<double>(gid * U) + F::template anchor<U, M>();
+  const double istep = static_cast<double>(lanes * T);
+  double ib = base + static_cast<double>(gid * T) + F::template anchor<T, M>();
   double acc = 0.0;
   uint64_t r = 0;
-  for (; r < r_all; ++r, ib += istep) acc = f.template tile_acc<U, M>(fma(ib, p.h, p.a), p.h, acc);
-  if (r < r_any && r < rounds) acc = f.template tile_acc<U, M>(fma(ib, p.h, p.a), p.h, acc);
-  const uint64_t done = ntile * U;
+  for (; r < r_all; ++r, ib += istep) acc = f.template tile_acc<T, M>(fma(ib, p.h, p.a), p.h, acc);
+  if (r < r_any && r < rounds) acc = f.template tile_acc<T, M>(fma(ib, p.h, p.a), p.h, acc);
+  // remainder (< T samples): one per lane; T <= 64 <= lanes of any grid
+  const uint64_t done = ntile * T;
   if (gid < p.n - done) acc += f.point(fma(base + static_cast<double>(done + gid), p.h, p.a));
   return acc;
 }
@@ -268,33 +270,29 @@ __global__ __launch_bounds__(B) void riemann_fused_kernel(RiemannParams p, const
 template <DivMode M, class F>
 __global__ __launch_bounds__(B) void point_values_kernel(RiemannParams p, const double* table,
                                                          int table_n, double* out) {
+  constexpr int T = F::template tile_len<M>();
   __shared__ double lds[Maker<F>::kLds];
   const F f = Maker<F>::make(p, table, table_n, lds);
   const uint64_t t = static_cast<uint64_t>(blockIdx.x) * B + threadIdx.x;
-  if (t * U >= p.n) return;
-  const double x0 = fma(static_cast<double>(p.i_begin) + p.off + static_cast<double>(t * U),
+  if (t * T >= p.n) return;
+  const double x0 = fma(static_cast<double>(p.i_begin) + p.off + static_cast<double>(t * T),
                         p.h, p.a);
-  const double xm = fma(0.5 * (U - 1), p.h, x0);
-  for (int u = 0; u < U && t * U + u < p.n; ++u) {
+  const double xm = fma(0.5 * (T - 1), p.h, x0);
+  const bool full = (t + 1) * T <= p.n;  // a partial tile is summed point by point
+  for (int u = 0; u < T && t * T + u < p.n; ++u) {
     const double x = fma(static_cast<double>(u), p.h, x0);
     double v;
-    if constexpr (M != DivMode::kIeee && __is_same(F, Pi4)) {
+    if constexpr (M == DivMode::kSeries && __is_same(F, Pi4)) {
+      // exactly the operations Pi4::tile_acc applies to sample u
+      v = full ? f.series_point(xm, p.h, u) : f.point(x);
+    } else if constexpr (M == DivMode::kSeriesDirect && __is_same(F, Pi4)) {
       const Pi4::Seed sd = Pi4::seed(xm, p.h);
-      double e;
-      if constexpr (M == DivMode::kSeries) {  // exactly the pair evaluation of Pi4::tile_acc
-        const int j = u >= U / 2 ? u - U / 2 : U / 2 - 1 - u;
-        const double k = j + 0.5;
-        double c = fma(0.25, sd.b, sd.em);
-        for (int q = 0; q < j; ++q) c = fma(static_cast<double>(2 * q + 2), sd.b, c);
-        e = u >= U / 2 ? fma(k, sd.a, c) : fma(-k, sd.a, c);
-      } else {
-        e = fma(-fma(x, x, 1.0), sd.s, 1.0);
-      }
+      const double e = fma(-fma(x, x, 1.0), sd.s, 1.0);
       v = fma(sd.s, e + e * e, sd.s);
     } else {
       v = f.point(x);
     }
-    out[t * U + u] = v * F::kScale;
+    out[t * T + u] = v * F::kScale;
   }
 }
 
@@ -345,7 +343,8 @@ template <DivMode M, class F> struct FusedOp {
 template <DivMode M, class F> struct PointsOp {
   static void run(const RiemannParams& p, const double* table, int table_n, double* out,
                   hipStream_t stream) {
-    const uint64_t ntile = (p.n + U - 1) / U;
+    constexpr int T = F::template tile_len<M>();
+    const uint64_t ntile = (p.n + T - 1) / T;
     const int grid = static_cast<int>((ntile + B - 1) / B);
     point_values_kernel<M, F><<<grid, B, 0, stream>>>(p, table, table_n, out);
   }

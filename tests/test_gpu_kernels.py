@@ -63,15 +63,22 @@ def test_rank_slices_sum_to_whole(cuda):
     assert math.fsum(parts) == pytest.approx(whole, rel=1e-14)
 
 
-def test_pi4_series_per_point_accuracy(cuda):
-    """The series reciprocal evaluates every sample to fp64 accuracy (<= 2 ulp vs IEEE)."""
+@pytest.mark.parametrize("n", [10**9, 17_000_000])
+def test_pi4_series_per_point_accuracy(cuda, n):
+    """Every sample of the series path against IEEE division, in units of ulp(IEEE value):
+    <= 5 ulp and >= 95 % within 2 ulp (whole domain: 91 % within 1, 99.4 % within 2; see
+    tools/ulp_probe.py). Also at the coarsest step the series path accepts (32 h <= 2e-6:
+    n >= 1.6e7 on [0, 1]). Per point, g = 1/2 + e is rounded at ulp(1/2) scale, and the IEEE
+    reference rounds every coordinate x0 + u h (the series uses exact offsets), so window
+    means are not a bias measure; the sum-level check is test_series_equals_ieee_sum."""
     spec = integrands.pi4()
-    n = 10**9
-    for i0 in (0, 123_456_789, 999_000_000):
+    for i0 in (0, n // 8 + 12_345, n - (1 << 16)):
         v = kernels.point_values(spec, n, rule="left", div="series", i_begin=i0, n_local=1 << 16)
         w = kernels.point_values(spec, n, rule="left", div="ieee", i_begin=i0, n_local=1 << 16)
-        ulp = torch.abs(v - w) / (torch.finfo(torch.float64).eps * torch.abs(w))
-        assert float(ulp.max()) <= 2.0
+        spacing = torch.nextafter(w.abs(), torch.full_like(w, math.inf)) - w.abs()
+        u = (v - w) / spacing
+        assert float(u.abs().max()) <= 5.0
+        assert float((u.abs() <= 2.0).double().mean()) >= 0.95
 
 
 def test_pi4_1e9_left_error_is_truncation(cuda):
@@ -81,14 +88,17 @@ def test_pi4_1e9_left_error_is_truncation(cuda):
 
 def test_pi4_1e9_mid_error(cuda):
     v = float(kernels.riemann(integrands.pi4(), 10**9, rule="mid").item())
-    assert abs(v - math.pi) < 1e-13
+    assert abs(v - math.pi) < 2e-15  # measured 4.4e-16 (2 ulp of pi)
 
 
-def test_series_equals_ieee_sum(cuda):
+@pytest.mark.parametrize("n", [17_000_000, 10**8, 10**9])
+def test_series_equals_ieee_sum(cuda, n):
+    """The whole sum: series vs correctly rounded division agree to fp64 resolution, i.e.
+    the series path's per-point rounding carries no bias into the result."""
     spec = integrands.pi4()
-    a = float(kernels.riemann(spec, 10**8, div="series").item())
-    b = float(kernels.riemann(spec, 10**8, div="ieee").item())
-    assert a == pytest.approx(b, rel=1e-14)
+    a = float(kernels.riemann(spec, n, div="series").item())
+    b = float(kernels.riemann(spec, n, div="ieee").item())
+    assert a == pytest.approx(b, rel=1e-15, abs=0)
 
 
 def test_fp32_error_vs_fp64(cuda):

@@ -4,8 +4,10 @@
 Metric and config come from BASELINE.json ("Riemann subintervals/sec at N=1e9 fp64; |error|
 vs analytic pi"). One step = one complete integration of N samples per GPU: gfx950 kernel
 (every sample evaluated, fp64) -> in-kernel DPP/LDS/ticket reduction -> RCCL all-reduce of
-the per-GPU partial over xGMI -> 8-byte D2H into pinned memory. Steps are hipGraph replays;
-with >1 GPU the all-reduce of step k overlaps the compute of step k+1 (separate streams).
+the per-GPU partial over xGMI -> D2H into pinned memory. Steps are hipGraph replays of
+batches of 16; with >1 GPU each batch ends in ONE all-reduce of its 16 step results
+(bucketed: every step still gets its own global sum; --no-bucket = one 8-byte all-reduce
+per step, overlapped on a side stream).
 
 Weak scaling: every GPU integrates its own 1e9-sample slice of a global N = 1e9 x n_gpus
 (N = 8e9 on 8 GPUs). The result of every timed step is checked on the host against pi.
@@ -49,6 +51,8 @@ def parse() -> argparse.Namespace:
     p.add_argument("--no-pipeline", action="store_true")
     p.add_argument("--unfused", action="store_true", help="partials + finalize (2 launches)")
     p.add_argument("--grid", type=int, default=0)
+    p.add_argument("--no-bucket", action="store_true",
+                   help="one all-reduce per step instead of one per graph batch of steps")
     p.add_argument("--force-collective", action="store_true",
                    help="run the RCCL all-reduce stage even on 1 GPU (tests the multi-GPU graph)")
     p.add_argument("--verbose", action="store_true")
@@ -80,7 +84,8 @@ def main() -> int:
     use_torch = args.comm == "torch" and world > 1
     integ = Integrator(args.integrand, n=n_total, rule=args.rule, dtype=args.dtype, div=args.div,
                        backend="hip", ctx=ctx, comm=args.comm, fused=not args.unfused,
-                       grid=args.grid, force_collective=args.force_collective)
+                       grid=args.grid, force_collective=args.force_collective,
+                       bucket=not args.no_bucket)
     plan = integ.plan
     graphs = not args.no_graph and not use_torch
     pipeline = not args.no_pipeline and (world > 1 or args.force_collective)
@@ -163,6 +168,7 @@ def main() -> int:
                 "graphs": graphs,
                 "graph_nodes": plan.graph_nodes if graphs else 0,
                 "pipeline": pipeline,
+                "bucketed_allreduce": bool(plan.bucketed),
                 "fused_reduction": not args.unfused,
                 "grid": plan.grid,
             },

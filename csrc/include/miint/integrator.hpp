@@ -47,7 +47,11 @@ struct RiemannConfig {
                                // keeps <= 80 SGPRs for this): the default grid is one full wave
   bool fused = true;           // one launch (ticket reduction) vs partials + finalize
   bool host_direct = true;     // world == 1: kernel stores the result into pinned memory
-  int slots = 8;               // steps per graph batch = result ring depth
+  int slots = 16;              // steps per graph batch = result ring depth
+  bool bucket = true;          // collective: ONE all-reduce of a batch's `slots` step results
+                               // (every step still gets its own global sum) instead of one
+                               // 8-byte all-reduce per step (~18 us each, not hidden: the
+                               // kernels hold every CU slot the RCCL kernel would need)
   int rank = 0, world = 1;     // slice of [0, n) when no communicator is given (e.g. the
                                // torch.distributed path reduces results itself)
   bool force_collective = false;  // run the RCCL stage even with a 1-rank communicator
@@ -113,6 +117,7 @@ class RiemannPlan {
   // replays (results of step k in host slot k % slots), remainder enqueued directly.
   // graphs=false: direct enqueue (result of step k in host slot k % host_capacity); with
   // pipeline=true and world > 1 the reduce/copy of step k overlaps compute of step k+1.
+  // bucketed(): batches of `slots` steps, one all-reduce each, host slot k % slots.
   StepTiming run_steps(int steps, bool pipeline, bool graphs);
   // The same without synchronisation (bench.py brackets it with its own barrier + device
   // synchronize); call sync() before reading host results.
@@ -123,8 +128,9 @@ class RiemannPlan {
   hipStream_t compute_stream() const { return compute_.get(); }
   hipStream_t comm_stream() const { return comm_stream_.get(); }
 
-  // True when this plan runs an RCCL reduction per step.
+  // True when this plan runs an RCCL reduction of its step results.
   bool collective() const { return comm_ && (world_ > 1 || cfg_.force_collective); }
+  bool bucketed() const { return collective() && cfg_.bucket; }
 
  private:
   void enqueue_batch(hipStream_t cs, hipStream_t rs, int nsteps, bool overlap);

@@ -116,10 +116,18 @@ struct Pi4F32 : TileDefaults<Pi4F32> {
     }
   }
 
-  // Default series path, midpoint-anchored: the pair residuals (e_{+k}, e_{-k}) =
-  // c_k + (k, -k) * A are exactly one v_pk_fma_f32 (x = +k side, y = -k side), summed with
-  // one v_pk_add_f32; c_k advances by the exact step (2j+2) B. In fp32 the e^2 term
-  // (< 3e-16) is far below the format's 6e-8 and is not carried. 1.5 VALU per sample.
+  // Default series path, midpoint-anchored, 64-sample tiles of two 32-sample sub-tiles
+  // (centres at -16 and +16 steps; e_c = e_m + c0 A + c0^2 B, A' = A + 2 c0 B: one seed per
+  // 64 samples). The pair residuals (e_{+k}, e_{-k}) = c_k + (k, -k) * A' are one
+  // v_pk_fma_f32 (op_sel broadcasts c_k), summed by one v_pk_add_f32, and the shared c_k of
+  // TWO consecutive pairs advance together by one v_pk_fma_f32 with the exact steps
+  // (k_{j+2}^2 - k_j^2, k_{j+3}^2 - k_{j+1}^2) = (4j+6, 4j+10) times B: 1.25 VALU per sample.
+  // In fp32 the e^2 term (< 3e-16) is far below the format's 6e-8 and is not carried.
+  static constexpr int kSubLen = 32;
+  template <DivMode M>
+  __host__ __device__ static constexpr int tile_len() {
+    return M == DivMode::kSeries ? 2 * kSubLen : 32;
+  }
   template <int UU, DivMode M>
   __device__ static constexpr double anchor() {
     return M == DivMode::kSeries ? 0.5 * (UU - 1) : 0.0;
@@ -127,6 +135,7 @@ struct Pi4F32 : TileDefaults<Pi4F32> {
   template <int UU, DivMode M>
   __device__ __forceinline__ double tile_acc(double xmd, double h, double acc) const {
     if constexpr (M == DivMode::kSeries) {
+      static_assert(UU == 2 * kSubLen, "fp32 series tiles are two 32-sample sub-tiles");
       const float xm = static_cast<float>(xmd);
       const float hf = static_cast<float>(h);
       const float dm = fmaf(xm, xm, 1.0f);
@@ -135,15 +144,25 @@ struct Pi4F32 : TileDefaults<Pi4F32> {
       const float em = fmaf(-dm, s, 1.0f);
       const float a = (-2.0f * hf) * xm * s;
       const float b = -(hf * hf) * s;
-      const f32x2 av = {a, a};
-      float c = fmaf(0.25f, b, em);
-      f32x2 t = {0.0f, 0.0f};
+      const f32x2 bb = {b, b};
+      f32x2 t;
 #pragma unroll
-      for (int j = 0; j < UU / 2; ++j) {
-        const f32x2 kk = {j + 0.5f, -(j + 0.5f)};
-        const f32x2 cc = {c, c};
-        t += pk_fma(kk, av, cc);  // (e_{+k}, e_{-k})
-        if (j + 1 < UU / 2) c = fmaf(static_cast<float>(2 * j + 2), b, c);
+      for (int q = 0; q < 2; ++q) {
+        const float c0 = q == 0 ? -0.5f * kSubLen : 0.5f * kSubLen;
+        const float ec = fmaf(c0, fmaf(c0, b, a), em);
+        const float aq = fmaf(2.0f * c0, b, a);
+        const f32x2 av = {aq, aq};
+        f32x2 cc = {fmaf(0.25f, b, ec), fmaf(2.25f, b, ec)};  // (c_0, c_1)
+#pragma unroll
+        for (int j = 0; j < kSubLen / 2; j += 2) {
+          const f32x2 k0 = {j + 0.5f, -(j + 0.5f)};
+          const f32x2 k1 = {j + 1.5f, -(j + 1.5f)};
+          const f32x2 e0 = pk_fma(k0, av, f32x2{cc.x, cc.x});  // (e_{+k_j}, e_{-k_j})
+          t = (q == 0 && j == 0) ? e0 : t + e0;
+          t += pk_fma(k1, av, f32x2{cc.y, cc.y});  // (e_{+k_{j+1}}, e_{-k_{j+1}})
+          if (j + 2 < kSubLen / 2)
+            cc = pk_fma(f32x2{4.0f * j + 6.0f, 4.0f * j + 10.0f}, bb, cc);
+        }
       }
       // tile value in fp32 (the path's precision); lanes accumulate tiles in fp64
       return acc + static_cast<double>(s * (static_cast<float>(UU) + (t.x + t.y)));
@@ -209,11 +228,35 @@ __global__ __launch_bounds__(B) void riemann_kernel(RiemannParams p, const doubl
 // Same width and order as the fused kernel's last-workgroup sum (B threads, partial i
 // folded into thread i % B in increasing i), so both paths are bitwise identical.
 constexpr int kFinalBlock = B;
+constexpr int kFinalBatch = 16;  // loads in flight per thread (grid <= 4096: one batch)
+
+// Thread t sums partials t, t + B, t + 2B, ... in increasing order — the same order for
+// both paths. The loads of a batch are all issued before the first add: as a plain loop
+// every iteration waited for its load (s_waitcnt vmcnt(0)), i.e. grid/B serial memory round
+// trips (8 at grid 2048) at the end of every integration (~25 us at small N, measured).
+template <bool AGENT_SCOPE>
+__device__ __forceinline__ double ordered_partials(const double* partials, int n) {
+  double v = 0.0;
+  for (int base = 0; base < n; base += kFinalBatch * kFinalBlock) {
+    double r[kFinalBatch];
+#pragma unroll
+    for (int k = 0; k < kFinalBatch; ++k) {
+      const int i = base + k * kFinalBlock + static_cast<int>(threadIdx.x);
+      if constexpr (AGENT_SCOPE)
+        r[k] = i < n ? __hip_atomic_load(&partials[i], __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT)
+                     : 0.0;
+      else
+        r[k] = i < n ? partials[i] : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < kFinalBatch; ++k) v += r[k];
+  }
+  return v;
+}
 
 __device__ __forceinline__ double ordered_sum(const double* partials, int n, double* red) {
-  double v = 0.0;
-  for (int i = threadIdx.x; i < n; i += kFinalBlock) v += partials[i];
-  return block_sum<kFinalBlock>(v, red);
+  return block_sum<kFinalBlock>(ordered_partials<false>(partials, n), red);
 }
 
 __global__ __launch_bounds__(kFinalBlock) void finalize_kernel(const double* partials, int n,
@@ -254,9 +297,7 @@ __global__ __launch_bounds__(B) void riemann_fused_kernel(RiemannParams p, const
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  double v = 0.0;
-  for (int i = threadIdx.x; i < static_cast<int>(gridDim.x); i += B)
-    v += __hip_atomic_load(&partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const double v = ordered_partials<true>(partials, static_cast<int>(gridDim.x));
   const double tot = block_sum<B>(v, red + 0);
   if (threadIdx.x == 0) {
     out[0] = tot * scale;

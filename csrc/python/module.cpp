@@ -136,6 +136,7 @@ PYBIND11_MODULE(_miint, m) {
       .def_readwrite("waves_per_cu", &RiemannConfig::waves_per_cu)
       .def_readwrite("fused", &RiemannConfig::fused)
       .def_readwrite("slots", &RiemannConfig::slots)
+      .def_readwrite("bucket", &RiemannConfig::bucket)
       .def_readwrite("rank", &RiemannConfig::rank)
       .def_readwrite("world", &RiemannConfig::world)
       .def_readwrite("force_collective", &RiemannConfig::force_collective)
@@ -177,6 +178,7 @@ PYBIND11_MODULE(_miint, m) {
       .def("host_result", &RiemannPlan::host_result)
       .def_property_readonly("host_capacity", &RiemannPlan::host_capacity)
       .def_property_readonly("slots", &RiemannPlan::slots)
+      .def_property_readonly("bucketed", &RiemannPlan::bucketed)
       .def_property_readonly("direct", &RiemannPlan::direct)
       .def_property_readonly("graph_nodes", &RiemannPlan::graph_nodes)
       .def_property_readonly("graphs_ready", &RiemannPlan::graphs_ready)

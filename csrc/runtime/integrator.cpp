@@ -121,6 +121,13 @@ double RiemannPlan::run() {
 // overlap), the reduce+copy chain runs on `rs` behind per-step events: a fork/join that
 // hipStreamBeginCapture turns into graph edges.
 void RiemannPlan::enqueue_batch(hipStream_t cs, hipStream_t rs, int nsteps, bool overlap) {
+  if (bucketed()) {  // nsteps kernels, then one all-reduce + one copy of all their results
+    for (int j = 0; j < nsteps; ++j) enqueue_compute(cs, j, j);
+    comm_->allreduce_sum(result_.get(), result_.get(), static_cast<size_t>(nsteps), cs);
+    MIINT_HIP(hipMemcpyAsync(host_.get(), result_.get(), sizeof(double) * nsteps,
+                             hipMemcpyDeviceToHost, cs));
+    return;
+  }
   if (!overlap || direct_ || !collective()) {
     for (int j = 0; j < nsteps; ++j) enqueue(cs, j, j);
     return;
@@ -163,7 +170,7 @@ bool RiemannPlan::use_graphs(bool requested) {
 }
 
 int RiemannPlan::host_index_of(int k, bool graphs) const {
-  return (graphs && batch_) ? k % cfg_.slots : k % host_capacity();
+  return ((graphs && batch_) || bucketed()) ? k % cfg_.slots : k % host_capacity();
 }
 
 void RiemannPlan::launch_steps(int steps, bool pipeline, bool graphs) {
@@ -175,6 +182,10 @@ void RiemannPlan::launch_steps(int steps, bool pipeline, bool graphs) {
   if (use_graphs(graphs)) {
     for (int b = 0; b < steps / S; ++b) batch_->launch(cs);
     if (steps % S) enqueue_batch(cs, rs, steps % S, pipeline);
+    return;
+  }
+  if (bucketed()) {
+    for (int k = 0; k < steps; k += S) enqueue_batch(cs, rs, std::min(S, steps - k), false);
     return;
   }
   const bool overlap = pipeline && !direct_ && collective();

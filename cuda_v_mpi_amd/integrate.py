@@ -61,8 +61,9 @@ class Integrator:
     def __init__(self, integrand: str | integrands.IntegrandSpec = "pi4", n: int = 10**9,
                  rule: str = "left", dtype: str = "fp64", div: str = "series",
                  backend: str = "hip", ctx: DistContext | None = None, comm: str = "native",
-                 fused: bool = True, grid: int = 0, slots: int = 8, a: float | None = None,
-                 b: float | None = None, force_collective: bool = False, **spec_kw):
+                 fused: bool = True, grid: int = 0, slots: int = 16, a: float | None = None,
+                 b: float | None = None, force_collective: bool = False, bucket: bool = True,
+                 **spec_kw):
         spec = integrands.get(integrand, **spec_kw) if isinstance(integrand, str) else integrand
         if a is not None or b is not None:
             spec = dataclasses.replace(spec, a=spec.a if a is None else a,
@@ -96,6 +97,7 @@ class Integrator:
             cfg.table = spec.native_table()
             cfg.grid, cfg.fused, cfg.slots = grid, fused, slots
             cfg.force_collective = force_collective
+            cfg.bucket = bucket
             if (self.ctx.world > 1 or force_collective) and comm == "native":
                 self._comm = native_comm(self.ctx)
                 self._plan = m.RiemannPlan(cfg, self.ctx.device, self._comm)

@@ -32,19 +32,22 @@ def test_plan_steps_graph_and_plain_agree(cuda, graphs, fused):
     assert it.plan.host_result(it.plan.host_index_of(8, graphs)) == one
 
 
+@pytest.mark.parametrize("bucket", [True, False])
 @pytest.mark.parametrize("graphs", [False, True])
-def test_plan_rccl_stage_on_one_gpu(cuda, graphs):
-    """The multi-GPU step (kernel -> RCCL allreduce on the comm stream -> memcpy to pinned,
-    fork/join-captured in a graph) run with a 1-rank communicator."""
+def test_plan_rccl_stage_on_one_gpu(cuda, graphs, bucket):
+    """The multi-GPU step run with a 1-rank communicator: bucketed (a batch of kernels, then
+    ONE RCCL all-reduce of all their results + one copy to pinned) or per step (kernel ->
+    all-reduce on the comm stream -> copy, fork/join-captured in a graph). 37 steps = two
+    full batches of 16 and a partial one."""
     base = Integrator("pi4", n=10**8, rule="mid")
     want = base.run().value
-    it = Integrator("pi4", n=10**8, rule="mid", force_collective=True)
-    assert it.plan.collective and not it.plan.direct
-    t = it.run_steps(19, pipeline=True, graphs=graphs)
-    assert t["steps"] == 19
+    it = Integrator("pi4", n=10**8, rule="mid", force_collective=True, bucket=bucket)
+    assert it.plan.collective and not it.plan.direct and it.plan.bucketed == bucket
+    t = it.run_steps(37, pipeline=True, graphs=graphs)
+    assert t["steps"] == 37
     if graphs:
         assert it.plan.graphs_ready, it.plan.graph_error
-    for k in range(11, 19):
+    for k in range(37 - it.plan.slots, 37):
         assert it.plan.host_result(it.plan.host_index_of(k, graphs)) == want
 
 
@@ -157,12 +160,14 @@ def test_bench_two_ranks_shared_gpu_torch_comm(native, cuda):
     assert js["n_gpus"] == 2 and js["config"]["N"] == 400_000_000 and js["verified"]
 
 
-def test_bench_force_collective_graph(native, cuda):
-    p = _run(["python", os.path.join(REPO, "bench.py"), "--steps", "24", "--warmup", "8",
-              "--force-collective"])
+@pytest.mark.parametrize("bucket", [True, False])
+def test_bench_force_collective_graph(native, cuda, bucket):
+    p = _run(["python", os.path.join(REPO, "bench.py"), "--steps", "40", "--warmup", "8",
+              "--force-collective"] + ([] if bucket else ["--no-bucket"]))
     assert p.returncode == 0, p.stderr[-2000:]
     js = json.loads(p.stdout.strip().splitlines()[-1])
     assert js["verified"] and js["config"]["graphs"] and js["config"]["pipeline"]
+    assert js["config"]["bucketed_allreduce"] == bucket
 
 
 def test_bench_contract(native, cuda):

@@ -10,7 +10,7 @@
 // printed element (P=7 -> 0.000000, P=16 -> 117642.707174). --replicate allgathers the full
 // table to every rank like 4main.c:157.
 //
-//   ./trainscan [--gpus G] [--parity] [--replicate] [--no-phase2] [--algo fused|lookback]
+//   ./trainscan [--gpus G] [--parity] [--replicate] [--no-phase2] [--algo onepass|fused|lookback]
 //               [--iters K] [--json]
 #include <cstdio>
 
@@ -29,7 +29,12 @@ int main(int argc, char** argv) {
     cfg.parity = a.flag("parity");
     cfg.replicate = a.flag("replicate");
     cfg.phase2 = !a.flag("no-phase2");
-    cfg.algo = a.str("algo", "fused") == "lookback" ? ScanAlgo::kLookback : ScanAlgo::kFused;
+    const std::string algo = a.str("algo", "fused");
+    MIINT_CHECK(algo == "onepass" || algo == "fused" || algo == "lookback",
+                "--algo must be onepass|fused|lookback");
+    cfg.algo = algo == "fused"      ? ScanAlgo::kFused
+               : algo == "lookback" ? ScanAlgo::kLookback
+                                    : ScanAlgo::kOnePass;
     const int iters = static_cast<int>(a.integer("iters", 1));
     if (topo.rank0 == 0)  // 4main.c:72-74 (tablelen/1800)
       std::printf("Step size of %ld\n", static_cast<long>(cfg.steps_per_sec));

@@ -5,12 +5,18 @@
 // element partition, ships every slice to rank 0, which adds carries serially and
 // broadcasts the 144 MB table; then does it all again for the second integral.
 //
-// Here, per rank (one GPU), two algorithms:
+// Here, per rank (one GPU), three algorithms:
 //   kFused (default)  reduce-then-scan on the *computed* samples (trainscan.hip): per-tile
 //                     sums (compute only) -> one-workgroup tile prefix -> [allgather of one
 //                     {T1, T2, count} triple per rank -> rank carries] -> one write-only pass
 //                     that emits both the running integral and its running integral.
 //                     HBM traffic: 16 B per sample, written once.
+//   kOnePass          the same outputs in ONE pass: samples generated once, local two-level
+//                     scan, decoupled look-back over the tile state {sum v, sum of local
+//                     running integral}, write-only vel/pos. Measured slower on MI355X
+//                     (103 us vs 66 us for 18e6 samples): each 33 KB-LDS workgroup (4 per CU)
+//                     holds its slot through cross-XCD sc1 look-back round trips before it
+//                     can write. With world > 1 the rank totals are needed first: kFused.
 //   kLookback         the general single-pass decoupled look-back scan (scan.hip), used as
 //                     phase-1 interp+scan and phase-2 scan, with an allgather + carry add per
 //                     phase (48 B per sample of traffic).
@@ -29,7 +35,7 @@
 
 namespace miint {
 
-enum class ScanAlgo : int { kFused = 0, kLookback = 1 };
+enum class ScanAlgo : int { kFused = 0, kLookback = 1, kOnePass = 2 };
 
 struct TrainScanConfig {
   int steps_per_sec = 10000;  // 4main.c:26
@@ -56,6 +62,8 @@ struct TrainScanKernelParams {
   uint64_t n;           // samples in the slice
   uint64_t win_lo, win_hi;  // samples outside [win_lo, win_hi) are zero (parity fills)
 };
+// Workspace of the fused/one-pass kernels: must be zero-filled once at allocation (tickets
+// live in it and every launch leaves them re-armed).
 size_t trainscan_workspace_bytes(uint64_t n);
 // K1 + K2: per-tile sums and tile prefixes into `ws`; totals[0..1] = {T1, T2} (device).
 void launch_trainscan_local(const TrainScanKernelParams& p, void* ws, double* totals,
@@ -66,6 +74,11 @@ void launch_trainscan_rank_carry(const double* gathered, int rank, double* carri
 // K4: write vel (running integral) and pos (its running integral); carries may be null.
 void launch_trainscan_write(const TrainScanKernelParams& p, const void* ws, const double* carries,
                             double* vel, double* pos, hipStream_t s);
+// One pass (K1 + K2 + K4 with a decoupled look-back): vel, pos and totals {T1, T2}.
+void launch_trainscan_onepass(const TrainScanKernelParams& p, void* ws, double* vel, double* pos,
+                              double* totals, hipStream_t s);
+// Nonzero if a one-pass look-back spin gave up (reads the workspace header; synchronises).
+unsigned trainscan_onepass_timeout(const void* ws, hipStream_t s);
 
 class TrainScan {
  public:
@@ -74,6 +87,7 @@ class TrainScan {
   // Enqueue one complete pipeline on the plan's stream without synchronising.
   void enqueue();
   uint64_t total() const { return total_; }
+  ScanAlgo algo() const { return cfg_.algo; }  // effective (kOnePass -> kFused when world > 1)
   uint64_t local_begin() const { return begin_; }
   uint64_t local_count() const { return count_; }
   const double* velocity() const { return vel_.get(); }
@@ -83,6 +97,7 @@ class TrainScan {
 
  private:
   void enqueue_fused(hipStream_t s);
+  void enqueue_onepass(hipStream_t s);
   void enqueue_lookback(hipStream_t s);
   void exchange_carry(const double* slice, uint64_t n, double* slice_out, hipStream_t s);
   double pick_global(const double* slice, uint64_t global_index, hipStream_t s);

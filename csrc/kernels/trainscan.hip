@@ -12,6 +12,9 @@
 //   K2 ts_tile_prefix one workgroup: P1(t) = sum_{u<t} S1(u),
 //                     Q(t) = sum_{u<t} [n_u P1(u) + S2(u)]   (DPP/LDS block scans), and the
 //                     rank totals T1 = P1(end), T2 = Q(end)
+//   (dt = 1/sps)      K1 + K2 as ONE launch, ts_tile_scan_closed: closed-form tile sums (one
+//                     thread per tile), in-block scans, last-workgroup scan of the block
+//                     aggregates; K4 composes block and in-block prefixes (6.8 us vs 22 us)
 //   (multi-GPU)       allgather (T1, T2, count) per rank -> rank carries C1, C2 (K3)
 //   K4 ts_write       per tile: recompute v, vel = C1 + P1(t) + local scan(v),
 //                     pos = C2 + 4096 t C1 + Q(t) + local scan(vel); both transposed through
@@ -21,6 +24,8 @@
 // The 4main --parity fill windows (rank-private fills, 4main.c:76-86) are honoured: samples
 // outside [win_lo, win_hi) are zero.
 #include <hip/hip_runtime.h>
+
+#include <cmath>
 
 #include "miint/common.hpp"
 #include "miint/trainscan.hpp"
@@ -90,9 +95,10 @@ __device__ __forceinline__ int seg_of(double t, int nseg) {
 // Stage only the table entries this tile's samples touch: a 4096-sample tile at 1e4
 // samples/s spans 0.41 s, i.e. 2-3 entries instead of the whole 14.4 KB table per
 // workgroup (the full re-staging cost 63 MB of L2 reads per pass).
-__device__ __forceinline__ Sampler make_sampler(const TrainScanKernelParams& p, double* tab) {
+__device__ __forceinline__ Sampler make_sampler(const TrainScanKernelParams& p, double* tab,
+                                                unsigned tile) {
   const int nseg = p.table_n - 1;
-  const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kTile;
+  const uint64_t t0 = static_cast<uint64_t>(tile) * kTile;
   const uint64_t last = (t0 + kTile < p.n ? t0 + kTile : p.n) - 1;
   const int s0 = seg_of(p.dt * static_cast<double>(p.i0 + t0), nseg);
   const int s1 = seg_of(p.dt * static_cast<double>(p.i0 + last), nseg) + 1;
@@ -107,7 +113,7 @@ __device__ __forceinline__ Sampler make_sampler(const TrainScanKernelParams& p, 
 __global__ __launch_bounds__(kB) void ts_tile_sums(TrainScanKernelParams p, f64x2* sums) {
   __shared__ double tab[kSpan];
   __shared__ double red1[kB / kWave], red2[kB / kWave];
-  const Sampler f = make_sampler(p, tab);
+  const Sampler f = make_sampler(p, tab, blockIdx.x);
   const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kTile;
   const uint64_t nt = p.n - t0 < kTile ? p.n - t0 : kTile;
   double v[kItems];
@@ -125,32 +131,186 @@ __global__ __launch_bounds__(kB) void ts_tile_sums(TrainScanKernelParams p, f64x
 }
 
 // ---------------------------------------------------------------------------- K2
+// One workgroup, a contiguous run of tiles per thread: serial within the thread, then two
+// block scans in total (S1 -> P1, then q = n_t P1 + S2 -> Q). The earlier form scanned
+// chunks of 1024 tiles with two block scans each (7.8 us for 4395 tiles).
 constexpr int kPB = 1024;
 __global__ __launch_bounds__(kPB) void ts_tile_prefix(const f64x2* sums, uint32_t ntiles,
                                                       uint64_t n, f64x2* prefix, double* totals) {
   __shared__ double red[kPB / kWave];
-  double c1 = 0.0, c2 = 0.0;  // running carries over chunks (uniform)
-  for (uint32_t base = 0; base < ntiles; base += kPB) {
-    const uint32_t t = base + threadIdx.x;
-    const f64x2 s = t < ntiles ? sums[t] : f64x2{0.0, 0.0};
+  const uint32_t per = (ntiles + kPB - 1) / kPB;
+  const uint32_t tb = threadIdx.x * per < ntiles ? threadIdx.x * per : ntiles;
+  const uint32_t te = tb + per < ntiles ? tb + per : ntiles;
+  auto count = [&](uint32_t t) {
     const uint64_t t0 = static_cast<uint64_t>(t) * kTile;
-    const double nt = t < ntiles ? static_cast<double>(n - t0 < kTile ? n - t0 : kTile) : 0.0;
-    double tot1;
-    const double incl1 = block_inclusive_scan<kPB>(s.x, red, &tot1);
-    const double p1 = c1 + (incl1 - s.x);  // exclusive prefix of S1
-    __syncthreads();
-    const double q = fma(nt, p1, s.y);
-    double tot2;
-    const double incl2 = block_inclusive_scan<kPB>(q, red, &tot2);
-    if (t < ntiles) prefix[t] = f64x2{p1, c2 + (incl2 - q)};
-    c1 += tot1;
-    c2 += tot2;
-    __syncthreads();
+    return static_cast<double>(n - t0 < kTile ? n - t0 : kTile);
+  };
+  double a = 0.0;
+  for (uint32_t t = tb; t < te; ++t) a += sums[t].x;
+  double tot1;
+  const double base1 = block_inclusive_scan<kPB>(a, red, &tot1) - a;
+  __syncthreads();
+  double q = 0.0, p1 = base1;
+  for (uint32_t t = tb; t < te; ++t) {
+    const f64x2 st = sums[t];
+    q += fma(count(t), p1, st.y);
+    p1 += st.x;
+  }
+  double tot2;
+  const double base2 = block_inclusive_scan<kPB>(q, red, &tot2) - q;
+  double run_p = base1, run_q = base2;
+  for (uint32_t t = tb; t < te; ++t) {
+    const f64x2 st = sums[t];
+    prefix[t] = f64x2{run_p, run_q};
+    run_q += fma(count(t), run_p, st.y);
+    run_p += st.x;
   }
   if (threadIdx.x == 0) {
-    totals[0] = c1;  // T1: slice sum of v
-    totals[1] = c2;  // T2: slice sum of the local running integral
+    totals[0] = tot1;  // T1: slice sum of v
+    totals[1] = tot2;  // T2: slice sum of the local running integral
   }
+}
+
+// ---------------------------------------------------------------------------- K1, closed form
+// When dt = 1/sps for an integer sps, sample i lies in segment s = min(i / sps, nseg - 1) at
+// fr = (i - s sps) dt, so a tile's samples are a few runs of an arithmetic sequence and its
+// sums have closed forms: with j = i - s sps over [ja, jb), m = jb - ja, v = v0 + c j
+// (c = (v1 - v0) dt) and weight n_t - l = W0 - j,
+//   S1 += m v0 + c sum(j),   S2 += W0 m v0 + (W0 c - v0) sum(j) - c sum(j^2).
+// One thread per tile instead of a workgroup re-sampling its 4096 points (14.5 us for 18e6
+// samples). The samples themselves are computed and written by K4 only; the closed form
+// differs from their rounded sum by ~1e-16 relative.
+__device__ __forceinline__ uint64_t div_sps(uint64_t i, uint64_t sps, double inv) {
+  uint64_t q = static_cast<uint64_t>(static_cast<double>(i) * inv);  // exact to +-1
+  if (q * sps > i) --q;
+  else if ((q + 1) * sps <= i) ++q;
+  return q;
+}
+
+__device__ __forceinline__ f64x2 tile_sums_closed(const TrainScanKernelParams& p, uint64_t sps,
+                                                  double inv_sps, uint64_t t) {
+  const int64_t nseg = p.table_n - 1;
+  const uint64_t g0 = t * kTile;
+  const uint64_t g1 = g0 + kTile < p.n ? g0 + kTile : p.n;
+  const uint64_t it0 = p.i0 + g0;  // global index of the tile's first sample
+  uint64_t ia = it0 > p.win_lo ? it0 : p.win_lo;
+  const uint64_t ib = p.i0 + g1 < p.win_hi ? p.i0 + g1 : p.win_hi;
+  double s1 = 0.0, s2 = 0.0;
+  while (ia < ib) {
+    int64_t sg = static_cast<int64_t>(div_sps(ia, sps, inv_sps));
+    if (sg > nseg - 1) sg = nseg - 1;
+    const uint64_t base = static_cast<uint64_t>(sg) * sps;
+    const uint64_t end = (sg == nseg - 1 || base + sps > ib) ? ib : base + sps;
+    const double ja = static_cast<double>(ia - base), jb = static_cast<double>(end - base);
+    const double m = jb - ja;
+    const double sj = 0.5 * m * (ja + jb - 1.0);
+    // sum_{ja <= j < jb} j^2 via (x-1) x (2x-1) / 6 (exact integers below 2^53)
+    auto sq = [](double x) { return (x - 1.0) * x * (2.0 * x - 1.0); };
+    const double sj2 = (sq(jb) - sq(ja)) * (1.0 / 6.0);
+    const double v0 = p.table[sg];
+    const double c = (p.table[sg + 1] - v0) * p.dt;
+    const double w0 = static_cast<double>(static_cast<int64_t>(g1 - g0) +
+                                          static_cast<int64_t>(it0) - static_cast<int64_t>(base));
+    s1 += fma(c, sj, m * v0);
+    s2 += fma(fma(w0, c, -v0), sj, w0 * m * v0) - c * sj2;
+    ia = end;
+  }
+  return f64x2{s1, s2};
+}
+
+// K1 + K2 in one launch: thread t computes tile t's closed-form sums; the block scans its
+// 256 tiles (local[t] = in-block exclusive {P1, Q}) and publishes its aggregate {A, B, N}
+// (sc1 stores, drain, agent-scope ticket); the block drawing the last ticket acquires and
+// scans the block aggregates into block prefixes {PB, QB} and the slice totals. K4 composes
+// P1(t) = PB + P1l(t), Q(t) = QB + (t mod 256) 4096 PB + Ql(t). The former one-workgroup
+// K2 took 7.8-8.7 us of serial memory latency for 4395 tiles.
+struct ClosedScan {
+  f64x2* local;      // per tile, in-block exclusive {P1, Q}
+  f64x2* blockpre;   // per block, exclusive {PB, QB}
+  double* agg;       // per block {A, B, N} (stride 4 doubles)
+  unsigned* ticket;
+};
+
+__global__ __launch_bounds__(kB) void ts_tile_scan_closed(TrainScanKernelParams p, uint64_t sps,
+                                                          uint32_t ntiles, ClosedScan cs,
+                                                          double* totals) {
+  __shared__ double red[kB / kWave];
+  __shared__ int is_last;
+  const uint32_t t = blockIdx.x * kB + threadIdx.x;
+  const bool valid = t < ntiles;
+  const f64x2 st = valid ? tile_sums_closed(p, sps, 1.0 / static_cast<double>(sps), t)
+                         : f64x2{0.0, 0.0};
+  const uint64_t t0 = static_cast<uint64_t>(t) * kTile;
+  const double cnt = valid ? static_cast<double>(p.n - t0 < kTile ? p.n - t0 : kTile) : 0.0;
+  double A, B, N;
+  const double p1 = block_inclusive_scan<kB>(st.x, red, &A) - st.x;
+  __syncthreads();
+  const double q = fma(cnt, p1, st.y);
+  const double ql = block_inclusive_scan<kB>(q, red, &B) - q;
+  __syncthreads();
+  block_inclusive_scan<kB>(cnt, red, &N);
+  if (valid) cs.local[t] = f64x2{p1, ql};
+  if (threadIdx.x == 0) {
+    double* g = cs.agg + 4 * blockIdx.x;
+    __hip_atomic_store(g, A, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(g + 1, B, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(g + 2, N, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned prev =
+        __hip_atomic_fetch_add(cs.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    is_last = (prev == gridDim.x - 1);
+  }
+  __syncthreads();
+  if (!is_last) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  // exclusive scan over the block aggregates, kB at a time (affine: Q += N PB + B)
+  double cp = 0.0, cq = 0.0;
+  for (uint32_t b0 = 0; b0 < gridDim.x; b0 += kB) {
+    const uint32_t b = b0 + threadIdx.x;
+    const bool vb = b < gridDim.x;
+    const double* g = cs.agg + 4 * b;
+    const double a = vb ? __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+    const double bb =
+        vb ? __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+    const double nb =
+        vb ? __hip_atomic_load(g + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+    double ta, tq;
+    const double pb = cp + (block_inclusive_scan<kB>(a, red, &ta) - a);
+    __syncthreads();
+    const double qq = fma(nb, pb, bb);
+    const double qb = cq + (block_inclusive_scan<kB>(qq, red, &tq) - qq);
+    __syncthreads();
+    if (vb) cs.blockpre[b] = f64x2{pb, qb};
+    cp += ta;
+    cq += tq;
+  }
+  if (threadIdx.x == 0) {
+    totals[0] = cp;  // T1: slice sum of v
+    totals[1] = cq;  // T2: slice sum of the local running integral
+    __hip_atomic_store(cs.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+  }
+}
+
+ClosedScan closed_carve(void* ws, uint64_t nt) {
+  const uint64_t nb = (nt + kB - 1) / kB;
+  ClosedScan cs;
+  cs.local = static_cast<f64x2*>(ws);
+  cs.blockpre = cs.local + nt;
+  cs.agg = reinterpret_cast<double*>(cs.blockpre + nb);
+  cs.ticket = reinterpret_cast<unsigned*>(cs.agg + 4 * nb);
+  return cs;
+}
+
+bool closed_form_sps(double dt, uint64_t* sps) {
+  const double r = 1.0 / dt;
+  const double k = std::nearbyint(r);
+  if (!(k >= 1.0 && std::fabs(r - k) <= 1e-9 * r)) return false;
+  *sps = static_cast<uint64_t>(k);
+  return true;
 }
 
 // ---------------------------------------------------------------------------- K3
@@ -199,13 +359,19 @@ __device__ __forceinline__ void store_tile(double* buf, const double (&v)[kItems
 }
 
 __global__ __launch_bounds__(kB) void ts_write(TrainScanKernelParams p, const f64x2* prefix,
-                                               const double* carries, double* vel, double* pos) {
+                                               const f64x2* blockpre, const double* carries,
+                                               double* vel, double* pos) {
   __shared__ double tab[kSpan];
   __shared__ double red[kB / kWave];
   __shared__ __attribute__((aligned(16))) double buf[kTile];
-  const Sampler f = make_sampler(p, tab);
+  const Sampler f = make_sampler(p, tab, blockIdx.x);
   const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kTile;
-  const f64x2 pr = prefix[blockIdx.x];
+  f64x2 pr = prefix[blockIdx.x];
+  if (blockpre) {  // closed-form path: tile prefix = block prefix (+) in-block prefix
+    const f64x2 bp = blockpre[blockIdx.x / kB];
+    const double before = static_cast<double>(blockIdx.x % kB) * kTile;
+    pr = f64x2{bp.x + pr.x, fma(before, bp.x, bp.y) + pr.y};
+  }
   const double c1 = carries ? carries[0] : 0.0;
   const double c2 = carries ? carries[1] : 0.0;
   double v[kItems];
@@ -236,11 +402,188 @@ __global__ __launch_bounds__(kB) void ts_write(TrainScanKernelParams p, const f6
   if (pos) store_tile(buf, v, pos, t0, p.n);
 }
 
+// ---------------------------------------------------------------------------- one pass
+// Single GPU: K1 + K2 + K4 in ONE pass with a decoupled look-back (as scan.hip) over the
+// two-component tile state (A, B) = (sum v, sum of the tile's local running integral).
+// Concatenation is affine — (A1,B1) then (A2,B2) = (A1+A2, B1 + B2 + n2 A1) — but every
+// predecessor of a tile is a full 4096-sample tile, so the exclusive state of tile t is a
+// plain sum over predecessors j of (A_j, B_j + 4096 (t-1-j) A_j), and over the nearest
+// predecessor s that published its inclusive state (P_s, Q_s): (P_s, Q_s + 4096 (t-1-s) P_s).
+// Commutative terms: the wave sums them with DPP exactly like the 1-component look-back.
+// Samples are generated once and HBM sees only the 16 B/sample of vel + pos stores.
+// Tile ids come from an atomic counter (forward progress under any dispatch order); spins
+// are bounded and report through the timeout word. The look-back sums whatever mix of
+// aggregates and prefixes it finds, so the last bits may differ run to run; the 3-kernel
+// path (ScanAlgo::kFused) is the bitwise-deterministic one.
+constexpr unsigned kOpAgg = 1u, kOpPrefix = 2u;
+constexpr unsigned kOpSpinLimit = 1u << 26;
+constexpr size_t kOpHeader = 64;  // counter @0, timeout @4
+
+struct OnePassState {
+  unsigned* counter;
+  unsigned* timeout;
+  unsigned* flags;  // per tile: 0 none, 1 aggregate, 2 inclusive prefix
+  double* agg;      // per tile {A, B}
+  double* pref;     // per tile inclusive {P, Q}
+};
+
+__device__ __forceinline__ void op_publish(const OnePassState& st, double* slot, unsigned tile,
+                                           double x, double y, unsigned flag) {
+  __hip_atomic_store(slot + 2 * tile, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(slot + 2 * tile + 1, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(st.flags + tile, flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Wave 0: exclusive {P, Q} of `tile` (lanes examine tile-1-lane, 64 at a time).
+__device__ f64x2 op_look_back(const OnePassState& st, unsigned tile) {
+  const int lane = threadIdx.x & 63;
+  double P = 0.0, Q = 0.0;
+  long base = static_cast<long>(tile) - 1;
+  for (;;) {
+    const long j = base - lane;
+    unsigned f = kOpPrefix;  // lanes past the front act as "prefix 0"
+    double a = 0.0, b = 0.0;
+    if (j >= 0) {
+      unsigned spins = 0;
+      while ((f = __hip_atomic_load(st.flags + j, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > kOpSpinLimit) {
+          __hip_atomic_store(st.timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          f = kOpPrefix;
+          break;
+        }
+      }
+      const double* src = (f == kOpPrefix ? st.pref : st.agg) + 2 * j;
+      a = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      b = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const unsigned long long pm = __ballot(f == kOpPrefix);
+    const int stop = pm ? __builtin_ctzll(pm) : 64;
+    const double gap = static_cast<double>(kTile) * static_cast<double>(static_cast<long>(tile) - 1 - j);
+    const bool use = lane <= stop && j >= 0;
+    P += wave_sum(use ? a : 0.0);
+    Q += wave_sum(use ? fma(gap, a, b) : 0.0);
+    if (pm) break;
+    base -= 64;
+  }
+  return f64x2{P, Q};
+}
+
+__global__ __launch_bounds__(kB) void ts_onepass(TrainScanKernelParams p, OnePassState st,
+                                                 unsigned ntiles, double* vel, double* pos,
+                                                 double* totals) {
+  __shared__ double tab[kSpan];
+  __shared__ double red[kB / kWave];
+  __shared__ __attribute__((aligned(16))) double buf[kTile];
+  __shared__ unsigned tile_sh;
+  __shared__ double pre_sh[2];
+  if (threadIdx.x == 0)
+    tile_sh = __hip_atomic_fetch_add(st.counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const unsigned tile = tile_sh;
+  const Sampler f = make_sampler(p, tab, tile);
+  const uint64_t t0 = static_cast<uint64_t>(tile) * kTile;
+  const double nt = static_cast<double>(p.n - t0 < kTile ? p.n - t0 : kTile);
+  double v[kItems], w[kItems];
+  f.items(t0 + threadIdx.x * kItems, f.plain_tile(t0), v);
+  double run = 0.0;
+#pragma unroll
+  for (int k = 0; k < kItems; ++k) {
+    run += v[k];
+    v[k] = run;
+  }
+  double A;
+  const double ex1 = block_inclusive_scan<kB>(run, red, &A) - run;
+  __syncthreads();  // red is reused
+  run = 0.0;
+#pragma unroll
+  for (int k = 0; k < kItems; ++k) {
+    v[k] += ex1;  // tile-local running integral of v
+    run += v[k];
+    w[k] = run;
+  }
+  double Bt;
+  const double ex2 = block_inclusive_scan<kB>(run, red, &Bt) - run;
+  // a partial (last) tile's padding holds v = 0, so each padded slot carries the running
+  // total A into Bt: only the first nt slots belong to the slice
+  Bt = fma(nt - static_cast<double>(kTile), A, Bt);
+#pragma unroll
+  for (int k = 0; k < kItems; ++k) w[k] += ex2;  // tile-local running integral of that
+  if (threadIdx.x < kWave) {
+    f64x2 ex = {0.0, 0.0};
+    if (tile > 0) {
+      if (threadIdx.x == 0) op_publish(st, st.agg, tile, A, Bt, kOpAgg);
+      ex = op_look_back(st, tile);
+    }
+    if (threadIdx.x == 0) {
+      const double pi = ex.x + A, qi = fma(nt, ex.x, ex.y + Bt);
+      op_publish(st, st.pref, tile, pi, qi, kOpPrefix);
+      pre_sh[0] = ex.x;
+      pre_sh[1] = ex.y;
+      if (tile + 1 == ntiles) {
+        totals[0] = pi;  // T1, T2 of this slice
+        totals[1] = qi;
+      }
+    }
+  }
+  __syncthreads();
+  const double P = pre_sh[0], Q = pre_sh[1];
+#pragma unroll
+  for (int k = 0; k < kItems; ++k) v[k] += P;  // velocity integral ("distance")
+  store_tile(buf, v, vel, t0, p.n);
+#pragma unroll
+  for (int k = 0; k < kItems; ++k) {
+    const double cnt = static_cast<double>(threadIdx.x * kItems + k + 1);
+    w[k] = Q + fma(cnt, P, w[k]);  // running integral of the above
+  }
+  store_tile(buf, w, pos, t0, p.n);
+}
+
+OnePassState op_carve(void* ws, uint64_t nt) {
+  char* p = static_cast<char*>(ws);
+  OnePassState st;
+  st.counter = reinterpret_cast<unsigned*>(p);
+  st.timeout = reinterpret_cast<unsigned*>(p + 4);
+  st.flags = reinterpret_cast<unsigned*>(p + kOpHeader);
+  char* q = p + kOpHeader + ((nt * sizeof(unsigned) + 15) & ~uint64_t(15));
+  st.agg = reinterpret_cast<double*>(q);
+  st.pref = st.agg + 2 * nt;
+  return st;
+}
+
 }  // namespace
 
 size_t trainscan_workspace_bytes(uint64_t n) {
   const uint64_t nt = (n + kTile - 1) / kTile;
-  return 2 * nt * sizeof(f64x2) + 64;
+  // 3-kernel path: {sums, prefix} f64x2 per tile; one-pass: header + flags + {agg, pref}
+  return kOpHeader + ((nt * sizeof(unsigned) + 15) & ~uint64_t(15)) + 2 * nt * sizeof(f64x2);
+}
+
+void launch_trainscan_onepass(const TrainScanKernelParams& p, void* ws, double* vel, double* pos,
+                              double* totals, hipStream_t s) {
+  MIINT_CHECK(p.n >= 1, "empty slice");
+  MIINT_CHECK(p.table_n >= 2 && p.table_n <= kMaxTable, "table size must be in [2, 2048]");
+  MIINT_CHECK(vel && pos && totals, "one-pass scan writes vel, pos and totals");
+  MIINT_CHECK((reinterpret_cast<uintptr_t>(vel) & 15) == 0 &&
+                  (reinterpret_cast<uintptr_t>(pos) & 15) == 0,
+              "trainscan outputs need 16-B alignment");
+  const uint64_t nt = (p.n + kTile - 1) / kTile;
+  MIINT_CHECK(nt < (1u << 31), "slice too large");
+  const OnePassState st = op_carve(ws, nt);
+  MIINT_HIP(hipMemsetAsync(ws, 0, kOpHeader + ((nt * sizeof(unsigned) + 15) & ~uint64_t(15)), s));
+  ts_onepass<<<static_cast<unsigned>(nt), kB, 0, s>>>(p, st, static_cast<unsigned>(nt), vel, pos,
+                                                       totals);
+  MIINT_HIP(hipGetLastError());
+}
+
+unsigned trainscan_onepass_timeout(const void* ws, hipStream_t s) {
+  unsigned v = 0;
+  MIINT_HIP(hipMemcpyAsync(&v, static_cast<const char*>(ws) + 4, sizeof(v), hipMemcpyDeviceToHost,
+                           s));
+  MIINT_HIP(hipStreamSynchronize(s));
+  return v;
 }
 
 void launch_trainscan_local(const TrainScanKernelParams& p, void* ws, double* totals,
@@ -249,6 +592,15 @@ void launch_trainscan_local(const TrainScanKernelParams& p, void* ws, double* to
   MIINT_CHECK(p.table_n >= 2 && p.table_n <= kMaxTable, "table size must be in [2, 2048]");
   const uint64_t nt = (p.n + kTile - 1) / kTile;
   MIINT_CHECK(nt < (1u << 31), "slice too large");
+  uint64_t sps = 0;
+  if (closed_form_sps(p.dt, &sps)) {  // dt = 1/sps: closed-form tile sums, one launch
+    // the ticket is zero from allocation (workspace contract) and re-armed by the kernel
+    const ClosedScan cs = closed_carve(ws, nt);
+    ts_tile_scan_closed<<<static_cast<unsigned>((nt + kB - 1) / kB), kB, 0, s>>>(
+        p, sps, static_cast<uint32_t>(nt), cs, totals);
+    MIINT_HIP(hipGetLastError());
+    return;
+  }
   f64x2* sums = static_cast<f64x2*>(ws);
   f64x2* prefix = sums + nt;
   ts_tile_sums<<<static_cast<unsigned>(nt), kB, 0, s>>>(p, sums);
@@ -269,8 +621,15 @@ void launch_trainscan_write(const TrainScanKernelParams& p, const void* ws, cons
                   (reinterpret_cast<uintptr_t>(pos) & 15) == 0,
               "trainscan outputs need 16-B alignment");
   const uint64_t nt = (p.n + kTile - 1) / kTile;
-  const f64x2* prefix = static_cast<const f64x2*>(ws) + nt;
-  ts_write<<<static_cast<unsigned>(nt), kB, 0, s>>>(p, prefix, carries, vel, pos);
+  uint64_t sps = 0;
+  if (closed_form_sps(p.dt, &sps)) {  // layout of launch_trainscan_local's closed-form path
+    const ClosedScan cs = closed_carve(const_cast<void*>(ws), nt);
+    ts_write<<<static_cast<unsigned>(nt), kB, 0, s>>>(p, cs.local, cs.blockpre, carries, vel,
+                                                      pos);
+  } else {
+    const f64x2* prefix = static_cast<const f64x2*>(ws) + nt;
+    ts_write<<<static_cast<unsigned>(nt), kB, 0, s>>>(p, prefix, nullptr, carries, vel, pos);
+  }
   MIINT_HIP(hipGetLastError());
 }
 

@@ -47,6 +47,15 @@ RiemannParams make_params(int integrand, double a, double h, double off, uint64_
 
 }  // namespace
 
+static const char* scan_algo_name(ScanAlgo a) {
+  return a == ScanAlgo::kFused ? "fused" : a == ScanAlgo::kOnePass ? "onepass" : "lookback";
+}
+static ScanAlgo scan_algo_of(const std::string& s) {
+  MIINT_CHECK(s == "fused" || s == "lookback" || s == "onepass",
+              "algo must be onepass|fused|lookback");
+  return s == "fused" ? ScanAlgo::kFused : s == "onepass" ? ScanAlgo::kOnePass : ScanAlgo::kLookback;
+}
+
 PYBIND11_MODULE(_miint, m) {
   m.doc() = "miint: MI355X-native numerical integration (HIP/gfx950 kernels, RCCL, hipGraph)";
   py::register_exception<miint::Error>(m, "MiintError", PyExc_RuntimeError);
@@ -272,11 +281,9 @@ PYBIND11_MODULE(_miint, m) {
       .def_readwrite("parity", &TrainScanConfig::parity)
       .def_readwrite("replicate", &TrainScanConfig::replicate)
       .def_readwrite("phase2", &TrainScanConfig::phase2)
-      .def_property("algo",
-                    [](const TrainScanConfig& c) { return c.algo == ScanAlgo::kFused ? "fused" : "lookback"; },
+      .def_property("algo", [](const TrainScanConfig& c) { return scan_algo_name(c.algo); },
                     [](TrainScanConfig& c, const std::string& s) {
-                      MIINT_CHECK(s == "fused" || s == "lookback", "algo must be fused|lookback");
-                      c.algo = s == "fused" ? ScanAlgo::kFused : ScanAlgo::kLookback;
+                      c.algo = scan_algo_of(s);
                     });
   m.def("trainscan_workspace_bytes", &trainscan_workspace_bytes);
 
@@ -303,6 +310,17 @@ PYBIND11_MODULE(_miint, m) {
     launch_trainscan_write(p, ptr<const void>(ws), ptr<const double>(carries), ptr<double>(vel),
                            ptr<double>(pos), stream(s));
   });
+  m.def("launch_trainscan_onepass", [](uintptr_t table, int tn, double dt, uint64_t i0,
+                                       uint64_t n, uint64_t win_lo, uint64_t win_hi, uintptr_t ws,
+                                       uintptr_t totals, uintptr_t vel, uintptr_t pos,
+                                       uintptr_t s) {
+    TrainScanKernelParams p{ptr<const double>(table), tn, dt, i0, n, win_lo, win_hi};
+    launch_trainscan_onepass(p, ptr<void>(ws), ptr<double>(vel), ptr<double>(pos),
+                             ptr<double>(totals), stream(s));
+  });
+  m.def("trainscan_onepass_timeout", [](uintptr_t ws, uintptr_t s) {
+    return trainscan_onepass_timeout(ptr<const void>(ws), stream(s));
+  });
   py::class_<TrainScan>(m, "TrainScan")
       .def(py::init<const TrainScanConfig&, int, const Comm*>(), py::arg("config"),
            py::arg("device"), py::arg("comm") = nullptr, py::keep_alive<1, 4>())
@@ -320,6 +338,7 @@ PYBIND11_MODULE(_miint, m) {
         return d;
       })
       .def_property_readonly("local_begin", &TrainScan::local_begin)
+      .def_property_readonly("algo", [](const TrainScan& t) { return scan_algo_name(t.algo()); })
       .def_property_readonly("local_count", &TrainScan::local_count)
       .def("velocity_ptr", [](const TrainScan& t) { return reinterpret_cast<uintptr_t>(t.velocity()); })
       .def("position_ptr", [](const TrainScan& t) { return reinterpret_cast<uintptr_t>(t.position()); });

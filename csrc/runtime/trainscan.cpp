@@ -45,14 +45,15 @@ TrainScan::TrainScan(const TrainScanConfig& cfg, int device, const Comm* comm)
   table_ = DeviceBuffer<double>(tab.size());
   MIINT_HIP(hipMemcpy(table_.get(), tab.data(), table_.bytes(), hipMemcpyHostToDevice));
   vel_ = DeviceBuffer<double>(count_);
-  if (cfg.phase2 || cfg.algo == ScanAlgo::kFused) pos_ = DeviceBuffer<double>(count_);
+  if (cfg.algo == ScanAlgo::kOnePass && world_ > 1) cfg_.algo = ScanAlgo::kFused;  // needs totals first
+  if (cfg.phase2 || cfg_.algo != ScanAlgo::kLookback) pos_ = DeviceBuffer<double>(count_);
   if (cfg.replicate) {
     MIINT_CHECK(!cfg.parity && total_ % static_cast<uint64_t>(world_) == 0,
                 "replicate needs equal slices (total divisible by world, no parity)");
     full_ = DeviceBuffer<double>(total_);
   }
-  state_ = DeviceBuffer<char>(cfg.algo == ScanAlgo::kFused ? trainscan_workspace_bytes(count_)
-                                                            : scan_state_bytes(count_));
+  state_ = DeviceBuffer<char>(cfg_.algo == ScanAlgo::kLookback ? scan_state_bytes(count_)
+                                                               : trainscan_workspace_bytes(count_));
   scratch_ = DeviceBuffer<double>(kGather + 3 * static_cast<size_t>(world_));
   host_ = PinnedBuffer<double>(4);
   MIINT_HIP(hipMemset(scratch_.get(), 0, scratch_.bytes()));
@@ -104,6 +105,12 @@ void TrainScan::enqueue_fused(hipStream_t s) {
   launch_trainscan_write(p, state_.get(), carries, vel_.get(), pos_.get(), s);
 }
 
+void TrainScan::enqueue_onepass(hipStream_t s) {
+  TrainScanKernelParams p{table_.get(), static_cast<int>(oracle::profile_table().size()),
+                          1.0 / cfg_.steps_per_sec, begin_, count_, win_lo_, win_hi_};
+  launch_trainscan_onepass(p, state_.get(), vel_.get(), pos_.get(), scratch_.get() + kTotals, s);
+}
+
 void TrainScan::enqueue_lookback(hipStream_t s) {
   const double dt = 1.0 / cfg_.steps_per_sec;
   const int tn = static_cast<int>(oracle::profile_table().size());
@@ -120,9 +127,12 @@ void TrainScan::enqueue_lookback(hipStream_t s) {
 
 void TrainScan::enqueue() {
   DeviceGuard g(device_);
-  TraceRange tr(cfg_.algo == ScanAlgo::kFused ? "miint.trainscan.fused" : "miint.trainscan.lookback");
+  TraceRange tr(cfg_.algo == ScanAlgo::kFused     ? "miint.trainscan.fused"
+                : cfg_.algo == ScanAlgo::kOnePass ? "miint.trainscan.onepass"
+                                                  : "miint.trainscan.lookback");
   hipStream_t s = stream_.get();
   if (cfg_.algo == ScanAlgo::kFused) enqueue_fused(s);
+  else if (cfg_.algo == ScanAlgo::kOnePass) enqueue_onepass(s);
   else enqueue_lookback(s);
   if (cfg_.replicate) {
     if (comm_) {
@@ -144,10 +154,11 @@ TrainScanResult TrainScan::run() {
   MIINT_HIP(hipStreamSynchronize(s));
   r.device_ms = Event::elapsed_ms(e0_, e1_);
   if (cfg_.algo == ScanAlgo::kLookback) r.timeout = scan_timeout_flag(state_.get(), s);
+  if (cfg_.algo == ScanAlgo::kOnePass) r.timeout = trainscan_onepass_timeout(state_.get(), s);
   // 4main.c:241 prints default_sum[tablelen-2]; the complete integral is element T-1.
   const uint64_t gi = cfg_.parity ? total_ - 2 : total_ - 1;
   r.distance = pick_global(vel_.get(), gi, s) / cfg_.steps_per_sec;
-  if (cfg_.phase2 || cfg_.algo == ScanAlgo::kFused) {
+  if (cfg_.phase2 || cfg_.algo != ScanAlgo::kLookback) {
     const uint64_t last = cfg_.parity ? (total_ / world_) * world_ - 1 : total_ - 1;
     r.sum_of_sums = pick_global(pos_.get(), last, s);
   }

@@ -165,7 +165,7 @@ def main(argv=None) -> int:
     c.add_argument("--json", action="store_true")
     t = sub.add_parser("trainscan")
     t.add_argument("--parity", action="store_true")
-    t.add_argument("--algo", default="fused", choices=["fused", "lookback"])
+    t.add_argument("--algo", default="fused", choices=["fused", "onepass", "lookback"])
     t.add_argument("--json", action="store_true")
     common(sub.add_parser("integrate"), integrand="pi4")
     sub.add_parser("oracle")

@@ -203,20 +203,31 @@ def interp_scan(n: int, i0: int = 0, dt: float = 1e-4, window: tuple[int, int] |
 
 
 def trainscan(n: int, i0: int = 0, dt: float = 1e-4, window: tuple[int, int] | None = None,
-              carries: torch.Tensor | None = None):
-    """Fused two-phase scan of the interpolated profile (csrc/kernels/trainscan.hip).
+              carries: torch.Tensor | None = None, algo: str = "fused"):
+    """Two-phase scan of the interpolated profile (csrc/kernels/trainscan.hip).
 
     Returns (vel, pos, totals): vel = running sum of the samples, pos = running sum of vel,
     totals = {T1, T2} (the slice's sample sum and vel sum without carries). `carries`
-    (2-element device tensor {C1, C2}) shifts the slice as if it followed earlier ranks."""
+    (2-element device tensor {C1, C2}) shifts the slice as if it followed earlier ranks
+    (algo="fused" only). algo="onepass": single pass with a decoupled look-back."""
+    if algo not in ("fused", "onepass"):
+        raise ValueError("algo must be fused|onepass")
+    if algo == "onepass" and carries is not None:
+        raise ValueError("the one-pass scan takes no carries (single-GPU form)")
     m = native()
     dev = _device()
     tab = profile_tensor(dev)
     vel = torch.empty(n, dtype=torch.float64, device=dev)
     pos = torch.empty(n, dtype=torch.float64, device=dev)
-    ws = torch.empty(m.trainscan_workspace_bytes(n), dtype=torch.uint8, device=dev)
+    ws = torch.zeros(m.trainscan_workspace_bytes(n), dtype=torch.uint8, device=dev)  # zeroed once
     totals = torch.zeros(2, dtype=torch.float64, device=dev)
     lo, hi = window if window is not None else (0, (1 << 64) - 1)
+    if algo == "onepass":
+        m.launch_trainscan_onepass(tab.data_ptr(), tab.numel(), dt, i0, n, lo, hi, ws.data_ptr(),
+                                   totals.data_ptr(), vel.data_ptr(), pos.data_ptr(), _stream())
+        if m.trainscan_onepass_timeout(ws.data_ptr(), _stream()):
+            raise RuntimeError("trainscan look-back spin limit hit")
+        return vel, pos, totals
     m.launch_trainscan(tab.data_ptr(), tab.numel(), dt, i0, n, lo, hi, ws.data_ptr(),
                        totals.data_ptr(), carries.data_ptr() if carries is not None else 0,
                        vel.data_ptr(), pos.data_ptr(), _stream())

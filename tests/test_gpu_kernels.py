@@ -193,9 +193,10 @@ def test_interp_scan_matches_fill_then_scan(cuda):
     assert float(fused[-1].item()) / 1e4 == pytest.approx(122000.004000, abs=1e-6)
 
 
+@pytest.mark.parametrize("algo", ["fused", "onepass"])
 @pytest.mark.parametrize("n", [1, 4095, 4097, 1_000_003, 18_000_000])
-def test_fused_trainscan_vs_cumsum(cuda, n):
-    vel, pos, totals = kernels.trainscan(n)
+def test_fused_trainscan_vs_cumsum(cuda, n, algo):
+    vel, pos, totals = kernels.trainscan(n, algo=algo)
     x = kernels.interp_fill(n)
     v_ref = torch.cumsum(x, 0)
     torch.testing.assert_close(vel, v_ref, rtol=1e-11, atol=1e-7)
@@ -203,6 +204,20 @@ def test_fused_trainscan_vs_cumsum(cuda, n):
     torch.testing.assert_close(pos, p_ref, rtol=1e-10, atol=1e-3)
     assert float(totals[0]) == pytest.approx(float(x.sum()), rel=1e-12)
     assert float(totals[1]) == pytest.approx(float(v_ref.sum()), rel=1e-11)
+
+
+@pytest.mark.parametrize("dt,i0", [(1.05e-4, 0), (1e-4, 7), (2e-3, 123)])
+def test_fused_trainscan_tile_sum_paths(cuda, dt, i0):
+    """Tile sums come in closed form when 1/dt is an integer (1e-4, 2e-3: 500 samples/s,
+    tiles span several segments) and from re-sampling otherwise (1.05e-4); both must give
+    the cumsum of the sampled profile, including tiles that start mid-segment (i0)."""
+    n = 700_001
+    vel, pos, totals = kernels.trainscan(n, i0=i0, dt=dt)
+    x = kernels.interp_fill(n, i0=i0, dt=dt)
+    v_ref = torch.cumsum(x, 0)
+    torch.testing.assert_close(vel, v_ref, rtol=1e-11, atol=1e-7)
+    torch.testing.assert_close(pos, torch.cumsum(v_ref, 0), rtol=1e-10, atol=1e-3)
+    assert float(totals[0]) == pytest.approx(float(x.sum()), rel=1e-12)
 
 
 def test_fused_trainscan_rank_carries(cuda):
@@ -226,16 +241,17 @@ def test_fused_trainscan_rank_carries(cuda):
         torch.testing.assert_close(p, pos[cuts[r]:cuts[r + 1]], rtol=1e-12, atol=1e-2)
 
 
-def test_fused_trainscan_parity_window(cuda):
+@pytest.mark.parametrize("algo", ["fused", "onepass"])
+def test_fused_trainscan_parity_window(cuda, algo):
     n = 2_000_000
-    vel, _, _ = kernels.trainscan(n, i0=1_000_000, window=(1_500_000, 2_500_000))
+    vel, _, _ = kernels.trainscan(n, i0=1_000_000, window=(1_500_000, 2_500_000), algo=algo)
     x = kernels.interp_fill(n, i0=1_000_000)
     x[:500_000] = 0
     x[1_500_000:] = 0
     torch.testing.assert_close(vel, torch.cumsum(x, 0), rtol=1e-11, atol=1e-7)
 
 
-@pytest.mark.parametrize("algo", ["fused", "lookback"])
+@pytest.mark.parametrize("algo", ["onepass", "fused", "lookback"])
 @pytest.mark.parametrize("parity", [False, True])
 def test_trainscan_class_algorithms_agree(native, cuda, algo, parity):
     cfg = native.TrainScanConfig()

@@ -72,6 +72,8 @@ inline double rule_offset(Rule r) {
 constexpr int kMaxPolyCoeffs = 16;
 
 // Everything a Riemann kernel needs, passed by value (kernarg segment, lands in SGPRs).
+constexpr int kSinTrig = 20;  // 8 x {cos, sin}(k_j h) + {cos, sin}(8h), {cos, sin}(24h)
+
 struct RiemannParams {
   double a;             // integration lower bound
   double h;             // subinterval width (b-a)/n_total
@@ -82,6 +84,10 @@ struct RiemannParams {
   int ncoef;            // polynomial: number of coefficients
   double coef[kMaxPolyCoeffs];  // polynomial coefficients c_0..c_{ncoef-1}
   double p0, p1;        // integrand parameters (train: ts, vs)
+  // Sin series path, filled on the host by the launchers (long double): trig[j] = cos(k_j h),
+  // trig[8 + j] = sin(k_j h) for k_j = j + 1/2 (j < 8), then cos(8h), sin(8h), cos(24h),
+  // sin(24h) (integrands.hpp, struct Sin)
+  double trig[kSinTrig];
 };
 
 }  // namespace miint

@@ -19,6 +19,8 @@
 //   * fp32 path: packed float2 math (v_pk_fma_f32), tile coordinates from an fp64 base.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
+
 #include "miint/common.hpp"
 #include "miint/integrands.hpp"
 #include "miint/kernels.hpp"
@@ -190,7 +192,11 @@ template <> struct Maker<Pi4F32> {
 };
 template <> struct Maker<Sin> {
   static constexpr int kLds = 1;
-  __device__ static Sin make(const RiemannParams&, const double*, int, double*) { return {}; }
+  __device__ static Sin make(const RiemannParams& p, const double*, int, double*) {
+    Sin f;
+    f.init(p.trig);
+    return f;
+  }
 };
 template <> struct Maker<Poly> {
   static constexpr int kLds = 1;
@@ -326,6 +332,8 @@ __global__ __launch_bounds__(B) void point_values_kernel(RiemannParams p, const 
     if constexpr (M == DivMode::kSeries && __is_same(F, Pi4)) {
       // exactly the operations Pi4::tile_acc applies to sample u
       v = full ? f.series_point(xm, p.h, u) : f.point(x);
+    } else if constexpr (M == DivMode::kSeries && __is_same(F, Sin)) {
+      v = full ? f.series_point(xm, u) : f.point(x);
     } else if constexpr (M == DivMode::kSeriesDirect && __is_same(F, Pi4)) {
       const Pi4::Seed sd = Pi4::seed(xm, p.h);
       const double e = fma(-fma(x, x, 1.0), sd.s, 1.0);
@@ -367,7 +375,10 @@ void dispatch(const RiemannParams& p, DType dtype, DivMode m, A&&... a) {
       else if (m == DivMode::kSeriesDirect) Op<DivMode::kSeriesDirect, Pi4>::run(a...);
       else Op<DivMode::kIeee, Pi4>::run(a...);
       return;
-    case Integrand::kSin: Op<DivMode::kIeee, Sin>::run(a...); return;
+    case Integrand::kSin:
+      if (m == DivMode::kSeries) Op<DivMode::kSeries, Sin>::run(a...);
+      else Op<DivMode::kIeee, Sin>::run(a...);
+      return;
     case Integrand::kPoly: Op<DivMode::kIeee, Poly>::run(a...); return;
     case Integrand::kTrainVel: Op<DivMode::kIeee, TrainVel>::run(a...); return;
     case Integrand::kTable: Op<DivMode::kIeee, Table>::run(a...); return;
@@ -423,7 +434,26 @@ static void check_params(const RiemannParams& p, const double* table, int table_
 }
 
 static DivMode effective_div(const RiemannParams& p, DivMode div) {
-  return miint::effective_div(div, p.h);
+  return miint::effective_div(div, p.h, static_cast<Integrand>(p.integrand));
+}
+
+// Host-side constants of the Sin series path (long double; see Sin in integrands.hpp).
+static RiemannParams prepared(const RiemannParams& p, DivMode eff) {
+  RiemannParams q = p;
+  if (static_cast<Integrand>(p.integrand) == Integrand::kSin && eff == DivMode::kSeries) {
+    const long double h = p.h;
+    for (int j = 0; j < Sin::kPairs; ++j) {
+      const long double k = j + 0.5L;
+      q.trig[j] = static_cast<double>(cosl(k * h));
+      q.trig[Sin::kPairs + j] = static_cast<double>(sinl(k * h));
+    }
+    for (int i = 0; i < 2; ++i) {
+      const long double c0 = Sin::kSub * (i + 0.5L);
+      q.trig[2 * Sin::kPairs + 2 * i] = static_cast<double>(cosl(c0 * h));
+      q.trig[2 * Sin::kPairs + 2 * i + 1] = static_cast<double>(sinl(c0 * h));
+    }
+  }
+  return q;
 }
 
 void launch_riemann_partials(const RiemannParams& p, DType dtype, DivMode div, LaunchShape shape,
@@ -431,8 +461,8 @@ void launch_riemann_partials(const RiemannParams& p, DType dtype, DivMode div, L
                              hipStream_t stream) {
   check_shape(shape);
   check_params(p, table, table_n);
-  dispatch<PartialsOp>(p, dtype, effective_div(p, div), p, shape, table, table_n, partials,
-                       stream);
+  const DivMode eff = effective_div(p, div);
+  dispatch<PartialsOp>(p, dtype, eff, prepared(p, eff), shape, table, table_n, partials, stream);
   MIINT_HIP(hipGetLastError());
 }
 
@@ -448,7 +478,8 @@ void launch_riemann_fused(const RiemannParams& p, DType dtype, DivMode div, Laun
                           unsigned int* ticket, double scale, double* out, hipStream_t stream) {
   check_shape(shape);
   check_params(p, table, table_n);
-  dispatch<FusedOp>(p, dtype, effective_div(p, div), p, shape, table, table_n, partials, ticket,
+  const DivMode eff = effective_div(p, div);
+  dispatch<FusedOp>(p, dtype, eff, prepared(p, eff), shape, table, table_n, partials, ticket,
                     scale, out, stream);
   MIINT_HIP(hipGetLastError());
 }
@@ -457,7 +488,8 @@ void launch_riemann_point_values(const RiemannParams& p, DivMode div, const doub
                                  int table_n, double* out, hipStream_t stream) {
   check_params(p, table, table_n);
   MIINT_CHECK(p.n >= 1, "empty range");
-  dispatch<PointsOp>(p, DType::kF64, effective_div(p, div), p, table, table_n, out, stream);
+  const DivMode eff = effective_div(p, div);
+  dispatch<PointsOp>(p, DType::kF64, eff, prepared(p, eff), table, table_n, out, stream);
   MIINT_HIP(hipGetLastError());
 }
 

@@ -74,7 +74,10 @@ RiemannPlan::~RiemannPlan() {
   (void)hipStreamSynchronize(comm_stream_.get());
 }
 
-DivMode RiemannPlan::effective_div() const { return miint::effective_div(cfg_.div, params_.h); }
+DivMode RiemannPlan::effective_div() const {
+  return cfg_.dtype == DType::kF32 ? miint::effective_div(cfg_.div, params_.h)
+                                   : miint::effective_div(cfg_.div, params_.h, cfg_.integrand);
+}
 
 size_t RiemannPlan::graph_nodes() const { return batch_ ? batch_->num_nodes() : 0; }
 

@@ -132,6 +132,17 @@ inline void run_ranks(const Topology& t,
   if (!err.empty()) throw Error(err);
 }
 
+// --integrand names shared by every tool (SURVEY §5 config flags); unknown names fail.
+inline Integrand parse_integrand(const std::string& s) {
+  if (s == "sin") return Integrand::kSin;
+  if (s == "pi4" || s == "pi") return Integrand::kPi4;
+  if (s == "poly") return Integrand::kPoly;
+  if (s == "train") return Integrand::kTrainVel;
+  if (s == "table") return Integrand::kTable;
+  if (s == "table2d") fail("the 2-D field is its own tool: miint table2d [--grid 4096]", __FILE__, __LINE__);
+  fail("unknown integrand '" + s + "' (sin|pi4|poly|train|table)", __FILE__, __LINE__);
+}
+
 inline std::string json_escape(const std::string& s) {
   std::string o;
   for (char c : s) {

@@ -61,6 +61,16 @@ int main() {
              a.positional().size() == 1,
          "cli argument parsing");
 
+  bool threw = false;
+  try {
+    (void)cli::parse_integrand("bogus");
+  } catch (const Error&) {
+    threw = true;
+  }
+  expect(threw && cli::parse_integrand("pi") == Integrand::kPi4 &&
+             cli::parse_integrand("table") == Integrand::kTable,
+         "integrand names: aliases accepted, unknown names rejected");
+
   std::printf("%s\n", g_bad ? "HOST SELFTEST FAILED" : "HOST SELFTEST OK");
   return g_bad ? 1 : 0;
 }

@@ -31,13 +31,7 @@ struct BenchRow {
   int gpus = 1;
 };
 
-Integrand integrand_of(const std::string& s) {
-  if (s == "sin") return Integrand::kSin;
-  if (s == "poly") return Integrand::kPoly;
-  if (s == "train") return Integrand::kTrainVel;
-  if (s == "table") return Integrand::kTable;
-  return Integrand::kPi4;
-}
+Integrand integrand_of(const std::string& s) { return cli::parse_integrand(s); }
 
 RiemannConfig make_cfg(const std::string& integ, double n, const std::string& dtype,
                        const std::string& rule, const std::string& div) {

@@ -24,14 +24,6 @@ using namespace miint;
 
 namespace {
 
-Integrand parse_integrand(const std::string& s) {
-  if (s == "sin") return Integrand::kSin;
-  if (s == "pi4") return Integrand::kPi4;
-  if (s == "poly") return Integrand::kPoly;
-  if (s == "train") return Integrand::kTrainVel;
-  if (s == "table") return Integrand::kTable;
-  fail("unknown integrand " + s, __FILE__, __LINE__);
-}
 Rule parse_rule(const std::string& s) {
   if (s == "left") return Rule::kLeft;
   if (s == "mid") return Rule::kMid;
@@ -44,7 +36,7 @@ Rule parse_rule(const std::string& s) {
 int main(int argc, char** argv) {
   try {
     cli::Args a(argc, argv);
-    const Integrand f = parse_integrand(a.str("integrand", "sin"));
+    const Integrand f = cli::parse_integrand(a.str("integrand", "sin"));
     const double pi = 3.14159265358979323846;
     double lo = 0.0, hi = pi;  // riemann.cpp:6 RANGE = M_PI
     if (f == Integrand::kPi4) hi = 1.0;

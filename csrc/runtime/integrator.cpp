@@ -151,6 +151,12 @@ void RiemannPlan::enqueue_batch(hipStream_t cs, hipStream_t rs, int nsteps, bool
 void RiemannPlan::capture_graphs() {
   DeviceGuard g(device_);
   TraceRange tr("miint.plan.capture_graphs");
+  if (collective()) {
+    // RCCL sets up peer connections lazily at a communicator's first collective: run that
+    // one eagerly, outside the capture, so the graph only records steady-state operations.
+    comm_->allreduce_sum(result_.get(), result_.get(), 1, compute_.get());
+    MIINT_HIP(hipStreamSynchronize(compute_.get()));
+  }
   batch_.reset(new Graph());
   try {
     batch_->capture(compute_.get(), [&](hipStream_t s) {

@@ -289,12 +289,24 @@ __global__ __launch_bounds__(B) void riemann_fused_kernel(RiemannParams p, const
   __shared__ int is_last;
   const F f = Maker<F>::make(p, table, table_n, lds);
   const double s = block_sum<B>(lane_sum<M>(p, f), red);
+  // Two-level ticket: workgroup b counts in group b % G; the last arrival of each group
+  // takes a top-level ticket, and the last of those reduces (same drain-then-atomic order
+  // at both levels, so every partial is at the coherence point before the final acquire).
+  const unsigned G = gridDim.x < kTicketGroups ? gridDim.x : kTicketGroups;
   if (threadIdx.x == 0) {
     __hip_atomic_store(&partials[blockIdx.x], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned prev =
-        __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    is_last = (prev == gridDim.x - 1);
+    const unsigned g = blockIdx.x % G;
+    const unsigned members = (gridDim.x - g + G - 1) / G;
+    const unsigned prev = __hip_atomic_fetch_add(ticket + g * kTicketStride, 1u,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int last = 0;
+    if (prev == members - 1) {
+      const unsigned top = __hip_atomic_fetch_add(ticket + kTicketGroups * kTicketStride, 1u,
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      last = (top == G - 1);
+    }
+    is_last = last;
   }
   __syncthreads();
   if (!is_last) return;
@@ -305,10 +317,13 @@ __global__ __launch_bounds__(B) void riemann_fused_kernel(RiemannParams p, const
   __syncthreads();
   const double v = ordered_partials<true>(partials, static_cast<int>(gridDim.x));
   const double tot = block_sum<B>(v, red + 0);
-  if (threadIdx.x == 0) {
-    out[0] = tot * scale;
-    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-  }
+  if (threadIdx.x == 0) out[0] = tot * scale;
+  if (threadIdx.x < G)  // re-arm: every group has arrived, nobody touches the ticket now
+    __hip_atomic_store(ticket + threadIdx.x * kTicketStride, 0u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0)
+    __hip_atomic_store(ticket + kTicketGroups * kTicketStride, 0u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------------------- validation

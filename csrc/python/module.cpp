@@ -74,6 +74,7 @@ PYBIND11_MODULE(_miint, m) {
       .value("ieee", DivMode::kIeee)
       .value("series_direct", DivMode::kSeriesDirect);
 
+  m.attr("TICKET_WORDS") = kTicketWords;
   m.attr("RIEMANN_TILE") = kRiemannTile;
   m.attr("RIEMANN_BLOCK") = kRiemannBlock;
   m.def("series_ok", &series_ok);

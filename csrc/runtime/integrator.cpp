@@ -52,8 +52,8 @@ RiemannPlan::RiemannPlan(const RiemannConfig& cfg, int device, const Comm* comm)
 
   partials_ = DeviceBuffer<double>(static_cast<size_t>(shape_.grid));
   result_ = DeviceBuffer<double>(static_cast<size_t>(cfg.slots));
-  ticket_ = DeviceBuffer<unsigned int>(1);
-  MIINT_HIP(hipMemset(ticket_.get(), 0, sizeof(unsigned int)));
+  ticket_ = DeviceBuffer<unsigned int>(kTicketWords);
+  MIINT_HIP(hipMemset(ticket_.get(), 0, ticket_.bytes()));
   MIINT_HIP(hipMemset(result_.get(), 0, result_.bytes()));
   if (cfg.integrand == Integrand::kTable) {
     MIINT_CHECK(cfg.table.size() >= 2, "table integrand needs a table");

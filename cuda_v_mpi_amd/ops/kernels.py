@@ -96,7 +96,7 @@ class FusedWorkspace:
         dev = device or _device()
         self.grid = grid
         self.partials = torch.empty(grid, dtype=torch.float64, device=dev)
-        self.ticket = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.ticket = torch.zeros(native().TICKET_WORDS, dtype=torch.int32, device=dev)
 
 
 def riemann(spec: IntegrandSpec, n: int, rule: str = "left", dtype: str = "fp64",

@@ -242,37 +242,26 @@ struct Pi4 : TileDefaults<Pi4> {
   }
 };
 
-// ------------------------------------------------------------------ sin(x), fp64
-//
-// kIeee: ocml sin per sample (~53 VALU per sample measured, with its range reduction).
-// kSeries (default): one ocml sincos per 64-sample tile at the midpoint x_m, re-centred to
-// four 16-sample sub-tiles (centres x_m + c0 h, c0 = -24, -8, 8, 24), then every sample by
-// the exact angle-addition formula
-//   sin(x_c +- k h) = S_c cos(k h) +- C_c sin(k h)
-// with cos/sin(k h) for the 8 pair offsets k = j + 1/2 and for the centres computed once per
-// launch on the host in long double (RiemannParams::trig, kernel arguments -> SGPRs).
+// ------------------------------------------------------------------ sin / cos by angle addition
+// Shared series path of Sin and TrainVel (both evaluate sin or cos of theta = w x):
+// one ocml sincos per 64-sample tile at the midpoint theta_m, re-centred to four 16-sample
+// sub-tiles (centres theta_m + c0 delta, c0 = -24, -8, 8, 24; delta = w h), then every
+// sample by the exact angle-addition formula
+//   sin(theta_c +- k delta) = S_c cos(k delta) +- C_c sin(k delta)
+//   cos(theta_c +- k delta) = C_c cos(k delta) -+ S_c sin(k delta)
+// with cos/sin(k delta) for the 8 pair offsets k = j + 1/2 and for the centres computed once
+// per launch on the host in long double (RiemannParams::trig, kernel arguments -> SGPRs).
 // Per pair: 1 mul + 2 fma for the two samples + 2 accumulations (2.5 VALU per sample).
-// No truncation (valid for any h). Per point: absolute error vs ocml sin <= 7.2e-16
-// measured (tests allow 4 ulp(1)); the sum agrees with the kIeee path to 2e-15 relative.
-// N = 1e9 on [0, pi]: 123 us per integration (8.1e12 subint/s) vs 1.53 ms with ocml sin.
-struct Sin : TileDefaults<Sin> {
-  static constexpr double kScale = 1.0;
+// No truncation (valid for any h).
+struct AngleSeries {
   static constexpr int kPairs = 8;
   static constexpr int kSub = 2 * kPairs;
   static constexpr int kSubs = 4;
   static constexpr int kSeriesTile = kSub * kSubs;
-  double ck[kPairs], sk[kPairs];  // cos(k_j h), sin(k_j h)
-  double cc[2], sc[2];            // cos/sin(8h), cos/sin(24h)
+  double ck[kPairs], sk[kPairs];  // cos(k_j delta), sin(k_j delta)
+  double cc[2], sc[2];            // cos/sin(8 delta), cos/sin(24 delta)
 
-  template <DivMode M>
-  __host__ __device__ static constexpr int tile_len() {
-    return M == DivMode::kSeries ? kSeriesTile : 32;
-  }
-  template <int U, DivMode M>
-  __device__ static constexpr double anchor() {
-    return M == DivMode::kSeries ? 0.5 * (U - 1) : 0.0;
-  }
-  __device__ __forceinline__ void init(const double* trig) {
+  __device__ __forceinline__ void init_trig(const double* trig) {
 #pragma unroll
     for (int j = 0; j < kPairs; ++j) {
       ck[j] = trig[j];
@@ -291,43 +280,70 @@ struct Sin : TileDefaults<Sin> {
     Sq = fma(C, s, S * c);
     Cq = fma(-S, s, C * c);
   }
+  // sum over a 64-sample tile anchored at theta_m of sin (COS = false) or cos (COS = true)
+  template <bool COS>
+  __device__ __forceinline__ double tile_sum(double theta_m) const {
+    double S, C;
+    sincos(theta_m, &S, &C);
+    double t = 0.0;
+#pragma unroll
+    for (int q = 0; q < kSubs; ++q) {
+      double Sq, Cq;
+      centre(S, C, q, Sq, Cq);
+      const double base = COS ? Cq : Sq, side = COS ? -Sq : Cq;
+#pragma unroll
+      for (int j = 0; j < kPairs; ++j) {
+        const double u = base * ck[j];
+        t += fma(side, sk[j], u);   // theta_c + k_j delta
+        t += fma(-side, sk[j], u);  // theta_c - k_j delta
+        asm volatile("" : "+v"(t));  // keep program order (see Pi4)
+      }
+    }
+    return t;
+  }
+  // sample u of a full series tile, by exactly tile_sum's operations (validation kernel)
+  template <bool COS>
+  __device__ __forceinline__ double point_of(double theta_m, int u) const {
+    double S, C, Sq, Cq;
+    sincos(theta_m, &S, &C);
+    const int q = u / kSub, w = u % kSub;
+    centre(S, C, q, Sq, Cq);
+    const double base = COS ? Cq : Sq, side = COS ? -Sq : Cq;
+    const int j = w >= kSub / 2 ? w - kSub / 2 : kSub / 2 - 1 - w;
+    const double v = base * ck[j];
+    return w >= kSub / 2 ? fma(side, sk[j], v) : fma(-side, sk[j], v);
+  }
+};
 
+// ------------------------------------------------------------------ sin(x), fp64
+// kIeee: ocml sin per sample (~53 VALU per sample measured, with its range reduction).
+// kSeries (default): AngleSeries with w = 1. Per point: absolute error vs ocml sin
+// <= 7.2e-16 measured (tests allow 4 ulp(1)); the sum agrees with the kIeee path to 2e-15
+// relative. N = 1e9 on [0, pi]: 112 us per integration (8.9e12 subint/s) vs 1.53 ms.
+struct Sin : TileDefaults<Sin>, AngleSeries {
+  static constexpr double kScale = 1.0;
+  template <DivMode M>
+  __host__ __device__ static constexpr int tile_len() {
+    return M == DivMode::kSeries ? kSeriesTile : 32;
+  }
+  template <int U, DivMode M>
+  __device__ static constexpr double anchor() {
+    return M == DivMode::kSeries ? 0.5 * (U - 1) : 0.0;
+  }
+  __device__ __forceinline__ void init(const double* trig) { init_trig(trig); }
   __device__ __forceinline__ double point(double x) const { return sin(x); }
   template <int U, DivMode M>
   __device__ __forceinline__ double tile_acc(double xa, double h, double acc) const {
     if constexpr (M == DivMode::kSeries) {
-      static_assert(U == kSeriesTile, "sin series tiles are kSubs sub-tiles of kSub samples");
-      double S, C;
-      sincos(xa, &S, &C);
-      double t = 0.0;
-#pragma unroll
-      for (int q = 0; q < kSubs; ++q) {
-        double Sq, Cq;
-        centre(S, C, q, Sq, Cq);
-#pragma unroll
-        for (int j = 0; j < kPairs; ++j) {
-          const double u = Sq * ck[j];
-          t += fma(Cq, sk[j], u);   // sin(x_c + k_j h)
-          t += fma(-Cq, sk[j], u);  // sin(x_c - k_j h)
-          asm volatile("" : "+v"(t));  // keep program order (see Pi4)
-        }
-      }
-      return acc + t;
+      static_assert(U == kSeriesTile, "angle series tiles are 64 samples");
+      return acc + tile_sum<false>(xa);
     } else {
       return acc + tile<U, M>(xa, h);
     }
   }
-  // sample u of a full series tile, by exactly tile_acc's operations (validation kernel)
   __device__ __forceinline__ double series_point(double xm, int u) const {
-    double S, C, Sq, Cq;
-    sincos(xm, &S, &C);
-    const int q = u / kSub, w = u % kSub;
-    centre(S, C, q, Sq, Cq);
-    const int j = w >= kSub / 2 ? w - kSub / 2 : kSub / 2 - 1 - w;
-    const double v = Sq * ck[j];
-    return w >= kSub / 2 ? fma(Cq, sk[j], v) : fma(-Cq, sk[j], v);
+    return point_of<false>(xm, u);
   }
-
   template <int U, DivMode>
   __device__ __forceinline__ double tile(double x0, double h) const {
     // ocml sin is ~40 VALU ops with its own range reduction; unrolling it fully blows the
@@ -343,13 +359,23 @@ struct Sin : TileDefaults<Sin> {
 };
 
 // ------------------------------------------------------------------ polynomial
-struct Poly : TileDefaults<Poly> {
+// Horner over a compile-time bucket of NC coefficients (4, 8 or 16), zero-padded at the top
+// (leading zeros keep r == 0 exactly). The coefficients are copied into the functor once
+// per kernel (uniform -> SGPRs): a runtime-length loop over a kernarg pointer reloaded every
+// coefficient of every sample through the scalar cache (1.19 ms per 1e9 samples at degree 6
+// vs this form's NC fma per sample).
+template <int NC>
+struct Poly : TileDefaults<Poly<NC>> {
   static constexpr double kScale = 1.0;
-  const double* c;  // points into the kernarg block (uniform -> SGPR loads)
-  int n;
+  double c[NC];
+  __device__ __forceinline__ void init(const double* coef, int n) {
+#pragma unroll
+    for (int k = 0; k < NC; ++k) c[k] = k < n ? coef[k] : 0.0;
+  }
   __device__ __forceinline__ double point(double x) const {
-    double r = 0.0;
-    for (int k = n - 1; k >= 0; --k) r = fma(r, x, c[k]);
+    double r = c[NC - 1];
+#pragma unroll
+    for (int k = NC - 2; k >= 0; --k) r = fma(r, x, c[k]);
     return r;
   }
   template <int U, DivMode>
@@ -364,11 +390,32 @@ struct Poly : TileDefaults<Poly> {
 // ------------------------------------------------------------------ analytic train velocity
 // v(t) = (1 - cos(t/ts)) * vs   (riemann.cpp:108-111). Integral over [0,1800] is
 // dis_function(1800) = vs*(1800 - ts*sin(1800/ts)) ~= 121999.99983.
-struct TrainVel : TileDefaults<TrainVel> {
+// kSeries: AngleSeries with w = 1/ts on cos; tile value vs (U - sum cos).
+struct TrainVel : TileDefaults<TrainVel>, AngleSeries {
   double inv_ts, vs;
   static constexpr double kScale = 1.0;
+  template <DivMode M>
+  __host__ __device__ static constexpr int tile_len() {
+    return M == DivMode::kSeries ? kSeriesTile : 32;
+  }
+  template <int U, DivMode M>
+  __device__ static constexpr double anchor() {
+    return M == DivMode::kSeries ? 0.5 * (U - 1) : 0.0;
+  }
   __device__ __forceinline__ double point(double t) const {
     return (1.0 - cos(t * inv_ts)) * vs;
+  }
+  template <int U, DivMode M>
+  __device__ __forceinline__ double tile_acc(double ta, double h, double acc) const {
+    if constexpr (M == DivMode::kSeries) {
+      static_assert(U == kSeriesTile, "angle series tiles are 64 samples");
+      return fma(-vs, tile_sum<true>(ta * inv_ts), fma(vs, static_cast<double>(U), acc));
+    } else {
+      return acc + tile<U, M>(ta, h);
+    }
+  }
+  __device__ __forceinline__ double series_point(double tm, int u) const {
+    return (1.0 - point_of<true>(tm * inv_ts, u)) * vs;
   }
   template <int U, DivMode>
   __device__ __forceinline__ double tile(double x0, double h) const {

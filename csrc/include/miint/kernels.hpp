@@ -29,10 +29,12 @@ inline bool series_ok(double h) { return kSeriesHalfSpan * (h < 0 ? -h : h) <= 2
 inline DivMode effective_div(DivMode d, double h) {
   return (d != DivMode::kIeee && !series_ok(h)) ? DivMode::kIeee : d;
 }
-// Per integrand: sin's series path (angle addition from a per-tile sincos seed) is exact for
-// any h, so only the direct/ieee choice applies; integrands without a series path run kIeee.
+// Per integrand: the sin / train-velocity series path (angle addition from a per-tile sincos
+// seed) is exact for any h, so only the series/ieee choice applies; integrands without a
+// series path run kIeee.
 inline DivMode effective_div(DivMode d, double h, Integrand f) {
-  if (f == Integrand::kSin) return d == DivMode::kSeries ? DivMode::kSeries : DivMode::kIeee;
+  if (f == Integrand::kSin || f == Integrand::kTrainVel)  // angle-addition series
+    return d == DivMode::kSeries ? DivMode::kSeries : DivMode::kIeee;
   if (f != Integrand::kPi4) return DivMode::kIeee;
   return effective_div(d, h);
 }

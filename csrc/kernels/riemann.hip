@@ -198,16 +198,22 @@ template <> struct Maker<Sin> {
     return f;
   }
 };
-template <> struct Maker<Poly> {
+template <int NC> struct Maker<Poly<NC>> {
   static constexpr int kLds = 1;
-  __device__ static Poly make(const RiemannParams& p, const double*, int, double*) {
-    return {{}, p.coef, p.ncoef};
+  __device__ static Poly<NC> make(const RiemannParams& p, const double*, int, double*) {
+    Poly<NC> f;
+    f.init(p.coef, p.ncoef);
+    return f;
   }
 };
 template <> struct Maker<TrainVel> {
   static constexpr int kLds = 1;
   __device__ static TrainVel make(const RiemannParams& p, const double*, int, double*) {
-    return {{}, 1.0 / p.p0, p.p1};
+    TrainVel f;
+    f.init_trig(p.trig);
+    f.inv_ts = 1.0 / p.p0;
+    f.vs = p.p1;
+    return f;
   }
 };
 template <> struct Maker<Table> {
@@ -347,7 +353,7 @@ __global__ __launch_bounds__(B) void point_values_kernel(RiemannParams p, const 
     if constexpr (M == DivMode::kSeries && __is_same(F, Pi4)) {
       // exactly the operations Pi4::tile_acc applies to sample u
       v = full ? f.series_point(xm, p.h, u) : f.point(x);
-    } else if constexpr (M == DivMode::kSeries && __is_same(F, Sin)) {
+    } else if constexpr (M == DivMode::kSeries && (__is_same(F, Sin) || __is_same(F, TrainVel))) {
       v = full ? f.series_point(xm, u) : f.point(x);
     } else if constexpr (M == DivMode::kSeriesDirect && __is_same(F, Pi4)) {
       const Pi4::Seed sd = Pi4::seed(xm, p.h);
@@ -394,8 +400,15 @@ void dispatch(const RiemannParams& p, DType dtype, DivMode m, A&&... a) {
       if (m == DivMode::kSeries) Op<DivMode::kSeries, Sin>::run(a...);
       else Op<DivMode::kIeee, Sin>::run(a...);
       return;
-    case Integrand::kPoly: Op<DivMode::kIeee, Poly>::run(a...); return;
-    case Integrand::kTrainVel: Op<DivMode::kIeee, TrainVel>::run(a...); return;
+    case Integrand::kPoly:  // coefficient bucket: 4, 8 or 16 (zero-padded)
+      if (p.ncoef <= 4) Op<DivMode::kIeee, Poly<4>>::run(a...);
+      else if (p.ncoef <= 8) Op<DivMode::kIeee, Poly<8>>::run(a...);
+      else Op<DivMode::kIeee, Poly<16>>::run(a...);
+      return;
+    case Integrand::kTrainVel:
+      if (m == DivMode::kSeries) Op<DivMode::kSeries, TrainVel>::run(a...);
+      else Op<DivMode::kIeee, TrainVel>::run(a...);
+      return;
     case Integrand::kTable: Op<DivMode::kIeee, Table>::run(a...); return;
   }
   fail("unknown integrand", __FILE__, __LINE__);
@@ -453,19 +466,24 @@ static DivMode effective_div(const RiemannParams& p, DivMode div) {
 }
 
 // Host-side constants of the Sin series path (long double; see Sin in integrands.hpp).
+// Host-side constants of the angle-addition series (long double; AngleSeries in
+// integrands.hpp): delta = h for sin, h / ts for the train velocity.
 static RiemannParams prepared(const RiemannParams& p, DivMode eff) {
   RiemannParams q = p;
-  if (static_cast<Integrand>(p.integrand) == Integrand::kSin && eff == DivMode::kSeries) {
-    const long double h = p.h;
-    for (int j = 0; j < Sin::kPairs; ++j) {
+  const Integrand f = static_cast<Integrand>(p.integrand);
+  if ((f == Integrand::kSin || f == Integrand::kTrainVel) && eff == DivMode::kSeries) {
+    const long double delta =
+        f == Integrand::kSin ? static_cast<long double>(p.h)
+                             : static_cast<long double>(p.h) / static_cast<long double>(p.p0);
+    for (int j = 0; j < AngleSeries::kPairs; ++j) {
       const long double k = j + 0.5L;
-      q.trig[j] = static_cast<double>(cosl(k * h));
-      q.trig[Sin::kPairs + j] = static_cast<double>(sinl(k * h));
+      q.trig[j] = static_cast<double>(cosl(k * delta));
+      q.trig[AngleSeries::kPairs + j] = static_cast<double>(sinl(k * delta));
     }
     for (int i = 0; i < 2; ++i) {
-      const long double c0 = Sin::kSub * (i + 0.5L);
-      q.trig[2 * Sin::kPairs + 2 * i] = static_cast<double>(cosl(c0 * h));
-      q.trig[2 * Sin::kPairs + 2 * i + 1] = static_cast<double>(sinl(c0 * h));
+      const long double c0 = AngleSeries::kSub * (i + 0.5L);
+      q.trig[2 * AngleSeries::kPairs + 2 * i] = static_cast<double>(cosl(c0 * delta));
+      q.trig[2 * AngleSeries::kPairs + 2 * i + 1] = static_cast<double>(sinl(c0 * delta));
     }
   }
   return q;

@@ -104,6 +104,22 @@ def test_sin_series_sum_matches_direct(cuda, n):
     assert abs(a - 2.0) < 2e-12 + 2.0 / n**2  # left rule on [0, pi]: O(h^2)
 
 
+def test_train_series_matches_direct(cuda):
+    """Train velocity vs(1 - cos(t/ts)) by the same angle-addition series: per point within
+    4 ulp(1) * vs of the ocml-cos path, the sum to 1e-14, and the analytic distance
+    dis_function(1800) = 121999.99983 (riemann.cpp:113-116) at N = 1e9."""
+    spec = integrands.train()
+    n = 10**9
+    for i0 in (0, n // 2 + 3, n - (1 << 16)):
+        v = kernels.point_values(spec, n, div="series", i_begin=i0, n_local=1 << 16)
+        w = kernels.point_values(spec, n, div="ieee", i_begin=i0, n_local=1 << 16)
+        assert float((v - w).abs().max()) <= 4 * 2.23e-16 * spec.p1
+    a = float(kernels.riemann(spec, n, div="series").item())
+    b = float(kernels.riemann(spec, n, div="ieee").item())
+    assert a == pytest.approx(b, rel=1e-14, abs=0)
+    assert a == pytest.approx(spec.analytic(), rel=1e-12)
+
+
 def test_pi4_1e9_left_error_is_truncation(cuda):
     v = float(kernels.riemann(integrands.pi4(), 10**9, rule="left").item())
     assert abs((v - math.pi) - 1e-9) < 1e-13   # left rule error = h exactly (SURVEY §6.1)
@@ -170,6 +186,29 @@ def test_block_ops(cuda, block):
     w = pad.view(-1, block)
     torch.testing.assert_close(sums, w.sum(1), rtol=1e-12, atol=1e-12)
     torch.testing.assert_close(scan, w.cumsum(1).flatten()[:n], rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("block", [64, 256, 1024])
+def test_block_ops_exact_and_nonfinite(cuda, block):
+    """Adversarial inputs. Integers below 2^40 with alternating signs make every partial
+    sum exact, so the DPP/LDS tree must equal the serial sum bitwise whatever its order;
+    an inf or nan anywhere in a block must reach that block's sum."""
+    g = torch.Generator(device="cpu").manual_seed(block)
+    n = 7 * block
+    ints = torch.randint(-(1 << 40), 1 << 40, (n,), generator=g).double()
+    ints[::3] *= -1
+    x = ints.cuda()
+    sums, scan = kernels.block_ops(x, block)
+    w = ints.view(-1, block)
+    assert torch.equal(sums.cpu(), w.sum(1))
+    assert torch.equal(scan.cpu(), w.cumsum(1).flatten())
+    y = torch.randn(n, dtype=torch.float64)
+    y[block + 5] = math.inf
+    y[3 * block + block - 1] = math.nan
+    ys, _ = kernels.block_ops(y.cuda(), block)
+    ys = ys.cpu()
+    assert math.isinf(float(ys[1])) and math.isnan(float(ys[3]))
+    assert all(math.isfinite(float(ys[b])) for b in (0, 2, 4, 5, 6))
 
 
 # ------------------------------------------------------------------ table kernels

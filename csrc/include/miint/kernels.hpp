@@ -126,6 +126,10 @@ struct Table2DParams {
 };
 int table2d_grid(const Table2DParams& p);
 void launch_table2d_partials(const Table2DParams& p, double* partials, hipStream_t stream);
+// One launch: partials + last-workgroup reduction into out[0] (ticket: kTicketWords words,
+// zero before the first launch, re-armed by the kernel; partials: table2d_grid(p) doubles).
+void launch_table2d_fused(const Table2DParams& p, double* partials, unsigned* ticket,
+                          double* out, hipStream_t stream);
 void launch_outer_product(const double* v, int n, double* table, hipStream_t stream);
 
 }  // namespace miint

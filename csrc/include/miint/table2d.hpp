@@ -29,7 +29,8 @@ struct Table2DConfig {
 class Table2DPlan {
  public:
   Table2DPlan(const Table2DConfig& cfg, int device, const Comm* comm = nullptr);
-  // One integration: kernel -> finalize -> [allreduce] -> pinned host. Returns the value.
+  // One integration: one fused kernel (result straight into pinned host memory on one
+  // rank) or kernel -> RCCL all-reduce -> 8-byte copy. Returns the value.
   double run();
   // `iters` back-to-back integrations; returns device ms per integration.
   double time(int iters);
@@ -45,6 +46,7 @@ class Table2DPlan {
   int row0_ = 0, row1_ = 0;
   Stream stream_;
   DeviceBuffer<double> v_, table_, partials_, result_;
+  DeviceBuffer<unsigned int> ticket_;
   PinnedBuffer<double> host_;
   Event e0_, e1_;
 };

@@ -22,6 +22,7 @@
 #include <cmath>
 
 #include "miint/common.hpp"
+#include "miint/handoff.hpp"
 #include "miint/integrands.hpp"
 #include "miint/kernels.hpp"
 #include "miint/wave_reduce.hpp"
@@ -240,35 +241,9 @@ __global__ __launch_bounds__(B) void riemann_kernel(RiemannParams p, const doubl
 // Same width and order as the fused kernel's last-workgroup sum (B threads, partial i
 // folded into thread i % B in increasing i), so both paths are bitwise identical.
 constexpr int kFinalBlock = B;
-constexpr int kFinalBatch = 16;  // loads in flight per thread (grid <= 4096: one batch)
-
-// Thread t sums partials t, t + B, t + 2B, ... in increasing order — the same order for
-// both paths. The loads of a batch are all issued before the first add: as a plain loop
-// every iteration waited for its load (s_waitcnt vmcnt(0)), i.e. grid/B serial memory round
-// trips (8 at grid 2048) at the end of every integration (~25 us at small N, measured).
-template <bool AGENT_SCOPE>
-__device__ __forceinline__ double ordered_partials(const double* partials, int n) {
-  double v = 0.0;
-  for (int base = 0; base < n; base += kFinalBatch * kFinalBlock) {
-    double r[kFinalBatch];
-#pragma unroll
-    for (int k = 0; k < kFinalBatch; ++k) {
-      const int i = base + k * kFinalBlock + static_cast<int>(threadIdx.x);
-      if constexpr (AGENT_SCOPE)
-        r[k] = i < n ? __hip_atomic_load(&partials[i], __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT)
-                     : 0.0;
-      else
-        r[k] = i < n ? partials[i] : 0.0;
-    }
-#pragma unroll
-    for (int k = 0; k < kFinalBatch; ++k) v += r[k];
-  }
-  return v;
-}
 
 __device__ __forceinline__ double ordered_sum(const double* partials, int n, double* red) {
-  return block_sum<kFinalBlock>(ordered_partials<false>(partials, n), red);
+  return block_sum<kFinalBlock>(ordered_partials<kFinalBlock, false>(partials, n), red);
 }
 
 __global__ __launch_bounds__(kFinalBlock) void finalize_kernel(const double* partials, int n,
@@ -279,12 +254,8 @@ __global__ __launch_bounds__(kFinalBlock) void finalize_kernel(const double* par
 }
 
 // ---------------------------------------------------------------------------- fused (ticket)
-// Every workgroup publishes its partial with an agent-scope (sc1, write-through) store,
-// drains it (s_waitcnt vmcnt(0)), then takes a ticket with an agent-scope atomic. The
-// workgroup that draws the last ticket acquires (buffer_inv sc1) and reduces all partials
-// in index order with sc1 loads — the R1 hand-off of cdna_hip_programming.md §6 G16.
-// Placement-independent: correctness never depends on which XCD a block lands on, and the
-// index-ordered final sum keeps the result bitwise identical to the two-kernel path.
+// One launch: partials, then the last-workgroup hand-off of handoff.hpp (sc1 publish,
+// two-level ticket, acquire, index-ordered sum) — bitwise identical to partials + finalize.
 template <DivMode M, class F>
 __global__ __launch_bounds__(B) void riemann_fused_kernel(RiemannParams p, const double* table,
                                                           int table_n, double* partials,
@@ -295,41 +266,11 @@ __global__ __launch_bounds__(B) void riemann_fused_kernel(RiemannParams p, const
   __shared__ int is_last;
   const F f = Maker<F>::make(p, table, table_n, lds);
   const double s = block_sum<B>(lane_sum<M>(p, f), red);
-  // Two-level ticket: workgroup b counts in group b % G; the last arrival of each group
-  // takes a top-level ticket, and the last of those reduces (same drain-then-atomic order
-  // at both levels, so every partial is at the coherence point before the final acquire).
-  const unsigned G = gridDim.x < kTicketGroups ? gridDim.x : kTicketGroups;
-  if (threadIdx.x == 0) {
-    __hip_atomic_store(&partials[blockIdx.x], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned g = blockIdx.x % G;
-    const unsigned members = (gridDim.x - g + G - 1) / G;
-    const unsigned prev = __hip_atomic_fetch_add(ticket + g * kTicketStride, 1u,
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int last = 0;
-    if (prev == members - 1) {
-      const unsigned top = __hip_atomic_fetch_add(ticket + kTicketGroups * kTicketStride, 1u,
-                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = (top == G - 1);
-    }
-    is_last = last;
-  }
-  __syncthreads();
-  if (!is_last) return;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  const double v = ordered_partials<true>(partials, static_cast<int>(gridDim.x));
-  const double tot = block_sum<B>(v, red + 0);
+  if (!publish_and_ticket(s, partials, ticket, blockIdx.x, gridDim.x, &is_last)) return;
+  const double v = ordered_partials<B, true>(partials, static_cast<int>(gridDim.x));
+  const double tot = block_sum<B>(v, red);
   if (threadIdx.x == 0) out[0] = tot * scale;
-  if (threadIdx.x < G)  // re-arm: every group has arrived, nobody touches the ticket now
-    __hip_atomic_store(ticket + threadIdx.x * kTicketStride, 0u, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  if (threadIdx.x == 0)
-    __hip_atomic_store(ticket + kTicketGroups * kTicketStride, 0u, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+  rearm_ticket(ticket, gridDim.x);
 }
 
 // ---------------------------------------------------------------------------- validation

@@ -263,6 +263,13 @@ PYBIND11_MODULE(_miint, m) {
     Table2DParams p{ptr<const double>(table), nx, ny, X, Y, gx, gy, row0, row1};
     launch_table2d_partials(p, ptr<double>(partials), stream(s));
   });
+  m.def("launch_table2d_fused", [](uintptr_t table, int nx, int ny, double X, double Y, int gx,
+                                    int gy, int row0, int row1, uintptr_t partials,
+                                    uintptr_t ticket, uintptr_t out, uintptr_t s) {
+    Table2DParams p{ptr<const double>(table), nx, ny, X, Y, gx, gy, row0, row1};
+    launch_table2d_fused(p, ptr<double>(partials), ptr<unsigned>(ticket), ptr<double>(out),
+                         stream(s));
+  });
   m.def("launch_outer_product", [](uintptr_t v, int n, uintptr_t t, uintptr_t s) {
     launch_outer_product(ptr<const double>(v), n, ptr<double>(t), stream(s));
   });

@@ -29,21 +29,26 @@ Table2DPlan::Table2DPlan(const Table2DConfig& cfg, int device, const Comm* comm)
                         row0_, std::max(row1_, row0_ + 1)};
   partials_ = DeviceBuffer<double>(static_cast<size_t>(table2d_grid(p)));
   result_ = DeviceBuffer<double>(1);
+  ticket_ = DeviceBuffer<unsigned int>(kTicketWords);
+  MIINT_HIP(hipMemset(ticket_.get(), 0, ticket_.bytes()));
   host_ = PinnedBuffer<double>(1);
   stream_.sync();
 }
 
 void Table2DPlan::enqueue(hipStream_t s) {
   const int n = static_cast<int>(oracle::profile_table().size());
+  const bool multi = comm_ && world_ > 1;
+  // one rank: the kernel's last workgroup stores straight into mapped pinned memory
+  double* out = multi ? result_.get() : host_.device_ptr();
   if (row1_ > row0_) {
     const Table2DParams p{table_.get(), n, n, cfg_.extent, cfg_.extent, cfg_.grid, cfg_.grid,
                           row0_, row1_};
-    launch_table2d_partials(p, partials_.get(), s);
-    launch_finalize(partials_.get(), table2d_grid(p), 1.0, result_.get(), s);
+    launch_table2d_fused(p, partials_.get(), ticket_.get(), out, s);
   } else {
     MIINT_HIP(hipMemsetAsync(result_.get(), 0, sizeof(double), s));  // more ranks than rows
   }
-  if (comm_ && world_ > 1) comm_->allreduce_sum(result_.get(), result_.get(), 1, s);
+  if (!multi) return;
+  comm_->allreduce_sum(result_.get(), result_.get(), 1, s);
   MIINT_HIP(hipMemcpyAsync(host_.get(), result_.get(), sizeof(double), hipMemcpyDeviceToHost, s));
 }
 

@@ -255,18 +255,25 @@ def outer_product(v: torch.Tensor) -> torch.Tensor:
 
 
 def table2d(table: torch.Tensor, X: float, Y: float, gx: int, gy: int, row0: int = 0,
-            row1: int | None = None) -> torch.Tensor:
+            row1: int | None = None, fused: bool = True) -> torch.Tensor:
     """Midpoint-rule integral of the bilinear interpolant of `table` (ny x nx) over
-    [0,X]x[0,Y] on a gx x gy grid, sample rows [row0, row1) only. 1-element tensor."""
+    [0,X]x[0,Y] on a gx x gy grid, sample rows [row0, row1) only. 1-element tensor.
+    fused: one launch with the last-workgroup reduction; else partials + finalize."""
     _check(table, name="table")
     ny, nx = table.shape
     row1 = gy if row1 is None else row1
     m = native()
     grid = m.table2d_grid(nx, ny, X, Y, gx, gy, row0, row1)
     partials = torch.empty(grid, dtype=torch.float64, device=table.device)
-    m.launch_table2d_partials(table.data_ptr(), nx, ny, X, Y, gx, gy, row0, row1,
-                              partials.data_ptr(), _stream())
-    return finalize(partials, 1.0)
+    if not fused:
+        m.launch_table2d_partials(table.data_ptr(), nx, ny, X, Y, gx, gy, row0, row1,
+                                  partials.data_ptr(), _stream())
+        return finalize(partials, 1.0)
+    ticket = torch.zeros(m.TICKET_WORDS, dtype=torch.int32, device=table.device)
+    out = torch.empty(1, dtype=torch.float64, device=table.device)
+    m.launch_table2d_fused(table.data_ptr(), nx, ny, X, Y, gx, gy, row0, row1,
+                           partials.data_ptr(), ticket.data_ptr(), out.data_ptr(), _stream())
+    return out
 
 
 def wave_ops(x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:

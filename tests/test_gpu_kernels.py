@@ -337,6 +337,37 @@ def test_table2d_separable_oracle(cuda):
     assert got == pytest.approx(122000.004 ** 2, rel=1e-5)
 
 
+def _bilinear_midpoint_sum(T, X, Y, gx, gy):
+    """torch fp64 reference: midpoint samples of the bilinear interpolant of T (ny x nx)."""
+    ny, nx = T.shape
+    xs = (torch.arange(gx, dtype=torch.float64, device=T.device) + 0.5) * (X / gx) * ((nx - 1) / X)
+    ys = (torch.arange(gy, dtype=torch.float64, device=T.device) + 0.5) * (Y / gy) * ((ny - 1) / Y)
+    ix = xs.long().clamp(0, nx - 2)
+    iy = ys.long().clamp(0, ny - 2)
+    fx = (xs - ix).unsqueeze(0)
+    fy = (ys - iy).unsqueeze(1)
+    v00 = T[iy][:, ix]
+    v01 = T[iy][:, ix + 1]
+    v10 = T[iy + 1][:, ix]
+    v11 = T[iy + 1][:, ix + 1]
+    top = v00 + (v01 - v00) * fx
+    bot = v10 + (v11 - v10) * fx
+    return float((top + (bot - top) * fy).sum()) * (X / gx) * (Y / gy)
+
+
+@pytest.mark.parametrize("shape,grid", [((37, 53), (300, 211)),      # LDS-tiled path
+                                        ((1801, 1801), (64, 96))])   # coarse: global path
+def test_table2d_general_table_vs_torch(cuda, shape, grid):
+    """A random (non-separable) table: the 2-D kernel is a general bilinear integrator."""
+    g = torch.Generator(device="cpu").manual_seed(shape[0])
+    T = torch.rand(shape, generator=g, dtype=torch.float64).cuda()
+    X, Y = 3.7, 2.1
+    got = float(kernels.table2d(T, X, Y, grid[0], grid[1]).item())
+    assert got == pytest.approx(_bilinear_midpoint_sum(T, X, Y, grid[0], grid[1]), rel=1e-13)
+    unfused = float(kernels.table2d(T, X, Y, grid[0], grid[1], fused=False).item())
+    assert got == unfused  # same partials, same index-ordered final sum
+
+
 def test_table2d_row_split(cuda):
     v = torch.as_tensor(fixtures.profile_table(), device="cuda")
     T = kernels.outer_product(v)

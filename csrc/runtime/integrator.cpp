@@ -45,7 +45,8 @@ RiemannPlan::RiemannPlan(const RiemannConfig& cfg, int device, const Comm* comm)
   const DeviceInfo info = device_info(device);
   shape_ = default_riemann_shape(info.num_cus, cfg.waves_per_cu);
   if (cfg.grid > 0) shape_.grid = cfg.grid;
-  // Never launch more workgroups than there are tiles to deal out.
+  // Never launch more workgroups than there are tiles to deal out (counted at the smallest
+  // tile length, 32 samples; series paths use 64).
   const uint64_t tiles = (params_.n + kRiemannTile - 1) / kRiemannTile;
   const uint64_t need = std::max<uint64_t>(1, (tiles + kRiemannBlock - 1) / kRiemannBlock);
   shape_.grid = static_cast<int>(std::min<uint64_t>(static_cast<uint64_t>(shape_.grid), need));

@@ -47,8 +47,8 @@ struct TileDefaults {
 // (~14 VALU f64 ops per sample with the coordinate and the accumulation).
 //
 // The series paths evaluate the same reciprocal per point from a per-tile seed:
-//   s  ~= 1/d(x_m)                   (v_rcp_f64 + one Newton step, once per tile;
-//                                     x_m = tile midpoint)
+//   s  ~= 1/d(x_m)                   (v_rcp_f64 once per tile; x_m = tile midpoint; the
+//                                     kSeriesDirect seed adds one Newton step)
 //   e_u = 1 - d(x_u)*s               (the point's exact residual)
 //   1/d(x_u) = s*(1 + e_u + e_u^2 + e_u^3/(1-e_u))
 // |e_u| <= |e_m| + (U/2)*h (max of 2|x|/(1+x^2) is 1), so the dropped e^3 term is < 1e-17
@@ -67,12 +67,14 @@ struct TileDefaults {
 // g_{+-k} = c_k +- k A. c_k is formed directly with one fma from an SGPR k^2 (no running
 // recurrence: increments of ~1e-17 would be lost against ulp(1/2)). Per PAIR of samples:
 // 1 fma for c_k, 2 for g, 2 accumulations = 2.5 VALU per sample.
-// A 64-sample tile is 4 sub-tiles of 16 whose centres sit at c0 = -24, -8, 8, 24 steps from
-// x_m; re-expanding the exact quadratic there gives e_c = e_m + c0 A + c0^2 B and slope
-// A' = A + 2 c0 B (3 fma per sub-tile, against ~12 for a fresh seed). Keeping sub-tiles at
-// 8 pairs keeps the constants at 22 SGPR pairs: 79 SGPRs, 8 resident workgroups per CU.
-// Measured (gfx950 .s): 183 VALU per 64-sample tile = 2.86 per sample (the previous form,
-// t += e; t = fma(e, e, t) with one seed per 32 samples, was 127 per 32 = 3.97).
+// A 128-sample tile is 8 sub-tiles of 16 whose centres sit at c0 = -56, -40, ..., 40, 56
+// steps from x_m; re-expanding the exact quadratic there gives e_c = e_m + c0 A + c0^2 B and
+// slope A' = A + 2 c0 B (3 fma per sub-tile, against ~10 for a fresh seed). Sub-tiles of 8
+// pairs keep the constants at 21 SGPR pairs: 83 SGPRs (96 allocated), 8 resident
+// workgroups per CU.
+// Measured (gfx950 .s): 354 VALU per 128-sample tile = 2.77 per sample (64-sample tiles with
+// a Newton step: 183 per 64 = 2.86; the first form, t += e; t = fma(e, e, t) with one seed
+// per 32 samples: 127 per 32 = 3.97).
 //
 // Accuracy: every sample still gets its own residual and its own contribution. Per point,
 // g is rounded at ulp(1/2) scale: <= 5 ulp vs IEEE division, 91 % within 1 ulp, 99.4 %
@@ -82,8 +84,8 @@ struct Pi4 : TileDefaults<Pi4> {
   static constexpr double kScale = 4.0;
   static constexpr int kPairs = 8;                  // sample pairs per sub-tile
   static constexpr int kSub = 2 * kPairs;           // 16 samples per sub-tile
-  static constexpr int kSubs = 4;                   // sub-tiles per series tile
-  static constexpr int kSeriesTile = kSub * kSubs;  // 64 samples per seed
+  static constexpr int kSubs = 8;                   // sub-tiles per series tile
+  static constexpr int kSeriesTile = kSub * kSubs;  // 128 samples per seed
 
   template <DivMode M>
   __host__ __device__ static constexpr int tile_len() {
@@ -97,9 +99,8 @@ struct Pi4 : TileDefaults<Pi4> {
   static constexpr double kMeanK2 = 21.25;
   double pk[kPairs];         // k_j = j + 1/2
   double pk2[kPairs];        // k_j^2 - kMeanK2
-  double pc[kSubs / 2];      // |sub-tile centre offset| c0: 8, 24
+  double pc[kSubs / 2];      // |sub-tile centre offset| c0: 8, 24, 40, 56
   double pcm[kSubs / 2];     // c0 + kMeanK2 / c0
-  double pc2[kSubs / 2];     // 2 c0: 16, 48
   double c15;                // 3/2 (e_m + 1/2 = 3/2 - d_m s in one fma)
 
   __device__ __forceinline__ static double opaque_s(double v) {
@@ -117,7 +118,6 @@ struct Pi4 : TileDefaults<Pi4> {
       const double c0 = kSub * (i + 0.5);
       pc[i] = opaque_s(c0);
       pcm[i] = opaque_s(c0 + kMeanK2 / c0);
-      pc2[i] = opaque_s(2.0 * c0);
     }
     c15 = opaque_s(1.5);
   }
@@ -134,11 +134,13 @@ struct Pi4 : TileDefaults<Pi4> {
     s = fma(s, fma(-dm, s, 1.0), s);  // one Newton step
     return {s, fma(-dm, s, 1.0), (-2.0 * h) * xm * s, -(h * h) * s};
   }
-  // kSeries seed: as seed() but with eh = 1/2 + e_m rounded once (3/2 - d_m s).
+  // kSeries seed: the raw v_rcp_f64 — no Newton step: the series is exact for any seed whose
+  // residual keeps e^3 negligible (e_m is formed from the s actually used), and the per-point
+  // error distribution measured with and without the step is the same (max 5 ulp) — with
+  // eh = 1/2 + e_m rounded once (3/2 - d_m s).
   __device__ __forceinline__ Seed seed_half(double xm, double h) const {
     const double dm = fma(xm, xm, 1.0);
-    double s = __builtin_amdgcn_rcp(dm);
-    s = fma(s, fma(-dm, s, 1.0), s);  // one Newton step
+    const double s = __builtin_amdgcn_rcp(dm);
     return {s, fma(-dm, s, c15), (-2.0 * h) * xm * s, -(h * h) * s};
   }
   // Sub-tile q's centre offset c0 (in steps from x_m), c0 + kMeanK2/c0 and 2 c0, from the
@@ -155,8 +157,10 @@ struct Pi4 : TileDefaults<Pi4> {
   __device__ __forceinline__ double centre_g(const Seed& sd, int q) const {
     return fma(side(pc, q), fma(side(pcm, q), sd.b, sd.a), sd.em);
   }
-  __device__ __forceinline__ double centre_slope(const Seed& sd, int q) const {
-    return fma(side(pc2, q), sd.b, sd.a);
+  // slope at the centre, A + 2 c0 B, from b2 = 2 B (formed once per tile: a 2 c0 table would
+  // push the kernel past 96 allocated SGPRs, i.e. 7 instead of 8 resident workgroups per CU)
+  __device__ __forceinline__ double centre_slope(const Seed& sd, double b2, int q) const {
+    return fma(side(pc, q), b2, sd.a);
   }
 
   template <int U, DivMode M>
@@ -201,6 +205,7 @@ struct Pi4 : TileDefaults<Pi4> {
     if constexpr (M == DivMode::kSeries) {
       static_assert(U == kSeriesTile, "series tiles are kSubs sub-tiles of kSub samples");
       const Seed sd = seed_half(xa, h);
+      const double b2 = 2.0 * sd.b;
       // One running sum for the whole tile, started at the tile's U * 3/4. Its rounding
       // (ulp(64) ~ 1.4e-14) is far below the lane accumulator's it is folded into (~1.5e3
       // after 30 tiles, ulp 2.3e-13); a single chain is fine at 8 waves per SIMD.
@@ -208,7 +213,7 @@ struct Pi4 : TileDefaults<Pi4> {
 #pragma unroll
       for (int q = 0; q < kSubs; ++q) {
         const double eh = centre_g(sd, q);     // 1/2 + e at the centre (+ mean k^2 B)
-        const double a = centre_slope(sd, q);  // slope there
+        const double a = centre_slope(sd, b2, q);  // slope there
 #pragma unroll
         for (int j = 0; j < kPairs; ++j) {
           const double c = fma(pk2[j], sd.b, eh);
@@ -232,9 +237,10 @@ struct Pi4 : TileDefaults<Pi4> {
   // it (validation kernel): s * (3/4 + g_u^2).
   __device__ __forceinline__ double series_point(double xm, double h, int u) const {
     const Seed sd = seed_half(xm, h);
+    const double b2 = 2.0 * sd.b;
     const int q = u / kSub, w = u % kSub;
     const double eh = centre_g(sd, q);
-    const double a = centre_slope(sd, q);
+    const double a = centre_slope(sd, b2, q);
     const int j = w >= kSub / 2 ? w - kSub / 2 : kSub / 2 - 1 - w;
     const double c = fma(pk2[j], sd.b, eh);
     const double g = w >= kSub / 2 ? fma(pk[j], a, c) : fma(-pk[j], a, c);

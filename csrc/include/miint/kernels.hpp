@@ -19,7 +19,7 @@ enum class DType : int { kF64 = 0, kF32 = 1 };
 // Tile (unroll) size of the Riemann kernels: U consecutive samples per lane per step.
 constexpr int kRiemannTile = 32;     // default samples per lane tile (Pi4 series: 64)
 constexpr int kRiemannBlock = 256;
-constexpr int kSeriesHalfSpan = 32;  // max |sample offset| from a Pi4 series seed, in steps
+constexpr int kSeriesHalfSpan = 64;  // max |sample offset| from a Pi4 series seed, in steps
 
 // True when the fp64 Pi4 series reciprocal is exact to fp64 for this h (see integrands.hpp).
 inline bool series_ok(double h) { return kSeriesHalfSpan * (h < 0 ? -h : h) <= 2e-6; }

@@ -13,7 +13,7 @@ from cuda_v_mpi_amd.ops import kernels  # noqa: E402
 
 spec = integrands.pi4()
 CH = 1 << 20
-for n in (10**9, 10**8, 17_000_000):
+for n in (10**9, 10**8, 33_000_000):
     hist = torch.zeros(8, dtype=torch.int64)
     worst = 0.0
     ssum, cnt = 0.0, 0

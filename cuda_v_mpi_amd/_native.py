@@ -3,7 +3,9 @@
 The extension is built by ``make ext`` (``__graft_entry__.build()`` does this) into this
 package directory so that it travels with the repository snapshot and is what every GPU
 test and the benchmark actually load. There is deliberately **no** Python fallback for the
-GPU kernels: if the extension is missing or stale, :func:`native` raises loudly.
+GPU kernels: if the extension is missing and cannot be built, :func:`native` raises loudly.
+A missing extension is built on first import; a stale one (older than its sources) is loaded
+with a warning unless ``MIINT_AUTOBUILD=1`` (never rebuild behind a profiler's back).
 """
 from __future__ import annotations
 
@@ -59,9 +61,21 @@ def native(auto_build: bool = True):
     with _lock:
         if _mod is not None:
             return _mod
-        if auto_build and os.environ.get("MIINT_NO_AUTOBUILD") != "1" and is_stale():
-            build()
         so = extension_path()
+        if auto_build and os.environ.get("MIINT_NO_AUTOBUILD") != "1":
+            if not os.path.exists(so):
+                if "rocprofiler" in os.environ.get("LD_PRELOAD", ""):
+                    # under a profiler preload every child process initialises the GPU,
+                    # and `make` / `sh` exec'ing from it is refused on the GPU pool
+                    raise ImportError(f"miint native extension not found at {so}; build it "
+                                      "(make ext) before profiling")
+                build()
+            elif is_stale():
+                if os.environ.get("MIINT_AUTOBUILD") == "1":
+                    build()
+                else:  # load what is there (a fresh box may reorder mtimes), but say so
+                    print(f"miint: warning: {so} is older than its sources; run `make ext` "
+                          "(MIINT_AUTOBUILD=1 rebuilds automatically)", file=sys.stderr)
         if not os.path.exists(so):
             raise ImportError(
                 f"miint native extension not found at {so}; run `make ext` in {_REPO}")

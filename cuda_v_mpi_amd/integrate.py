@@ -171,10 +171,13 @@ class Integrator:
         return self._plan.run_steps(steps, pipeline, graphs)
 
     def launch_steps(self, steps: int, pipeline: bool = True, graphs: bool = True) -> None:
+        if self._plan is None:
+            raise RuntimeError("launch_steps needs backend='hip'")
         self._plan.launch_steps(steps, pipeline, graphs)
 
     def sync(self) -> None:
-        self._plan.sync()
+        if self._plan is not None:
+            self._plan.sync()
 
 
 def integrate(integrand: str = "pi4", n: int = 10**9, **kw) -> IntegrationResult:

@@ -5,8 +5,8 @@ Markers
         `-m gpu` on a GPU box. GPU tests never fall back to CPU paths: they exercise the
         in-tree native extension (cuda_v_mpi_amd/_miint*.so) and fail if it is missing.
 
-The native extension is (re)built once per session if sources are newer than the .so, so a
-fresh checkout works on both boxes.
+The native extension is built on first use if it is missing, so a fresh checkout works on
+both boxes (a stale one is loaded with a warning; `make ext` or MIINT_AUTOBUILD=1 rebuilds).
 """
 from __future__ import annotations
 
@@ -48,7 +48,8 @@ def pytest_collection_modifyitems(config, items):
 
 @pytest.fixture(scope="session")
 def native():
-    """The native module (built in-tree if stale). Loads without a GPU too."""
+    """The native module (built in-tree if missing; a stale one loads with a warning).
+    Loads without a GPU too."""
     from cuda_v_mpi_amd._native import native as load
 
     return load()

@@ -9,6 +9,13 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 : > gpurun_out/session.txt
+# Bring the in-tree build up to date from plain bash (no GPU initialised here), never from a
+# profiled or GPU-initialised process: under rocprofv3 --pmc every child process initialises
+# the GPU and exec'ing make/sh from it is refused on this pool.
+if ! make -q all >/dev/null 2>&1; then
+  echo "=== build out of date: make -j16 all" | tee -a gpurun_out/session.txt
+  make -j16 all > gpurun_out/build.txt 2>&1 || { echo "=== build failed"; exit 1; }
+fi
 for spec in "$@"; do
   name="${spec%%:*}"; rest="${spec#*:}"
   secs="${rest%%:*}"; cmd="${rest#*:}"

@@ -24,7 +24,12 @@ for g in G1 G2; do
   run pi4_series $g "${!g}" "$REPO/build/bin/miint" bench --iters 20
   run pi4_ieee $g "${!g}" "$REPO/build/bin/miint" bench --iters 10 --div ieee
   run pi4_fp32 $g "${!g}" "$REPO/build/bin/miint" bench --iters 20 --dtype fp32
-  run sin $g "${!g}" "$REPO/build/bin/miint" bench --iters 4 --integrand sin
+  run sin $g "${!g}" "$REPO/build/bin/miint" bench --iters 20 --integrand sin
+  run sin_ocml $g "${!g}" "$REPO/build/bin/miint" bench --iters 4 --integrand sin --div ieee
+  run train $g "${!g}" "$REPO/build/bin/miint" bench --iters 20 --integrand train
+  run poly $g "${!g}" "$REPO/build/bin/miint" bench --iters 10 --integrand poly
+  run table $g "${!g}" "$REPO/build/bin/miint" bench --iters 10 --integrand table
+  run table2d $g "${!g}" "$REPO/build/bin/miint" table2d
   run dpp_selftest $g "${!g}" python3 "$REPO/tools/dpp_probe.py"
 done
 for g in G1 G2 G3 G4; do

@@ -250,22 +250,25 @@ struct Pi4 : TileDefaults<Pi4> {
 
 // ------------------------------------------------------------------ sin / cos by angle addition
 // Shared series path of Sin and TrainVel (both evaluate sin or cos of theta = w x):
-// one ocml sincos per 64-sample tile at the midpoint theta_m, re-centred to four 16-sample
-// sub-tiles (centres theta_m + c0 delta, c0 = -24, -8, 8, 24; delta = w h), then every
+// one ocml sincos per 128-sample tile at the midpoint theta_m, re-centred to eight 16-sample
+// sub-tiles (centres theta_m + c0 delta, c0 = +-8, +-24, +-40, +-56; delta = w h), then every
 // sample by the exact angle-addition formula
 //   sin(theta_c +- k delta) = S_c cos(k delta) +- C_c sin(k delta)
 //   cos(theta_c +- k delta) = C_c cos(k delta) -+ S_c sin(k delta)
 // with cos/sin(k delta) for the 8 pair offsets k = j + 1/2 and for the centres computed once
 // per launch on the host in long double (RiemannParams::trig, kernel arguments -> SGPRs).
-// Per pair: 1 mul + 2 fma for the two samples + 2 accumulations (2.5 VALU per sample).
-// No truncation (valid for any h).
+// Per pair: 1 mul + 2 fma for the two samples + 2 accumulations (2.5 VALU per sample); the
+// sincos (~70 VALU) and the 4-op re-centring per sub-tile add ~0.8 per sample (64-sample
+// tiles: 1.3). Every centre comes straight from the tile midpoint (one rounding), so the
+// per-point error does not grow with the tile. No truncation (valid for any h).
 struct AngleSeries {
   static constexpr int kPairs = 8;
   static constexpr int kSub = 2 * kPairs;
-  static constexpr int kSubs = 4;
+  static constexpr int kSubs = 8;
   static constexpr int kSeriesTile = kSub * kSubs;
-  double ck[kPairs], sk[kPairs];  // cos(k_j delta), sin(k_j delta)
-  double cc[2], sc[2];            // cos/sin(8 delta), cos/sin(24 delta)
+  static_assert(2 * kPairs + kSubs == kSinTrig, "RiemannParams::trig layout");
+  double ck[kPairs], sk[kPairs];       // cos(k_j delta), sin(k_j delta)
+  double cc[kSubs / 2], sc[kSubs / 2];  // cos/sin(c0 delta), c0 = 8, 24, 40, 56
 
   __device__ __forceinline__ void init_trig(const double* trig) {
 #pragma unroll
@@ -273,12 +276,13 @@ struct AngleSeries {
       ck[j] = trig[j];
       sk[j] = trig[kPairs + j];
     }
-    cc[0] = trig[2 * kPairs];
-    sc[0] = trig[2 * kPairs + 1];
-    cc[1] = trig[2 * kPairs + 2];
-    sc[1] = trig[2 * kPairs + 3];
+#pragma unroll
+    for (int i = 0; i < kSubs / 2; ++i) {
+      cc[i] = trig[2 * kPairs + 2 * i];
+      sc[i] = trig[2 * kPairs + 2 * i + 1];
+    }
   }
-  // sin and cos at the centre of sub-tile q (centre offsets -24, -8, 8, 24 steps)
+  // sin and cos at the centre of sub-tile q (centre offsets -56, -40, ..., 40, 56 steps)
   __device__ __forceinline__ void centre(double S, double C, int q, double& Sq,
                                          double& Cq) const {
     const int i = q < kSubs / 2 ? kSubs / 2 - 1 - q : q - kSubs / 2;
@@ -286,7 +290,7 @@ struct AngleSeries {
     Sq = fma(C, s, S * c);
     Cq = fma(-S, s, C * c);
   }
-  // sum over a 64-sample tile anchored at theta_m of sin (COS = false) or cos (COS = true)
+  // sum over a series tile anchored at theta_m of sin (COS = false) or cos (COS = true)
   template <bool COS>
   __device__ __forceinline__ double tile_sum(double theta_m) const {
     double S, C;
@@ -325,7 +329,7 @@ struct AngleSeries {
 // kIeee: ocml sin per sample (~53 VALU per sample measured, with its range reduction).
 // kSeries (default): AngleSeries with w = 1. Per point: absolute error vs ocml sin
 // <= 7.2e-16 measured (tests allow 4 ulp(1)); the sum agrees with the kIeee path to 2e-15
-// relative. N = 1e9 on [0, pi]: 112 us per integration (8.9e12 subint/s) vs 1.53 ms.
+// relative. N = 1e9 on [0, pi]: 103.5 us per integration (9.66e12 subint/s) vs 1.53 ms.
 struct Sin : TileDefaults<Sin>, AngleSeries {
   static constexpr double kScale = 1.0;
   template <DivMode M>
@@ -341,7 +345,7 @@ struct Sin : TileDefaults<Sin>, AngleSeries {
   template <int U, DivMode M>
   __device__ __forceinline__ double tile_acc(double xa, double h, double acc) const {
     if constexpr (M == DivMode::kSeries) {
-      static_assert(U == kSeriesTile, "angle series tiles are 64 samples");
+      static_assert(U == kSeriesTile, "angle series tiles are kSeriesTile samples");
       return acc + tile_sum<false>(xa);
     } else {
       return acc + tile<U, M>(xa, h);
@@ -414,7 +418,7 @@ struct TrainVel : TileDefaults<TrainVel>, AngleSeries {
   template <int U, DivMode M>
   __device__ __forceinline__ double tile_acc(double ta, double h, double acc) const {
     if constexpr (M == DivMode::kSeries) {
-      static_assert(U == kSeriesTile, "angle series tiles are 64 samples");
+      static_assert(U == kSeriesTile, "angle series tiles are kSeriesTile samples");
       return fma(-vs, tile_sum<true>(ta * inv_ts), fma(vs, static_cast<double>(U), acc));
     } else {
       return acc + tile<U, M>(ta, h);

@@ -406,7 +406,6 @@ static DivMode effective_div(const RiemannParams& p, DivMode div) {
   return miint::effective_div(div, p.h, static_cast<Integrand>(p.integrand));
 }
 
-// Host-side constants of the Sin series path (long double; see Sin in integrands.hpp).
 // Host-side constants of the angle-addition series (long double; AngleSeries in
 // integrands.hpp): delta = h for sin, h / ts for the train velocity.
 static RiemannParams prepared(const RiemannParams& p, DivMode eff) {
@@ -421,7 +420,7 @@ static RiemannParams prepared(const RiemannParams& p, DivMode eff) {
       q.trig[j] = static_cast<double>(cosl(k * delta));
       q.trig[AngleSeries::kPairs + j] = static_cast<double>(sinl(k * delta));
     }
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < AngleSeries::kSubs / 2; ++i) {
       const long double c0 = AngleSeries::kSub * (i + 0.5L);
       q.trig[2 * AngleSeries::kPairs + 2 * i] = static_cast<double>(cosl(c0 * delta));
       q.trig[2 * AngleSeries::kPairs + 2 * i + 1] = static_cast<double>(sinl(c0 * delta));

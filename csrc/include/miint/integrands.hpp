@@ -67,14 +67,14 @@ struct TileDefaults {
 // g_{+-k} = c_k +- k A. c_k is formed directly with one fma from an SGPR k^2 (no running
 // recurrence: increments of ~1e-17 would be lost against ulp(1/2)). Per PAIR of samples:
 // 1 fma for c_k, 2 for g, 2 accumulations = 2.5 VALU per sample.
-// A 128-sample tile is 8 sub-tiles of 16 whose centres sit at c0 = -56, -40, ..., 40, 56
-// steps from x_m; re-expanding the exact quadratic there gives e_c = e_m + c0 A + c0^2 B and
-// slope A' = A + 2 c0 B (3 fma per sub-tile, against ~10 for a fresh seed). Sub-tiles of 8
-// pairs keep the constants at 21 SGPR pairs: 83 SGPRs (96 allocated), 8 resident
-// workgroups per CU.
-// Measured (gfx950 .s): 354 VALU per 128-sample tile = 2.77 per sample (64-sample tiles with
-// a Newton step: 183 per 64 = 2.86; the first form, t += e; t = fma(e, e, t) with one seed
-// per 32 samples: 127 per 32 = 3.97).
+// A 128-sample tile is 4 sub-tiles of 32 whose centres sit at c0 = -48, -16, 16, 48 steps
+// from x_m; re-expanding the exact quadratic there gives e_c = e_m + c0 A + c0^2 B and
+// slope A' = A + 2 c0 B (3 fma per sub-tile, against ~10 for a fresh seed). The 16 pair
+// constants k_j and k_j^2 - kMeanK2 take 23 SGPR pairs plus 9 VGPR pairs: 89 SGPRs
+// (96 allocated) and 60 VGPRs, 8 resident workgroups per CU.
+// Measured (gfx950 .s, tools/isa_count.py): 342 VALU per 128-sample tile = 2.67 per sample
+// (8 sub-tiles of 16: 354 = 2.77; 64-sample tiles with a Newton step: 183 per 64 = 2.86;
+// the first form, t += e; t = fma(e, e, t) with one seed per 32 samples: 127 per 32 = 3.97).
 //
 // Accuracy: every sample still gets its own residual and its own contribution. Per point,
 // g is rounded at ulp(1/2) scale: <= 5 ulp vs IEEE division, 91 % within 1 ulp, 99.4 %
@@ -82,9 +82,9 @@ struct TileDefaults {
 // the IEEE path to 1e-15 relative and |error| at N = 1e9 is unchanged (4.4e-16, mid rule).
 struct Pi4 : TileDefaults<Pi4> {
   static constexpr double kScale = 4.0;
-  static constexpr int kPairs = 8;                  // sample pairs per sub-tile
-  static constexpr int kSub = 2 * kPairs;           // 16 samples per sub-tile
-  static constexpr int kSubs = 8;                   // sub-tiles per series tile
+  static constexpr int kPairs = 16;                 // sample pairs per sub-tile
+  static constexpr int kSub = 2 * kPairs;           // 32 samples per sub-tile
+  static constexpr int kSubs = 4;                   // sub-tiles per series tile
   static constexpr int kSeriesTile = kSub * kSubs;  // 128 samples per seed
 
   template <DivMode M>
@@ -92,26 +92,36 @@ struct Pi4 : TileDefaults<Pi4> {
     return M == DivMode::kSeries ? kSeriesTile : 32;
   }
 
-  // Constants held in SGPRs for the whole kernel (see init()). Every fma of the pair
-  // evaluation is then a 3-operand VOP3 v_fma_f64 with one SGPR source; as literals, hipcc
-  // has to use the 2-operand v_fmac_f64 and copy the shared operand with a v_mov_b64.
-  // Mean of k_j^2 over a sub-tile's pairs: sum_j (j + 1/2)^2 / 8 = 170/8.
-  static constexpr double kMeanK2 = 21.25;
-  double pk[kPairs];         // k_j = j + 1/2
-  double pk2[kPairs];        // k_j^2 - kMeanK2
-  double pc[kSubs / 2];      // |sub-tile centre offset| c0: 8, 24, 40, 56
-  double pcm[kSubs / 2];     // c0 + kMeanK2 / c0
+  // Constants held in registers for the whole kernel (see init()). Every fma of the pair
+  // evaluation is then a 3-operand VOP3 v_fma_f64 with register sources; as literals, hipcc
+  // has to use the 2-operand v_fmac_f64 and copy the shared operand with a v_mov_b64
+  // (gfx9 VOP3 takes no literal). k_j and the centre constants live in SGPRs; the 16
+  // k_j^2 - kMeanK2 would push the kernel past 96 allocated SGPRs (7 instead of 8 resident
+  // workgroups per CU), so they sit in VGPRs instead (32 of the 64 a wave may hold at 8 waves
+  // per SIMD), loaded once per kernel.
+  // Mean of k_j^2 over a sub-tile's pairs: sum_j (j + 1/2)^2 / 16 = 1364/16.
+  static constexpr double kMeanK2 = 85.25;
+  static constexpr int kPk2Sgpr = 7;  // pk2[j < 7] in SGPRs: fills the 96 (89 + 6 reserved)
+  double pk[kPairs];         // k_j = j + 1/2                          (SGPR)
+  double pk2[kPairs];        // k_j^2 - kMeanK2                        (VGPR)
+  double pc[kSubs / 2];      // |sub-tile centre offset| c0: 16, 48    (SGPR)
+  double pcm[kSubs / 2];     // c0 + kMeanK2 / c0                      (SGPR)
   double c15;                // 3/2 (e_m + 1/2 = 3/2 - d_m s in one fma)
 
   __device__ __forceinline__ static double opaque_s(double v) {
     asm volatile("" : "+s"(v));  // opaque -> stays an SGPR pair, never a literal
     return v;
   }
+  __device__ __forceinline__ static double opaque_v(double v) {
+    asm volatile("" : "+v"(v));  // opaque -> stays a VGPR pair
+    return v;
+  }
   __device__ __forceinline__ void init() {
 #pragma unroll
     for (int j = 0; j < kPairs; ++j) {
       pk[j] = opaque_s(j + 0.5);
-      pk2[j] = opaque_s((j + 0.5) * (j + 0.5) - kMeanK2);
+      const double k2 = (j + 0.5) * (j + 0.5) - kMeanK2;
+      pk2[j] = j < kPk2Sgpr ? opaque_s(k2) : opaque_v(k2);
     }
 #pragma unroll
     for (int i = 0; i < kSubs / 2; ++i) {

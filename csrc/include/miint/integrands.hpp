@@ -77,7 +77,7 @@ struct TileDefaults {
 // the first form, t += e; t = fma(e, e, t) with one seed per 32 samples: 127 per 32 = 3.97).
 //
 // Accuracy: every sample still gets its own residual and its own contribution. Per point,
-// g is rounded at ulp(1/2) scale: <= 5 ulp vs IEEE division, 91 % within 1 ulp, 99.4 %
+// g is rounded at ulp(1/2) scale: <= 5 ulp vs IEEE division, 92 % within 1 ulp, 99.5 %
 // within 2 (tools/ulp_probe.py, whole domain at three step sizes); the sum agrees with
 // the IEEE path to 1e-15 relative and |error| at N = 1e9 is unchanged (4.4e-16, mid rule).
 struct Pi4 : TileDefaults<Pi4> {

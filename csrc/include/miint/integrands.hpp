@@ -453,13 +453,54 @@ struct TrainVel : TileDefaults<TrainVel>, AngleSeries {
 // The 1801-sample table (14.4 KB) lives in LDS, loaded once per workgroup. Segment index is
 // clamped to [0, nseg-1] so t == 1800 interpolates the last segment instead of reading
 // past the end (the reference copies only 1800 of 1801 entries: cintegrate.cu:117,121).
+//
+// kIeee (the reference's per-sample form, cintegrate.cu:36-44): every sample forms its
+// coordinate, truncates it to a segment index, clamps, re-reads v[k] and v[k+1] from LDS and
+// interpolates: ~11 VALU + 2 LDS reads per sample.
+// kSeries (default): a 64-sample tile almost never straddles a knot (a segment holds
+// 1/h samples: 555 556 at N = 1e9 over [0, 1800], 10 000 at the reference's 1e4 samples/s),
+// and inside one segment the interpolant is the straight line v(x_m + k h) = v_m + k (d h).
+// The tile reads its segment once (v_m at the tile midpoint, slope D = d h), then every
+// sample is that line at its own offset from a sub-tile centre: one fma per sample plus its
+// accumulation (pairs at +-k share the centre and k), 2.2 VALU per sample with the tile
+// set-up. A lane whose tile straddles a knot takes the per-sample path for that tile (exec
+// divergence; at N = 1e9 one wave in ~140 has such a lane).
 struct Table : TileDefaults<Table> {
   const double* lds;  // LDS copy of the table
   int nseg;           // number of segments = entries - 1
   static constexpr double kScale = 1.0;
+  static constexpr int kPairs = 16;                 // sample pairs per sub-tile
+  static constexpr int kSub = 2 * kPairs;           // 32 samples per sub-tile
+  static constexpr int kSubs = 2;                   // sub-tile centres at -16, +16 steps
+  static constexpr int kSeriesTile = kSub * kSubs;  // 64 samples per segment read
+  double pk[kPairs];  // k_j = j + 1/2 (SGPR: VOP3 f64 ops take no literal on gfx9)
+  double c16;         // sub-tile centre offset
+  double hspan;       // (kSeriesTile - 1) / 2: tile midpoint to its end samples
+
+  __device__ __forceinline__ static double opaque_s(double v) {
+    asm volatile("" : "+s"(v));
+    return v;
+  }
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int j = 0; j < kPairs; ++j) pk[j] = opaque_s(j + 0.5);
+    c16 = opaque_s(0.5 * kSub);
+    hspan = opaque_s(0.5 * (kSeriesTile - 1));
+  }
+  template <DivMode M>
+  __host__ __device__ static constexpr int tile_len() {
+    return M == DivMode::kSeries ? kSeriesTile : 32;
+  }
+  template <int U, DivMode M>
+  __device__ static constexpr double anchor() {
+    return M == DivMode::kSeries ? 0.5 * (U - 1) : 0.0;
+  }
+  __device__ __forceinline__ int segment(double t) const {
+    const int i = static_cast<int>(t);
+    return i < 0 ? 0 : (i >= nseg ? nseg - 1 : i);
+  }
   __device__ __forceinline__ double point(double t) const {
-    int i = static_cast<int>(t);
-    i = i < 0 ? 0 : (i >= nseg ? nseg - 1 : i);
+    const int i = segment(t);
     const double fr = t - static_cast<double>(i);
     const double v0 = lds[i];
     const double v1 = lds[i + 1];
@@ -474,6 +515,57 @@ struct Table : TileDefaults<Table> {
       acc1 += point(fma(static_cast<double>(u + 1), h, x0));
     }
     return acc0 + acc1;
+  }
+  // Segment line of a tile: value at the midpoint and per-step slope; false if it straddles
+  // a knot (or a clamp boundary) and must be evaluated per sample.
+  __device__ __forceinline__ bool line(double xm, double h, double& vm, double& D) const {
+    const int i = segment(fma(-hspan, h, xm));
+    if (i != segment(fma(hspan, h, xm))) return false;
+    const double v0 = lds[i];
+    const double d = lds[i + 1] - v0;
+    vm = fma(d, xm - static_cast<double>(i), v0);
+    D = d * h;
+    return true;
+  }
+  template <int U, DivMode M>
+  __device__ __forceinline__ double tile_acc(double xm, double h, double acc) const {
+    if constexpr (M == DivMode::kSeries) {
+      static_assert(U == kSeriesTile, "segment tiles are kSubs sub-tiles of kSub samples");
+      double vm, D;
+      if (!line(xm, h, vm, D)) {  // rare: per sample, rolled (keeps the kernel's SGPRs <= 96)
+        const double x0 = fma(-hspan, h, xm);
+        double s0 = 0.0, s1 = 0.0;
+#pragma unroll 1
+        for (int u = 0; u < U; u += 2) {
+          s0 += point(fma(static_cast<double>(u), h, x0));
+          s1 += point(fma(static_cast<double>(u + 1), h, x0));
+        }
+        return acc + (s0 + s1);
+      }
+      double t = 0.0;
+#pragma unroll
+      for (int q = 0; q < kSubs; ++q) {
+        const double vc = fma(q == 0 ? -c16 : c16, D, vm);
+#pragma unroll
+        for (int j = 0; j < kPairs; ++j) {
+          t += fma(pk[j], D, vc);   // sample kSub/2 + j of the sub-tile
+          t += fma(-pk[j], D, vc);  // sample kSub/2 - 1 - j
+          asm volatile("" : "+v"(t));  // keep program order (see Pi4)
+        }
+      }
+      return acc + t;
+    } else {
+      return acc + tile<U, M>(xm, h);
+    }
+  }
+  // Sample u of a full segment tile by exactly tile_acc's operations (validation kernel).
+  __device__ __forceinline__ double series_point(double xm, double h, int u) const {
+    double vm, D;
+    if (!line(xm, h, vm, D)) return point(fma(static_cast<double>(u), h, fma(-hspan, h, xm)));
+    const int q = u / kSub, w = u % kSub;
+    const double vc = fma(q == 0 ? -c16 : c16, D, vm);
+    const int j = w >= kSub / 2 ? w - kSub / 2 : kSub / 2 - 1 - w;
+    return w >= kSub / 2 ? fma(pk[j], D, vc) : fma(-pk[j], D, vc);
   }
 };
 

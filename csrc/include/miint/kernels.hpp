@@ -30,10 +30,10 @@ inline DivMode effective_div(DivMode d, double h) {
   return (d != DivMode::kIeee && !series_ok(h)) ? DivMode::kIeee : d;
 }
 // Per integrand: the sin / train-velocity series path (angle addition from a per-tile sincos
-// seed) is exact for any h, so only the series/ieee choice applies; integrands without a
-// series path run kIeee.
+// seed) and the table's segment-line tiles are exact for any h, so only the series/ieee
+// choice applies; integrands without a series path run kIeee.
 inline DivMode effective_div(DivMode d, double h, Integrand f) {
-  if (f == Integrand::kSin || f == Integrand::kTrainVel)  // angle-addition series
+  if (f == Integrand::kSin || f == Integrand::kTrainVel || f == Integrand::kTable)
     return d == DivMode::kSeries ? DivMode::kSeries : DivMode::kIeee;
   if (f != Integrand::kPi4) return DivMode::kIeee;
   return effective_div(d, h);

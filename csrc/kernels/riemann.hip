@@ -119,17 +119,19 @@ struct Pi4F32 : TileDefaults<Pi4F32> {
     }
   }
 
-  // Default series path, midpoint-anchored, 64-sample tiles of two 32-sample sub-tiles
-  // (centres at -16 and +16 steps; e_c = e_m + c0 A + c0^2 B, A' = A + 2 c0 B: one seed per
-  // 64 samples). The pair residuals (e_{+k}, e_{-k}) = c_k + (k, -k) * A' are one
+  // Default series path, midpoint-anchored, 128-sample tiles of four 32-sample sub-tiles
+  // (centres at -48, -16, 16, 48 steps; e_c = e_m + c0 A + c0^2 B, A' = A + 2 c0 B: one seed
+  // per 128 samples; 64-sample tiles of two sub-tiles spent ~29 VALU of seed, coordinate and
+  // fp64 fold per 80 of pair work). The pair residuals (e_{+k}, e_{-k}) = c_k + (k, -k) * A' are one
   // v_pk_fma_f32 (op_sel broadcasts c_k), summed by one v_pk_add_f32, and the shared c_k of
   // TWO consecutive pairs advance together by one v_pk_fma_f32 with the exact steps
   // (k_{j+2}^2 - k_j^2, k_{j+3}^2 - k_{j+1}^2) = (4j+6, 4j+10) times B: 1.25 VALU per sample.
   // In fp32 the e^2 term (< 3e-16) is far below the format's 6e-8 and is not carried.
   static constexpr int kSubLen = 32;
+  static constexpr int kSubs = 4;
   template <DivMode M>
   __host__ __device__ static constexpr int tile_len() {
-    return M == DivMode::kSeries ? 2 * kSubLen : 32;
+    return M == DivMode::kSeries ? kSubs * kSubLen : 32;
   }
   template <int UU, DivMode M>
   __device__ static constexpr double anchor() {
@@ -138,7 +140,7 @@ struct Pi4F32 : TileDefaults<Pi4F32> {
   template <int UU, DivMode M>
   __device__ __forceinline__ double tile_acc(double xmd, double h, double acc) const {
     if constexpr (M == DivMode::kSeries) {
-      static_assert(UU == 2 * kSubLen, "fp32 series tiles are two 32-sample sub-tiles");
+      static_assert(UU == kSubs * kSubLen, "fp32 series tiles are four 32-sample sub-tiles");
       const float xm = static_cast<float>(xmd);
       const float hf = static_cast<float>(h);
       const float dm = fmaf(xm, xm, 1.0f);
@@ -150,8 +152,8 @@ struct Pi4F32 : TileDefaults<Pi4F32> {
       const f32x2 bb = {b, b};
       f32x2 t;
 #pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const float c0 = q == 0 ? -0.5f * kSubLen : 0.5f * kSubLen;
+      for (int q = 0; q < kSubs; ++q) {
+        const float c0 = (q - 0.5f * (kSubs - 1)) * kSubLen;
         const float ec = fmaf(c0, fmaf(c0, b, a), em);
         const float aq = fmaf(2.0f * c0, b, a);
         const f32x2 av = {aq, aq};
@@ -222,7 +224,9 @@ template <> struct Maker<Table> {
   __device__ static Table make(const RiemannParams&, const double* table, int n, double* lds) {
     for (int i = threadIdx.x; i < n; i += B) lds[i] = table[i];  // 14.4 KB, once per block
     __syncthreads();
-    return {{}, lds, n - 1};
+    Table f{{}, lds, n - 1};
+    f.init();
+    return f;
   }
 };
 
@@ -294,6 +298,8 @@ __global__ __launch_bounds__(B) void point_values_kernel(RiemannParams p, const 
     if constexpr (M == DivMode::kSeries && __is_same(F, Pi4)) {
       // exactly the operations Pi4::tile_acc applies to sample u
       v = full ? f.series_point(xm, p.h, u) : f.point(x);
+    } else if constexpr (M == DivMode::kSeries && __is_same(F, Table)) {
+      v = full ? f.series_point(xm, p.h, u) : f.point(x);
     } else if constexpr (M == DivMode::kSeries && (__is_same(F, Sin) || __is_same(F, TrainVel))) {
       v = full ? f.series_point(xm, u) : f.point(x);
     } else if constexpr (M == DivMode::kSeriesDirect && __is_same(F, Pi4)) {
@@ -350,7 +356,10 @@ void dispatch(const RiemannParams& p, DType dtype, DivMode m, A&&... a) {
       if (m == DivMode::kSeries) Op<DivMode::kSeries, TrainVel>::run(a...);
       else Op<DivMode::kIeee, TrainVel>::run(a...);
       return;
-    case Integrand::kTable: Op<DivMode::kIeee, Table>::run(a...); return;
+    case Integrand::kTable:
+      if (m == DivMode::kSeries) Op<DivMode::kSeries, Table>::run(a...);
+      else Op<DivMode::kIeee, Table>::run(a...);
+      return;
   }
   fail("unknown integrand", __FILE__, __LINE__);
 }

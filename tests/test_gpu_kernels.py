@@ -120,6 +120,24 @@ def test_train_series_matches_direct(cuda):
     assert a == pytest.approx(spec.analytic(), rel=1e-12)
 
 
+@pytest.mark.parametrize("n", [10**9, 18_000_000, 1_000_003])
+def test_table_segment_tiles_match_per_sample(cuda, n):
+    """Velocity-table integrand: the segment-line tiles (one segment read per 64 samples,
+    v = v_c +- k D per sample) against the reference-form per-sample interpolation at the
+    same index. 18e6 (the reference's 1e4 samples/s) and 1e6 put a knot inside many tiles,
+    so both the line path and the per-sample fallback of straddling tiles are checked.
+    Per point within 4 ulp of the value scale (v <= 87.15 m/s); sums to 1e-14."""
+    spec = integrands.table()
+    for i0 in (0, n // 3 + 17, n - (1 << 16)):
+        v = kernels.point_values(spec, n, rule="mid", div="series", i_begin=i0, n_local=1 << 16)
+        w = kernels.point_values(spec, n, rule="mid", div="ieee", i_begin=i0, n_local=1 << 16)
+        assert float((v - w).abs().max()) <= 4 * 2.0 ** -52 * 128
+    a = float(kernels.riemann(spec, n, rule="mid", div="series").item())
+    b = float(kernels.riemann(spec, n, rule="mid", div="ieee").item())
+    assert a == pytest.approx(b, rel=1e-14, abs=0)
+    assert a == pytest.approx(122000.004, rel=1e-9)
+
+
 def test_pi4_1e9_left_error_is_truncation(cuda):
     v = float(kernels.riemann(integrands.pi4(), 10**9, rule="left").item())
     assert abs((v - math.pi) - 1e-9) < 1e-13   # left rule error = h exactly (SURVEY §6.1)

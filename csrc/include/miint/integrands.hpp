@@ -463,10 +463,12 @@ struct TrainVel : TileDefaults<TrainVel>, AngleSeries {
 // The tile reads its segment once (v_m at the tile midpoint, slope D = d h), then every
 // sample is that line at its own offset from a sub-tile centre: one fma per sample plus its
 // accumulation (pairs at +-k share the centre and k), 2.2 VALU per sample with the tile
-// set-up. A lane whose tile straddles a knot takes the per-sample path for that tile (exec
-// divergence; at N = 1e9 one wave in ~140 has such a lane).
+// set-up. A lane whose tile straddles a knot evaluates that tile per sample in the
+// reference's form, with both segments' entries loaded once (exec divergence; at N = 1e9 one
+// wave in ~140 has such a lane, at 18e6 two in five). The table is read from global memory
+// (L2-resident), not staged in LDS.
 struct Table : TileDefaults<Table> {
-  const double* lds;  // LDS copy of the table
+  const double* lds;  // the table: LDS copy (kIeee) or the global array (kSeries)
   int nseg;           // number of segments = entries - 1
   static constexpr double kScale = 1.0;
   static constexpr int kPairs = 16;                 // sample pairs per sub-tile
@@ -516,32 +518,60 @@ struct Table : TileDefaults<Table> {
     }
     return acc0 + acc1;
   }
-  // Segment line of a tile: value at the midpoint and per-step slope; false if it straddles
-  // a knot (or a clamp boundary) and must be evaluated per sample.
-  __device__ __forceinline__ bool line(double xm, double h, double& vm, double& D) const {
-    const int i = segment(fma(-hspan, h, xm));
-    if (i != segment(fma(hspan, h, xm))) return false;
+  // Segments of a tile's first and last samples.
+  __device__ __forceinline__ void ends(double xm, double h, int& lo, int& hi) const {
+    lo = segment(fma(-hspan, h, xm));
+    hi = segment(fma(hspan, h, xm));
+  }
+  // Segment line of a one-segment tile: value at the midpoint and per-step slope.
+  __device__ __forceinline__ void line(double xm, double h, int i, double& vm, double& D) const {
     const double v0 = lds[i];
     const double d = lds[i + 1] - v0;
     vm = fma(d, xm - static_cast<double>(i), v0);
     D = d * h;
-    return true;
+  }
+  // Sample of a tile that straddles exactly one knot: the reference's per-sample
+  // interpolation (point()) with both segments' entries already in registers.
+  struct Knot {
+    int lo;
+    double v0, v1, d0, d1;
+  };
+  __device__ __forceinline__ Knot knot(int lo) const {
+    const double v0 = lds[lo], v1 = lds[lo + 1], v2 = lds[lo + 2];
+    return {lo, v0, v1, v1 - v0, v2 - v1};
+  }
+  __device__ __forceinline__ double knot_point(const Knot& k, double t) const {
+    const int i = segment(t);
+    const bool second = i != k.lo;
+    return fma(second ? k.d1 : k.d0, t - static_cast<double>(i), second ? k.v1 : k.v0);
   }
   template <int U, DivMode M>
   __device__ __forceinline__ double tile_acc(double xm, double h, double acc) const {
     if constexpr (M == DivMode::kSeries) {
       static_assert(U == kSeriesTile, "segment tiles are kSubs sub-tiles of kSub samples");
-      double vm, D;
-      if (!line(xm, h, vm, D)) {  // rare: per sample, rolled (keeps the kernel's SGPRs <= 96)
+      int lo, hi;
+      ends(xm, h, lo, hi);
+      if (lo != hi) {  // rare: per sample, rolled (keeps the kernel's SGPRs <= 96)
         const double x0 = fma(-hspan, h, xm);
         double s0 = 0.0, s1 = 0.0;
+        if (hi == lo + 1) {  // one knot: no memory access per sample
+          const Knot k = knot(lo);
+#pragma unroll 2
+          for (int u = 0; u < U; u += 2) {
+            s0 += knot_point(k, fma(static_cast<double>(u), h, x0));
+            s1 += knot_point(k, fma(static_cast<double>(u + 1), h, x0));
+          }
+        } else {  // coarse step: a tile spans several segments
 #pragma unroll 1
-        for (int u = 0; u < U; u += 2) {
-          s0 += point(fma(static_cast<double>(u), h, x0));
-          s1 += point(fma(static_cast<double>(u + 1), h, x0));
+          for (int u = 0; u < U; u += 2) {
+            s0 += point(fma(static_cast<double>(u), h, x0));
+            s1 += point(fma(static_cast<double>(u + 1), h, x0));
+          }
         }
         return acc + (s0 + s1);
       }
+      double vm, D;
+      line(xm, h, lo, vm, D);
       double t = 0.0;
 #pragma unroll
       for (int q = 0; q < kSubs; ++q) {
@@ -560,8 +590,14 @@ struct Table : TileDefaults<Table> {
   }
   // Sample u of a full segment tile by exactly tile_acc's operations (validation kernel).
   __device__ __forceinline__ double series_point(double xm, double h, int u) const {
+    int lo, hi;
+    ends(xm, h, lo, hi);
+    if (lo != hi) {
+      const double t = fma(static_cast<double>(u), h, fma(-hspan, h, xm));
+      return hi == lo + 1 ? knot_point(knot(lo), t) : point(t);
+    }
     double vm, D;
-    if (!line(xm, h, vm, D)) return point(fma(static_cast<double>(u), h, fma(-hspan, h, xm)));
+    line(xm, h, lo, vm, D);
     const int q = u / kSub, w = u % kSub;
     const double vc = fma(q == 0 ? -c16 : c16, D, vm);
     const int j = w >= kSub / 2 ? w - kSub / 2 : kSub / 2 - 1 - w;

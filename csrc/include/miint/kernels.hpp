@@ -77,6 +77,10 @@ void launch_riemann_fused(const RiemannParams& p, DType dtype, DivMode div, Laun
 void launch_riemann_point_values(const RiemannParams& p, DivMode div, const double* table,
                                  int table_n, double* out, hipStream_t stream);
 
+// Samples per lane tile of the kernel that launch_riemann_* would run for these arguments
+// (32; 64 or 128 on the series paths): host-side grid sizing.
+int riemann_tile_len(const RiemannParams& p, DType dtype, DivMode div);
+
 // Integrand scale factor (4 for Pi4, 1 otherwise).
 double integrand_scale(Integrand f);
 

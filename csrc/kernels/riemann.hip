@@ -230,15 +230,64 @@ template <> struct Maker<Table> {
   }
 };
 
+// Functor construction and LDS size per (division mode, integrand). The table's segment-line
+// tiles read two entries per 64 samples, so they read the (L2-resident, 14.4 KB) table from
+// global memory instead of staging it: at the reference's 18e6 samples the per-workgroup
+// staging (7 dependent load/store rounds, 2048 workgroups) was most of the kernel's 15.5 us.
+template <DivMode M, class F>
+constexpr int lds_words() {
+  if constexpr (__is_same(F, Table) && M == DivMode::kSeries) return 1;
+  else return Maker<F>::kLds;
+}
+template <DivMode M, class F>
+__device__ __forceinline__ F make_functor(const RiemannParams& p, const double* table, int n,
+                                          double* lds) {
+  if constexpr (__is_same(F, Table) && M == DivMode::kSeries) {
+    Table f{{}, table, n - 1};
+    f.init();
+    return f;
+  } else {
+    return Maker<F>::make(p, table, n, lds);
+  }
+}
+
+// The default grid (default_riemann_shape) deals 8 workgroups of 4 waves to every CU, i.e.
+// 8 waves per SIMD in ONE resident round. A kernel that fits fewer (more than 64 VGPRs or
+// ~96 SGPRs per wave) leaves 1/8 or more of the workgroups for a second, nearly empty round,
+// and the scheduler does not trade registers for occupancy by itself: the table's segment
+// tiles took 98 VGPRs (4 waves/SIMD), the sin/train series 105 SGPRs (7 waves/SIMD). Those
+// instantiations get amdgpu_waves_per_eu(8). The ones that already fit 8 keep the unhinted
+// kernel: the hint also changes their allocation (Pi4 series: 8 more VALU per tile, its
+// k^2 constants moved from SGPRs to VGPR copies).
+#define kFullOccupancy __attribute__((amdgpu_waves_per_eu(8, 8)))
+template <DivMode M, class F>
+constexpr bool occupancy_hint() {
+  if constexpr (__is_same(F, Pi4)) return M == DivMode::kSeriesDirect;
+  else if constexpr (__is_same(F, Pi4F32)) return M == DivMode::kIeee;
+  else return __is_same(F, Sin) || __is_same(F, TrainVel) || __is_same(F, Table);
+}
+
 // Partials kernel: one fp64 partial per workgroup.
+template <DivMode M, class F>
+__device__ __forceinline__ void partials_body(const RiemannParams& p, const double* table,
+                                              int table_n, double* partials) {
+  __shared__ double red[B / kWave];
+  __shared__ double lds[lds_words<M, F>()];
+  const F f = make_functor<M, F>(p, table, table_n, lds);
+  const double s = block_sum<B>(lane_sum<M>(p, f), red);
+  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
 template <DivMode M, class F>
 __global__ __launch_bounds__(B) void riemann_kernel(RiemannParams p, const double* table,
                                                     int table_n, double* partials) {
-  __shared__ double red[B / kWave];
-  __shared__ double lds[Maker<F>::kLds];
-  const F f = Maker<F>::make(p, table, table_n, lds);
-  const double s = block_sum<B>(lane_sum<M>(p, f), red);
-  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+  partials_body<M, F>(p, table, table_n, partials);
+}
+template <DivMode M, class F>
+__global__ __launch_bounds__(B) kFullOccupancy void riemann_kernel_o8(RiemannParams p,
+                                                                      const double* table,
+                                                                      int table_n,
+                                                                      double* partials) {
+  partials_body<M, F>(p, table, table_n, partials);
 }
 
 // ---------------------------------------------------------------------------- finalize
@@ -261,20 +310,32 @@ __global__ __launch_bounds__(kFinalBlock) void finalize_kernel(const double* par
 // One launch: partials, then the last-workgroup hand-off of handoff.hpp (sc1 publish,
 // two-level ticket, acquire, index-ordered sum) — bitwise identical to partials + finalize.
 template <DivMode M, class F>
-__global__ __launch_bounds__(B) void riemann_fused_kernel(RiemannParams p, const double* table,
-                                                          int table_n, double* partials,
-                                                          unsigned int* ticket, double scale,
-                                                          double* out) {
+__device__ __forceinline__ void fused_body(const RiemannParams& p, const double* table,
+                                           int table_n, double* partials, unsigned int* ticket,
+                                           double scale, double* out) {
   __shared__ double red[B / kWave];
-  __shared__ double lds[Maker<F>::kLds];
+  __shared__ double lds[lds_words<M, F>()];
   __shared__ int is_last;
-  const F f = Maker<F>::make(p, table, table_n, lds);
+  const F f = make_functor<M, F>(p, table, table_n, lds);
   const double s = block_sum<B>(lane_sum<M>(p, f), red);
   if (!publish_and_ticket(s, partials, ticket, blockIdx.x, gridDim.x, &is_last)) return;
   const double v = ordered_partials<B, true>(partials, static_cast<int>(gridDim.x));
   const double tot = block_sum<B>(v, red);
   if (threadIdx.x == 0) out[0] = tot * scale;
   rearm_ticket(ticket, gridDim.x);
+}
+template <DivMode M, class F>
+__global__ __launch_bounds__(B) void riemann_fused_kernel(RiemannParams p, const double* table,
+                                                          int table_n, double* partials,
+                                                          unsigned int* ticket, double scale,
+                                                          double* out) {
+  fused_body<M, F>(p, table, table_n, partials, ticket, scale, out);
+}
+template <DivMode M, class F>
+__global__ __launch_bounds__(B) kFullOccupancy void riemann_fused_kernel_o8(
+    RiemannParams p, const double* table, int table_n, double* partials, unsigned int* ticket,
+    double scale, double* out) {
+  fused_body<M, F>(p, table, table_n, partials, ticket, scale, out);
 }
 
 // ---------------------------------------------------------------------------- validation
@@ -284,8 +345,8 @@ template <DivMode M, class F>
 __global__ __launch_bounds__(B) void point_values_kernel(RiemannParams p, const double* table,
                                                          int table_n, double* out) {
   constexpr int T = F::template tile_len<M>();
-  __shared__ double lds[Maker<F>::kLds];
-  const F f = Maker<F>::make(p, table, table_n, lds);
+  __shared__ double lds[lds_words<M, F>()];
+  const F f = make_functor<M, F>(p, table, table_n, lds);
   const uint64_t t = static_cast<uint64_t>(blockIdx.x) * B + threadIdx.x;
   if (t * T >= p.n) return;
   const double x0 = fma(static_cast<double>(p.i_begin) + p.off + static_cast<double>(t * T),
@@ -316,14 +377,21 @@ __global__ __launch_bounds__(B) void point_values_kernel(RiemannParams p, const 
 template <DivMode M, class F>
 void launch_partials_t(const RiemannParams& p, LaunchShape shape, const double* table,
                        int table_n, double* partials, hipStream_t stream) {
-  riemann_kernel<M, F><<<shape.grid, B, 0, stream>>>(p, table, table_n, partials);
+  if constexpr (occupancy_hint<M, F>())
+    riemann_kernel_o8<M, F><<<shape.grid, B, 0, stream>>>(p, table, table_n, partials);
+  else
+    riemann_kernel<M, F><<<shape.grid, B, 0, stream>>>(p, table, table_n, partials);
 }
 template <DivMode M, class F>
 void launch_fused_t(const RiemannParams& p, LaunchShape shape, const double* table, int table_n,
                     double* partials, unsigned* ticket, double scale, double* out,
                     hipStream_t stream) {
-  riemann_fused_kernel<M, F>
-      <<<shape.grid, B, 0, stream>>>(p, table, table_n, partials, ticket, scale, out);
+  if constexpr (occupancy_hint<M, F>())
+    riemann_fused_kernel_o8<M, F>
+        <<<shape.grid, B, 0, stream>>>(p, table, table_n, partials, ticket, scale, out);
+  else
+    riemann_fused_kernel<M, F>
+        <<<shape.grid, B, 0, stream>>>(p, table, table_n, partials, ticket, scale, out);
 }
 
 // Dispatch (integrand, dtype, division mode) to a template instantiation. Transcendental
@@ -369,6 +437,9 @@ template <DivMode M, class F> struct PartialsOp {
 };
 template <DivMode M, class F> struct FusedOp {
   template <class... A> static void run(A... a) { launch_fused_t<M, F>(a...); }
+};
+template <DivMode M, class F> struct TileLenOp {
+  static void run(int* out) { *out = F::template tile_len<M>(); }
 };
 template <DivMode M, class F> struct PointsOp {
   static void run(const RiemannParams& p, const double* table, int table_n, double* out,
@@ -436,6 +507,13 @@ static RiemannParams prepared(const RiemannParams& p, DivMode eff) {
     }
   }
   return q;
+}
+
+int riemann_tile_len(const RiemannParams& p, DType dtype, DivMode div) {
+  int t = 0;
+  dispatch<TileLenOp>(p, dtype, dtype == DType::kF32 ? miint::effective_div(div, p.h)
+                                                     : effective_div(p, div), &t);
+  return t;
 }
 
 void launch_riemann_partials(const RiemannParams& p, DType dtype, DivMode div, LaunchShape shape,

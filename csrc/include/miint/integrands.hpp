@@ -463,10 +463,9 @@ struct TrainVel : TileDefaults<TrainVel>, AngleSeries {
 // The tile reads its segment once (v_m at the tile midpoint, slope D = d h), then every
 // sample is that line at its own offset from a sub-tile centre: one fma per sample plus its
 // accumulation (pairs at +-k share the centre and k), 2.2 VALU per sample with the tile
-// set-up. A lane whose tile straddles a knot evaluates that tile per sample in the
-// reference's form, with both segments' entries loaded once (exec divergence; at N = 1e9 one
-// wave in ~140 has such a lane, at 18e6 two in five). The table is read from global memory
-// (L2-resident), not staged in LDS.
+// set-up. A lane whose tile straddles a knot adds the kink of the next segment per sample
+// (exec divergence; at N = 1e9 one wave in ~140 has such a lane, at 18e6 two in five). The
+// table is read from global memory (L2-resident), not staged in LDS.
 struct Table : TileDefaults<Table> {
   const double* lds;  // the table: LDS copy (kIeee) or the global array (kSeries)
   int nseg;           // number of segments = entries - 1
@@ -478,6 +477,7 @@ struct Table : TileDefaults<Table> {
   double pk[kPairs];  // k_j = j + 1/2 (SGPR: VOP3 f64 ops take no literal on gfx9)
   double c16;         // sub-tile centre offset
   double hspan;       // (kSeriesTile - 1) / 2: tile midpoint to its end samples
+  double inv_h;       // 1 / h (knot offsets in steps)
 
   __device__ __forceinline__ static double opaque_s(double v) {
     asm volatile("" : "+s"(v));
@@ -530,20 +530,44 @@ struct Table : TileDefaults<Table> {
     vm = fma(d, xm - static_cast<double>(i), v0);
     D = d * h;
   }
-  // Sample of a tile that straddles exactly one knot: the reference's per-sample
-  // interpolation (point()) with both segments' entries already in registers.
-  struct Knot {
-    int lo;
-    double v0, v1, d0, d1;
+  // A tile that straddles exactly one knot (at x_k = lo + 1) is the line of segment lo with a
+  // kink: v(x_m + k h) = v_m + k D + max(k - k_knot, 0) dD, dD = (d_{lo+1} - d_lo) h, k_knot =
+  // (x_k - x_m) / h. Each sample costs 5 VALU instead of 2 (a per-sample segment select in
+  // the reference's form costs ~15 and was most of the time at 18e6 samples, where two waves
+  // in five carry such a tile). Entries lo..lo+2 are read once.
+  struct Kink {
+    double dD, kk;  // slope change per step, knot offset from the tile midpoint in steps
   };
-  __device__ __forceinline__ Knot knot(int lo) const {
+  __device__ __forceinline__ Kink kink(double xm, double h, int lo, double& vm, double& D) const {
     const double v0 = lds[lo], v1 = lds[lo + 1], v2 = lds[lo + 2];
-    return {lo, v0, v1, v1 - v0, v2 - v1};
+    const double d0 = v1 - v0;
+    vm = fma(d0, xm - static_cast<double>(lo), v0);
+    D = d0 * h;
+    return {((v2 - v1) - d0) * h, (static_cast<double>(lo + 1) - xm) * inv_h};
   }
-  __device__ __forceinline__ double knot_point(const Knot& k, double t) const {
-    const int i = segment(t);
-    const bool second = i != k.lo;
-    return fma(second ? k.d1 : k.d0, t - static_cast<double>(i), second ? k.v1 : k.v0);
+  // Sum of the tile's samples on the line (v_m, D), plus the kink when KINK.
+  template <bool KINK>
+  __device__ __forceinline__ double line_sum(double vm, double D, const Kink& kn) const {
+    double t = 0.0;
+#pragma unroll
+    for (int q = 0; q < kSubs; ++q) {
+      const double c0 = q == 0 ? -c16 : c16;
+      const double vc = fma(c0, D, vm);
+      const double r = c0 - kn.kk;  // sub-tile centre relative to the knot
+#pragma unroll
+      for (int j = 0; j < kPairs; ++j) {
+        double gp = fma(pk[j], D, vc);   // sample kSub/2 + j of the sub-tile
+        double gn = fma(-pk[j], D, vc);  // sample kSub/2 - 1 - j
+        if constexpr (KINK) {
+          gp = fma(fmax(r + pk[j], 0.0), kn.dD, gp);
+          gn = fma(fmax(r - pk[j], 0.0), kn.dD, gn);
+        }
+        t += gp;
+        t += gn;
+        asm volatile("" : "+v"(t));  // keep program order (see Pi4)
+      }
+    }
+    return t;
   }
   template <int U, DivMode M>
   __device__ __forceinline__ double tile_acc(double xm, double h, double acc) const {
@@ -551,39 +575,24 @@ struct Table : TileDefaults<Table> {
       static_assert(U == kSeriesTile, "segment tiles are kSubs sub-tiles of kSub samples");
       int lo, hi;
       ends(xm, h, lo, hi);
-      if (lo != hi) {  // rare: per sample, rolled (keeps the kernel's SGPRs <= 96)
-        const double x0 = fma(-hspan, h, xm);
-        double s0 = 0.0, s1 = 0.0;
-        if (hi == lo + 1) {  // one knot: no memory access per sample
-          const Knot k = knot(lo);
-#pragma unroll 2
-          for (int u = 0; u < U; u += 2) {
-            s0 += knot_point(k, fma(static_cast<double>(u), h, x0));
-            s1 += knot_point(k, fma(static_cast<double>(u + 1), h, x0));
-          }
-        } else {  // coarse step: a tile spans several segments
-#pragma unroll 1
-          for (int u = 0; u < U; u += 2) {
-            s0 += point(fma(static_cast<double>(u), h, x0));
-            s1 += point(fma(static_cast<double>(u + 1), h, x0));
-          }
-        }
-        return acc + (s0 + s1);
-      }
       double vm, D;
-      line(xm, h, lo, vm, D);
-      double t = 0.0;
-#pragma unroll
-      for (int q = 0; q < kSubs; ++q) {
-        const double vc = fma(q == 0 ? -c16 : c16, D, vm);
-#pragma unroll
-        for (int j = 0; j < kPairs; ++j) {
-          t += fma(pk[j], D, vc);   // sample kSub/2 + j of the sub-tile
-          t += fma(-pk[j], D, vc);  // sample kSub/2 - 1 - j
-          asm volatile("" : "+v"(t));  // keep program order (see Pi4)
-        }
+      if (lo == hi) {
+        line(xm, h, lo, vm, D);
+        return acc + line_sum<false>(vm, D, Kink{0.0, 0.0});
       }
-      return acc + t;
+      if (hi == lo + 1) {
+        const Kink kn = kink(xm, h, lo, vm, D);
+        return acc + line_sum<true>(vm, D, kn);
+      }
+      // coarse step (a tile spans several segments): per sample, rolled
+      const double x0 = fma(-hspan, h, xm);
+      double s0 = 0.0, s1 = 0.0;
+#pragma unroll 1
+      for (int u = 0; u < U; u += 2) {
+        s0 += point(fma(static_cast<double>(u), h, x0));
+        s1 += point(fma(static_cast<double>(u + 1), h, x0));
+      }
+      return acc + (s0 + s1);
     } else {
       return acc + tile<U, M>(xm, h);
     }
@@ -592,16 +601,19 @@ struct Table : TileDefaults<Table> {
   __device__ __forceinline__ double series_point(double xm, double h, int u) const {
     int lo, hi;
     ends(xm, h, lo, hi);
-    if (lo != hi) {
-      const double t = fma(static_cast<double>(u), h, fma(-hspan, h, xm));
-      return hi == lo + 1 ? knot_point(knot(lo), t) : point(t);
-    }
+    if (hi > lo + 1) return point(fma(static_cast<double>(u), h, fma(-hspan, h, xm)));
     double vm, D;
-    line(xm, h, lo, vm, D);
+    Kink kn{0.0, 0.0};
+    if (lo == hi) line(xm, h, lo, vm, D);
+    else kn = kink(xm, h, lo, vm, D);
     const int q = u / kSub, w = u % kSub;
-    const double vc = fma(q == 0 ? -c16 : c16, D, vm);
+    const double c0 = q == 0 ? -c16 : c16;
+    const double vc = fma(c0, D, vm);
+    const double r = c0 - kn.kk;
     const int j = w >= kSub / 2 ? w - kSub / 2 : kSub / 2 - 1 - w;
-    return w >= kSub / 2 ? fma(pk[j], D, vc) : fma(-pk[j], D, vc);
+    double g = w >= kSub / 2 ? fma(pk[j], D, vc) : fma(-pk[j], D, vc);
+    if (lo != hi) g = fma(fmax(w >= kSub / 2 ? r + pk[j] : r - pk[j], 0.0), kn.dD, g);
+    return g;
   }
 };
 

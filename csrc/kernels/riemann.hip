@@ -245,6 +245,7 @@ __device__ __forceinline__ F make_functor(const RiemannParams& p, const double* 
   if constexpr (__is_same(F, Table) && M == DivMode::kSeries) {
     Table f{{}, table, n - 1};
     f.init();
+    f.inv_h = 1.0 / p.h;
     return f;
   } else {
     return Maker<F>::make(p, table, n, lds);

@@ -258,18 +258,54 @@ struct Pi4 : TileDefaults<Pi4> {
   }
 };
 
+// ------------------------------------------------------------------ tile seed: sin and cos
+// sin and cos of a tile midpoint angle (|theta| up to ~1e5; the integrands use [0, 2 pi]):
+// n = rint(theta 2/pi), r = theta - n pi/2 by a two-part Cody-Waite reduction (pi/2 = hi + lo,
+// hi with 33 significant bits, so n hi is exact and both fma steps round only at ulp(r)),
+// then the fdlibm kernel polynomials on [-pi/4, pi/4] (sin: odd degree 13; cos: even degree
+// 14 with the 1 - z/2 split that keeps it within 1 ulp), and the quadrant's swap and signs.
+// ~40 VALU against ~110 for ocml sincos (general range reduction with a Payne-Hanek path),
+// which was ~0.9 VALU per sample of a 128-sample angle-addition tile.
+__device__ __forceinline__ void tile_sincos(double th, double& S, double& C) {
+  constexpr double kTwoOverPi = 6.36619772367581382433e-01;
+  constexpr double kPio2Hi = 1.57079632673412561417e+00;  // 0x1.921fb544p+0
+  constexpr double kPio2Lo = 6.07710050650619224932e-11;  // pi/2 - kPio2Hi
+  const double n = rint(th * kTwoOverPi);
+  const double r = fma(-n, kPio2Lo, fma(-n, kPio2Hi, th));
+  const int q = static_cast<int>(n);
+  const double z = r * r, w = z * z;
+  // sin r = r + r z (S1 + z (S2 + ... + z S6))
+  const double s26 = fma(z, fma(z, fma(z, fma(z, 1.58969099521155010221e-10,
+                                                -2.50507602534068634195e-08),
+                                           2.75573137070700676789e-06),
+                                      -1.98412698298579493134e-04),
+                         8.33333333332248946124e-03);
+  const double sr = fma(r * z, fma(z, s26, -1.66666666666666324348e-01), r);
+  // cos r = (1 - z/2) + (((1 - (1 - z/2)) - z/2) + z (z (C1 + z C2 + z^2 C3) + z^4 (C4 + ...)))
+  const double c13 = fma(z, fma(z, 2.48015872894767294178e-05, -1.38888888888741095749e-03),
+                         4.16666666666666019037e-02);
+  const double c46 = fma(z, fma(z, -1.13596475577881948265e-11, 2.08757232129817482790e-09),
+                         -2.75573143513906633035e-07);
+  const double rc = fma(w * w, c46, z * c13);
+  const double hz = 0.5 * z, cw = 1.0 - hz;
+  const double cc = cw + (((1.0 - cw) - hz) + z * rc);
+  const bool swap = (q & 1) != 0;
+  const double a = swap ? cc : sr, b = swap ? sr : cc;
+  S = (q & 2) ? -a : a;
+  C = ((q + 1) & 2) ? -b : b;
+}
+
 // ------------------------------------------------------------------ sin / cos by angle addition
 // Shared series path of Sin and TrainVel (both evaluate sin or cos of theta = w x):
-// one ocml sincos per 128-sample tile at the midpoint theta_m, re-centred to eight 16-sample
-// sub-tiles (centres theta_m + c0 delta, c0 = +-8, +-24, +-40, +-56; delta = w h), then every
-// sample by the exact angle-addition formula
+// one sin/cos pair per 128-sample tile at the midpoint theta_m (tile_sincos), re-centred to
+// eight 16-sample sub-tiles (centres theta_m + c0 delta, c0 = +-8, +-24, +-40, +-56;
+// delta = w h), then every sample by the exact angle-addition formula
 //   sin(theta_c +- k delta) = S_c cos(k delta) +- C_c sin(k delta)
 //   cos(theta_c +- k delta) = C_c cos(k delta) -+ S_c sin(k delta)
 // with cos/sin(k delta) for the 8 pair offsets k = j + 1/2 and for the centres computed once
 // per launch on the host in long double (RiemannParams::trig, kernel arguments -> SGPRs).
 // Per pair: 1 mul + 2 fma for the two samples + 2 accumulations (2.5 VALU per sample); the
-// sincos (~70 VALU) and the 4-op re-centring per sub-tile add ~0.8 per sample (64-sample
-// tiles: 1.3). Every centre comes straight from the tile midpoint (one rounding), so the
+// seed and the 4-op re-centring per sub-tile add the rest. Every centre comes straight from the tile midpoint (one rounding), so the
 // per-point error does not grow with the tile. No truncation (valid for any h).
 struct AngleSeries {
   static constexpr int kPairs = 8;
@@ -304,7 +340,7 @@ struct AngleSeries {
   template <bool COS>
   __device__ __forceinline__ double tile_sum(double theta_m) const {
     double S, C;
-    sincos(theta_m, &S, &C);
+    tile_sincos(theta_m, S, C);
     double t = 0.0;
 #pragma unroll
     for (int q = 0; q < kSubs; ++q) {
@@ -325,7 +361,7 @@ struct AngleSeries {
   template <bool COS>
   __device__ __forceinline__ double point_of(double theta_m, int u) const {
     double S, C, Sq, Cq;
-    sincos(theta_m, &S, &C);
+    tile_sincos(theta_m, S, C);
     const int q = u / kSub, w = u % kSub;
     centre(S, C, q, Sq, Cq);
     const double base = COS ? Cq : Sq, side = COS ? -Sq : Cq;

@@ -256,16 +256,17 @@ __device__ __forceinline__ F make_functor(const RiemannParams& p, const double* 
 // 8 waves per SIMD in ONE resident round. A kernel that fits fewer (more than 64 VGPRs or
 // ~96 SGPRs per wave) leaves 1/8 or more of the workgroups for a second, nearly empty round,
 // and the scheduler does not trade registers for occupancy by itself: the table's segment
-// tiles took 98 VGPRs (4 waves/SIMD), the sin/train series 105 SGPRs (7 waves/SIMD). Those
-// instantiations get amdgpu_waves_per_eu(8). The ones that already fit 8 keep the unhinted
-// kernel: the hint also changes their allocation (Pi4 series: 8 more VALU per tile, its
-// k^2 constants moved from SGPRs to VGPR copies).
+// tiles took 98 VGPRs (4 waves/SIMD), the train series 90 SGPRs + 66 VGPRs (7 waves/SIMD).
+// Those instantiations get amdgpu_waves_per_eu(8). The ones that already fit 8 keep the
+// unhinted kernel: the hint also changes their allocation (Pi4 series: 8 more VALU per tile,
+// its k^2 constants moved from SGPRs to VGPR copies; sin series: 12 bytes of scratch).
 #define kFullOccupancy __attribute__((amdgpu_waves_per_eu(8, 8)))
 template <DivMode M, class F>
 constexpr bool occupancy_hint() {
   if constexpr (__is_same(F, Pi4)) return M == DivMode::kSeriesDirect;
   else if constexpr (__is_same(F, Pi4F32)) return M == DivMode::kIeee;
-  else return __is_same(F, Sin) || __is_same(F, TrainVel) || __is_same(F, Table);
+  else if constexpr (__is_same(F, Sin)) return M == DivMode::kIeee;
+  else return __is_same(F, TrainVel) || __is_same(F, Table);
 }
 
 // Partials kernel: one fp64 partial per workgroup.

@@ -5,12 +5,17 @@ Metric and config come from BASELINE.json ("Riemann subintervals/sec at N=1e9 fp
 vs analytic pi"). One step = one complete integration of N samples per GPU: gfx950 kernel
 (every sample evaluated, fp64) -> in-kernel DPP/LDS/ticket reduction -> RCCL all-reduce of
 the per-GPU partial over xGMI -> D2H into pinned memory. Steps are hipGraph replays of
-batches of 16; with >1 GPU each batch ends in ONE all-reduce of its 16 step results
-(bucketed: every step still gets its own global sum; --no-bucket = one 8-byte all-reduce
-per step, overlapped on a side stream).
+batches of --slots (48) steps; with >1 GPU each batch ends in ONE all-reduce of its 48 step
+results (bucketed: every step still gets its own global sum; --no-bucket = one 8-byte
+all-reduce per step, overlapped on a side stream).
+
+Warmup: the W warmup steps, then at least --settle-ms (60) more untimed steps so the timed
+region starts at steady clocks (from idle the GPU ramps from ~90 to 76.8 us per step over
+~25 ms; the JSON line reports the settle steps run as "warmup_settle_steps").
 
 Weak scaling: every GPU integrates its own 1e9-sample slice of a global N = 1e9 x n_gpus
-(N = 8e9 on 8 GPUs). The result of every timed step is checked on the host against pi.
+(N = 8e9 on 8 GPUs). The results of the last batch of timed steps (every rank holds the
+global sums) are checked on the host against pi.
 
     python bench.py                          # 1 GPU
     torchrun --nproc-per-node 8 bench.py --gpus 8
@@ -34,6 +39,9 @@ def parse() -> argparse.Namespace:
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=400)
     p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--settle-ms", type=float, default=60.0,
+                   help="after the W warmup steps, keep stepping (untimed) for at least this "
+                        "long so the timed steps run at steady clocks (0 = off)")
     # (--n is a prefix of torchrun's own --nnodes/--nproc-per-node: use --samples under torchrun)
     p.add_argument("--samples", "--n", dest="n", type=float, default=1e9,
                    help="samples per GPU (weak) or total (strong)")
@@ -51,6 +59,8 @@ def parse() -> argparse.Namespace:
     p.add_argument("--no-pipeline", action="store_true")
     p.add_argument("--unfused", action="store_true", help="partials + finalize (2 launches)")
     p.add_argument("--grid", type=int, default=0)
+    p.add_argument("--slots", type=int, default=48,
+                   help="steps per captured graph batch (= steps per bucketed all-reduce)")
     p.add_argument("--no-bucket", action="store_true",
                    help="one all-reduce per step instead of one per graph batch of steps")
     p.add_argument("--force-collective", action="store_true",
@@ -84,7 +94,7 @@ def main() -> int:
     use_torch = args.comm == "torch" and world > 1
     integ = Integrator(args.integrand, n=n_total, rule=args.rule, dtype=args.dtype, div=args.div,
                        backend="hip", ctx=ctx, comm=args.comm, fused=not args.unfused,
-                       grid=args.grid, force_collective=args.force_collective,
+                       grid=args.grid, slots=args.slots, force_collective=args.force_collective,
                        bucket=not args.no_bucket)
     plan = integ.plan
     graphs = not args.no_graph and not use_torch
@@ -108,6 +118,23 @@ def main() -> int:
         print(f"bench.py: hipGraph capture failed ({plan.graph_error}); "
               "running with direct stream enqueue", file=sys.stderr)
         graphs = False
+    # ---- clock settle: from idle the MI355X needs ~25 ms of continuous work before its
+    # per-step time is steady (90 -> 76.8 us per step; profiles/r1/clock_ramp.jsonl). The W
+    # warmup steps alone (20 x 85 us) end inside that ramp, so the warmup also runs at least
+    # --settle-ms of back-to-back steps. The step count comes from one calibration batch,
+    # agreed across ranks (MAX) so every rank runs the same collectives.
+    settle_steps = 0
+    if args.settle_ms > 0:
+        t_c = time.perf_counter()
+        launch(plan.slots)
+        finish()
+        per_step = (time.perf_counter() - t_c) / plan.slots
+        want = torch.tensor([math.ceil(args.settle_ms * 1e-3 / max(per_step, 1e-7))],
+                            dtype=torch.float64, device="cuda" if ctx.backend == "nccl" else "cpu")
+        ctx.all_reduce_max(want)
+        settle_steps = plan.slots + int(want.item())
+        launch(settle_steps - plan.slots)
+        finish()
 
     # ---- timed region: barrier + device sync on both sides, K steps in between
     ctx.barrier()
@@ -145,6 +172,7 @@ def main() -> int:
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "warmup_settle_steps": settle_steps,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
             "scaling": args.scaling,

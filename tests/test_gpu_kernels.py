@@ -95,6 +95,23 @@ def test_sin_series_per_point_accuracy(cuda, n):
         assert float((v - w).abs().max()) <= 8.9e-16
 
 
+def test_sin_series_seed_all_quadrants(cuda):
+    """The series seed (tile_sincos: rint(2 theta/pi), two-part Cody-Waite, fdlibm kernels,
+    quadrant swap/sign) on [-40, 40]: negative angles and every quadrant. Per point against
+    ocml sin within 4 ulp(1) plus ulp(40) = 7.1e-15, the coordinate rounding both paths carry
+    at |x| ~ 40 (a wrong quadrant or coefficient would be off by 1e-14 or far more); the sum
+    against cos(-40) - cos(40) = 0."""
+    spec = integrands.IntegrandSpec("sin", -40.0, 40.0)
+    n = 10**8
+    for i0 in (0, n // 4 + 5, n // 2 - 3_000, 3 * n // 4, n - (1 << 16)):
+        v = kernels.point_values(spec, n, rule="mid", div="series", i_begin=i0, n_local=1 << 16)
+        w = kernels.point_values(spec, n, rule="mid", div="ieee", i_begin=i0, n_local=1 << 16)
+        assert float((v - w).abs().max()) <= 8.9e-16 + 7.2e-15
+    a = float(kernels.riemann(spec, n, rule="mid", div="series").item())
+    b = float(kernels.riemann(spec, n, rule="mid", div="ieee").item())
+    assert abs(a - b) < 1e-13 and abs(a) < 1e-12
+
+
 @pytest.mark.parametrize("n", [10**6, 10**8, 10**9])
 def test_sin_series_sum_matches_direct(cuda, n):
     spec = integrands.sin()
@@ -120,12 +137,12 @@ def test_train_series_matches_direct(cuda):
     assert a == pytest.approx(spec.analytic(), rel=1e-12)
 
 
-@pytest.mark.parametrize("n", [10**9, 18_000_000, 1_000_003])
+@pytest.mark.parametrize("n", [10**9, 18_000_000, 1_000_003, 100_003])
 def test_table_segment_tiles_match_per_sample(cuda, n):
     """Velocity-table integrand: the segment-line tiles (one segment read per 64 samples,
     v = v_c +- k D per sample) against the reference-form per-sample interpolation at the
-    same index. 18e6 (the reference's 1e4 samples/s) and 1e6 put a knot inside many tiles,
-    so both the line path and the per-sample fallback of straddling tiles are checked.
+    same index. 18e6 (the reference's 1e4 samples/s) and 1e6 put a knot inside many tiles
+    (the kinked-line path), 1e5 makes tiles span several segments (per-sample fallback).
     Per point within 4 ulp of the value scale (v <= 87.15 m/s); sums to 1e-14."""
     spec = integrands.table()
     for i0 in (0, n // 3 + 17, n - (1 << 16)):

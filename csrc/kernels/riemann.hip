@@ -150,14 +150,25 @@ struct Pi4F32 : TileDefaults<Pi4F32> {
       const float a = (-2.0f * hf) * xm * s;
       const float b = -(hf * hf) * s;
       const f32x2 bb = {b, b};
+      const f32x2 aa = {a, a};
+      const f32x2 emv = {em, em};
+      // Sub-tile centre residuals and slopes, two sub-tiles per packed op:
+      // (e_c, e_c') = c0 (c0 B + A) + e_m and (A', A'') = 2 c0 B + A for c0 = (-48, -16), (16, 48).
+      f32x2 ecs[kSubs / 2], aqs[kSubs / 2];
+#pragma unroll
+      for (int p2 = 0; p2 < kSubs / 2; ++p2) {
+        const f32x2 c0v = {(2 * p2 - 0.5f * (kSubs - 1)) * kSubLen,
+                           (2 * p2 + 1 - 0.5f * (kSubs - 1)) * kSubLen};
+        ecs[p2] = pk_fma(c0v, pk_fma(c0v, bb, aa), emv);
+        aqs[p2] = pk_fma(c0v + c0v, bb, aa);
+      }
       f32x2 t;
 #pragma unroll
       for (int q = 0; q < kSubs; ++q) {
-        const float c0 = (q - 0.5f * (kSubs - 1)) * kSubLen;
-        const float ec = fmaf(c0, fmaf(c0, b, a), em);
-        const float aq = fmaf(2.0f * c0, b, a);
+        const float ec = (q & 1) ? ecs[q / 2].y : ecs[q / 2].x;
+        const float aq = (q & 1) ? aqs[q / 2].y : aqs[q / 2].x;
         const f32x2 av = {aq, aq};
-        f32x2 cc = {fmaf(0.25f, b, ec), fmaf(2.25f, b, ec)};  // (c_0, c_1)
+        f32x2 cc = pk_fma(f32x2{0.25f, 2.25f}, bb, f32x2{ec, ec});  // (c_0, c_1)
 #pragma unroll
         for (int j = 0; j < kSubLen / 2; j += 2) {
           const f32x2 k0 = {j + 0.5f, -(j + 0.5f)};

@@ -21,13 +21,19 @@ constexpr int kRiemannTile = 32;     // default samples per lane tile (Pi4 serie
 constexpr int kRiemannBlock = 256;
 constexpr int kSeriesHalfSpan = 64;  // max |sample offset| from a Pi4 series seed, in steps
 
+constexpr int kDirectHalfSpan = 16;  // the same for kSeriesDirect's 32-sample tiles
+
 // True when the fp64 Pi4 series reciprocal is exact to fp64 for this h (see integrands.hpp).
 inline bool series_ok(double h) { return kSeriesHalfSpan * (h < 0 ? -h : h) <= 2e-6; }
+inline bool direct_ok(double h) { return kDirectHalfSpan * (h < 0 ? -h : h) <= 2e-6; }
 
-// Division mode actually used for step h: the series paths fall back to IEEE division when
-// the tile span is too coarse for the truncated series to be exact to fp64.
+// Division mode actually used for step h: a step too coarse for the 128-sample series tiles
+// (N < 3.2e7 on [0, 1]) still fits the 32-sample kSeriesDirect tiles down to N = 8e6 (5 VALU
+// per sample against ~14 for IEEE division); coarser steps use IEEE division.
 inline DivMode effective_div(DivMode d, double h) {
-  return (d != DivMode::kIeee && !series_ok(h)) ? DivMode::kIeee : d;
+  if (d == DivMode::kIeee) return d;
+  if (d == DivMode::kSeries && series_ok(h)) return d;
+  return direct_ok(h) ? DivMode::kSeriesDirect : DivMode::kIeee;
 }
 // Per integrand: the sin / train-velocity series path (angle addition from a per-tile sincos
 // seed) and the table's segment-line tiles are exact for any h, so only the series/ieee
@@ -37,6 +43,13 @@ inline DivMode effective_div(DivMode d, double h, Integrand f) {
     return d == DivMode::kSeries ? DivMode::kSeries : DivMode::kIeee;
   if (f != Integrand::kPi4) return DivMode::kIeee;
   return effective_div(d, h);
+}
+
+// With the dtype: the fp32 path has one series form (128-sample tiles, first order) and
+// otherwise IEEE division.
+inline DivMode effective_div(DivMode d, double h, Integrand f, DType t) {
+  if (t == DType::kF32) return (d == DivMode::kIeee || !series_ok(h)) ? DivMode::kIeee : DivMode::kSeries;
+  return effective_div(d, h, f);
 }
 
 struct LaunchShape {

@@ -495,8 +495,8 @@ static void check_params(const RiemannParams& p, const double* table, int table_
   MIINT_CHECK(p.i_begin + p.n < (uint64_t(1) << 52), "sample index must stay below 2^52");
 }
 
-static DivMode effective_div(const RiemannParams& p, DivMode div) {
-  return miint::effective_div(div, p.h, static_cast<Integrand>(p.integrand));
+static DivMode effective_div(const RiemannParams& p, DivMode div, DType dtype) {
+  return miint::effective_div(div, p.h, static_cast<Integrand>(p.integrand), dtype);
 }
 
 // Host-side constants of the angle-addition series (long double; AngleSeries in
@@ -524,8 +524,7 @@ static RiemannParams prepared(const RiemannParams& p, DivMode eff) {
 
 int riemann_tile_len(const RiemannParams& p, DType dtype, DivMode div) {
   int t = 0;
-  dispatch<TileLenOp>(p, dtype, dtype == DType::kF32 ? miint::effective_div(div, p.h)
-                                                     : effective_div(p, div), &t);
+  dispatch<TileLenOp>(p, dtype, effective_div(p, div, dtype), &t);
   return t;
 }
 
@@ -534,7 +533,7 @@ void launch_riemann_partials(const RiemannParams& p, DType dtype, DivMode div, L
                              hipStream_t stream) {
   check_shape(shape);
   check_params(p, table, table_n);
-  const DivMode eff = effective_div(p, div);
+  const DivMode eff = effective_div(p, div, dtype);
   dispatch<PartialsOp>(p, dtype, eff, prepared(p, eff), shape, table, table_n, partials, stream);
   MIINT_HIP(hipGetLastError());
 }
@@ -551,7 +550,7 @@ void launch_riemann_fused(const RiemannParams& p, DType dtype, DivMode div, Laun
                           unsigned int* ticket, double scale, double* out, hipStream_t stream) {
   check_shape(shape);
   check_params(p, table, table_n);
-  const DivMode eff = effective_div(p, div);
+  const DivMode eff = effective_div(p, div, dtype);
   dispatch<FusedOp>(p, dtype, eff, prepared(p, eff), shape, table, table_n, partials, ticket,
                     scale, out, stream);
   MIINT_HIP(hipGetLastError());
@@ -561,7 +560,7 @@ void launch_riemann_point_values(const RiemannParams& p, DivMode div, const doub
                                  int table_n, double* out, hipStream_t stream) {
   check_params(p, table, table_n);
   MIINT_CHECK(p.n >= 1, "empty range");
-  const DivMode eff = effective_div(p, div);
+  const DivMode eff = effective_div(p, div, DType::kF64);
   dispatch<PointsOp>(p, DType::kF64, eff, prepared(p, eff), table, table_n, out, stream);
   MIINT_HIP(hipGetLastError());
 }

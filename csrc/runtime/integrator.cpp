@@ -79,8 +79,7 @@ RiemannPlan::~RiemannPlan() {
 }
 
 DivMode RiemannPlan::effective_div() const {
-  return cfg_.dtype == DType::kF32 ? miint::effective_div(cfg_.div, params_.h)
-                                   : miint::effective_div(cfg_.div, params_.h, cfg_.integrand);
+  return miint::effective_div(cfg_.div, params_.h, cfg_.integrand, cfg_.dtype);
 }
 
 size_t RiemannPlan::graph_nodes() const { return batch_ ? batch_->num_nodes() : 0; }

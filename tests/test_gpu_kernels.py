@@ -165,6 +165,25 @@ def test_pi4_1e9_mid_error(cuda):
     assert abs(v - math.pi) < 2e-15  # measured 4.4e-16 (2 ulp of pi)
 
 
+@pytest.mark.parametrize("n", [10**7, 8_000_000])
+def test_pi4_mid_steps_use_direct_series(native, cuda, n):
+    """8e6 <= N < 3.2e7 on [0, 1]: too coarse for the 128-sample series tiles, fine for the
+    32-sample kSeriesDirect tiles (16 h <= 2e-6). The plan reports it, every sample stays
+    within 5 ulp of IEEE division and the sum agrees to 1e-15."""
+    from cuda_v_mpi_amd import Integrator
+    assert "series_direct" in str(Integrator("pi4", n=n, div="series").plan.effective_div)
+    assert "ieee" in str(Integrator("pi4", n=7_000_000, div="series").plan.effective_div)
+    spec = integrands.pi4()
+    for i0 in (0, n // 2 + 7, n - (1 << 16)):
+        v = kernels.point_values(spec, n, rule="left", div="series", i_begin=i0, n_local=1 << 16)
+        w = kernels.point_values(spec, n, rule="left", div="ieee", i_begin=i0, n_local=1 << 16)
+        spacing = torch.nextafter(w.abs(), torch.full_like(w, math.inf)) - w.abs()
+        assert float(((v - w) / spacing).abs().max()) <= 5.0
+    a = float(kernels.riemann(spec, n, div="series").item())
+    b = float(kernels.riemann(spec, n, div="ieee").item())
+    assert a == pytest.approx(b, rel=1e-15, abs=0)
+
+
 @pytest.mark.parametrize("n", [33_000_000, 10**8, 10**9])
 def test_series_equals_ieee_sum(cuda, n):
     """The whole sum: series vs correctly rounded division agree to fp64 resolution, i.e.

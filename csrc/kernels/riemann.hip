@@ -122,9 +122,9 @@ struct Pi4F32 : TileDefaults<Pi4F32> {
   // Default series path, midpoint-anchored, 128-sample tiles of four 32-sample sub-tiles
   // (centres at -48, -16, 16, 48 steps; e_c = e_m + c0 A + c0^2 B, A' = A + 2 c0 B: one seed
   // per 128 samples; 64-sample tiles of two sub-tiles spent ~29 VALU of seed, coordinate and
-  // fp64 fold per 80 of pair work). The pair residuals (e_{+k}, e_{-k}) = c_k + (k, -k) * A' are one
-  // v_pk_fma_f32 (op_sel broadcasts c_k), summed by one v_pk_add_f32, and the shared c_k of
-  // TWO consecutive pairs advance together by one v_pk_fma_f32 with the exact steps
+  // fp64 fold per 80 of pair work). The pair residuals (e_{+k}, e_{-k}) = c_k + (k, -k) * A'
+  // are one v_pk_fma_f32 (op_sel broadcasts c_k), summed by one v_pk_add_f32, and the shared
+  // c_k of TWO consecutive pairs advance together by one v_pk_fma_f32 with the exact steps
   // (k_{j+2}^2 - k_j^2, k_{j+3}^2 - k_{j+1}^2) = (4j+6, 4j+10) times B: 1.25 VALU per sample.
   // In fp32 the e^2 term (< 3e-16) is far below the format's 6e-8 and is not carried.
   static constexpr int kSubLen = 32;
@@ -183,7 +183,7 @@ struct Pi4F32 : TileDefaults<Pi4F32> {
       // tile value in fp32 (the path's precision); lanes accumulate tiles in fp64
       return acc + static_cast<double>(s * (static_cast<float>(UU) + (t.x + t.y)));
     } else {
-      return acc + tile<UU, M>(xmd - 0.0, h);
+      return acc + tile<UU, M>(xmd, h);
     }
   }
 };
@@ -242,9 +242,8 @@ template <> struct Maker<Table> {
 };
 
 // Functor construction and LDS size per (division mode, integrand). The table's segment-line
-// tiles read two entries per 64 samples, so they read the (L2-resident, 14.4 KB) table from
-// global memory instead of staging it: at the reference's 18e6 samples the per-workgroup
-// staging (7 dependent load/store rounds, 2048 workgroups) was most of the kernel's 15.5 us.
+// tiles read two or three entries per 64 samples, so they read the (L2-resident, 14.4 KB)
+// table from global memory instead of staging all of it in every workgroup's LDS.
 template <DivMode M, class F>
 constexpr int lds_words() {
   if constexpr (__is_same(F, Table) && M == DivMode::kSeries) return 1;

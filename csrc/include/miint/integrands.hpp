@@ -305,8 +305,9 @@ __device__ __forceinline__ void tile_sincos(double th, double& S, double& C) {
 // with cos/sin(k delta) for the 8 pair offsets k = j + 1/2 and for the centres computed once
 // per launch on the host in long double (RiemannParams::trig, kernel arguments -> SGPRs).
 // Per pair: 1 mul + 2 fma for the two samples + 2 accumulations (2.5 VALU per sample); the
-// seed and the 4-op re-centring per sub-tile add the rest. Every centre comes straight from the tile midpoint (one rounding), so the
-// per-point error does not grow with the tile. No truncation (valid for any h).
+// seed and the 4-op re-centring per sub-tile add the rest (388 VALU per 128-sample tile).
+// Every centre comes straight from the tile midpoint (one rounding), so the per-point error
+// does not grow with the tile. No truncation (valid for any h).
 struct AngleSeries {
   static constexpr int kPairs = 8;
   static constexpr int kSub = 2 * kPairs;

@@ -48,7 +48,8 @@ inline DivMode effective_div(DivMode d, double h, Integrand f) {
 // With the dtype: the fp32 path has one series form (128-sample tiles, first order) and
 // otherwise IEEE division.
 inline DivMode effective_div(DivMode d, double h, Integrand f, DType t) {
-  if (t == DType::kF32) return (d == DivMode::kIeee || !series_ok(h)) ? DivMode::kIeee : DivMode::kSeries;
+  if (t == DType::kF32)
+    return (d == DivMode::kIeee || !series_ok(h)) ? DivMode::kIeee : DivMode::kSeries;
   return effective_div(d, h, f);
 }
 

@@ -83,6 +83,9 @@ struct RiemannParams {
   int integrand;        // Integrand
   int ncoef;            // polynomial: number of coefficients
   double coef[kMaxPolyCoeffs];  // polynomial coefficients c_0..c_{ncoef-1}
+  // Polynomial series path, filled on the host by the launchers (long double): c_i h^i
+  // (integrands.hpp, Poly::tile_acc)
+  double coef_h[kMaxPolyCoeffs];
   double p0, p1;        // integrand parameters (train: ts, vs)
   // Sin series path, filled on the host by the launchers (long double): trig[j] = cos(k_j h),
   // trig[8 + j] = sin(k_j h) for k_j = j + 1/2 (j < 8), then cos(c0 h), sin(c0 h) for the

@@ -45,11 +45,18 @@ inline DivMode effective_div(DivMode d, double h, Integrand f) {
   return effective_div(d, h);
 }
 
-// With the dtype: the fp32 path has one series form (128-sample tiles, first order) and
-// otherwise IEEE division.
-inline DivMode effective_div(DivMode d, double h, Integrand f, DType t) {
+constexpr int kPolySeriesMaxCoeffs = 8;  // polynomials up to degree 7 have a series path
+
+// With the dtype (the fp32 path has one series form, 128-sample tiles of first order, and
+// otherwise IEEE division) and the polynomial's coefficient count (Taylor-pair tiles for up
+// to kPolySeriesMaxCoeffs coefficients, exact for any h; Horner per sample otherwise).
+inline DivMode effective_div(DivMode d, double h, Integrand f, DType t, int ncoef = 0) {
   if (t == DType::kF32)
     return (d == DivMode::kIeee || !series_ok(h)) ? DivMode::kIeee : DivMode::kSeries;
+  if (f == Integrand::kPoly)
+    return (d == DivMode::kSeries && ncoef >= 1 && ncoef <= kPolySeriesMaxCoeffs)
+               ? DivMode::kSeries
+               : DivMode::kIeee;
   return effective_div(d, h, f);
 }
 

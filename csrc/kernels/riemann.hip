@@ -249,10 +249,17 @@ constexpr int lds_words() {
   if constexpr (__is_same(F, Table) && M == DivMode::kSeries) return 1;
   else return Maker<F>::kLds;
 }
+template <class F> struct IsPoly { static constexpr bool value = false; };
+template <int NC> struct IsPoly<Poly<NC>> { static constexpr bool value = true; };
+
 template <DivMode M, class F>
 __device__ __forceinline__ F make_functor(const RiemannParams& p, const double* table, int n,
                                           double* lds) {
-  if constexpr (__is_same(F, Table) && M == DivMode::kSeries) {
+  if constexpr (IsPoly<F>::value && M == DivMode::kSeries) {
+    F f = Maker<F>::make(p, table, n, lds);
+    f.init_series(p.coef_h, p.ncoef, p.h);
+    return f;
+  } else if constexpr (__is_same(F, Table) && M == DivMode::kSeries) {
     Table f{{}, table, n - 1};
     f.init();
     f.inv_h = 1.0 / p.h;
@@ -276,6 +283,7 @@ constexpr bool occupancy_hint() {
   if constexpr (__is_same(F, Pi4)) return M == DivMode::kSeriesDirect;
   else if constexpr (__is_same(F, Pi4F32)) return M == DivMode::kIeee;
   else if constexpr (__is_same(F, Sin)) return M == DivMode::kIeee;
+  else if constexpr (IsPoly<F>::value) return M == DivMode::kSeries;
   else return __is_same(F, TrainVel) || __is_same(F, Table);
 }
 
@@ -371,6 +379,8 @@ __global__ __launch_bounds__(B) void point_values_kernel(RiemannParams p, const 
     if constexpr (M == DivMode::kSeries && __is_same(F, Pi4)) {
       // exactly the operations Pi4::tile_acc applies to sample u
       v = full ? f.series_point(xm, p.h, u) : f.point(x);
+    } else if constexpr (M == DivMode::kSeries && IsPoly<F>::value) {
+      v = full ? f.series_point(xm, u) : f.point(x);
     } else if constexpr (M == DivMode::kSeries && __is_same(F, Table)) {
       v = full ? f.series_point(xm, p.h, u) : f.point(x);
     } else if constexpr (M == DivMode::kSeries && (__is_same(F, Sin) || __is_same(F, TrainVel))) {
@@ -428,7 +438,9 @@ void dispatch(const RiemannParams& p, DType dtype, DivMode m, A&&... a) {
       else Op<DivMode::kIeee, Sin>::run(a...);
       return;
     case Integrand::kPoly:  // coefficient bucket: 4, 8 or 16 (zero-padded)
-      if (p.ncoef <= 4) Op<DivMode::kIeee, Poly<4>>::run(a...);
+      if (m == DivMode::kSeries && p.ncoef <= 4) Op<DivMode::kSeries, Poly<4>>::run(a...);
+      else if (m == DivMode::kSeries && p.ncoef <= 8) Op<DivMode::kSeries, Poly<8>>::run(a...);
+      else if (p.ncoef <= 4) Op<DivMode::kIeee, Poly<4>>::run(a...);
       else if (p.ncoef <= 8) Op<DivMode::kIeee, Poly<8>>::run(a...);
       else Op<DivMode::kIeee, Poly<16>>::run(a...);
       return;
@@ -495,7 +507,7 @@ static void check_params(const RiemannParams& p, const double* table, int table_
 }
 
 static DivMode effective_div(const RiemannParams& p, DivMode div, DType dtype) {
-  return miint::effective_div(div, p.h, static_cast<Integrand>(p.integrand), dtype);
+  return miint::effective_div(div, p.h, static_cast<Integrand>(p.integrand), dtype, p.ncoef);
 }
 
 // Host-side constants of the angle-addition series (long double; AngleSeries in
@@ -503,6 +515,14 @@ static DivMode effective_div(const RiemannParams& p, DivMode div, DType dtype) {
 static RiemannParams prepared(const RiemannParams& p, DivMode eff) {
   RiemannParams q = p;
   const Integrand f = static_cast<Integrand>(p.integrand);
+  if (f == Integrand::kPoly && eff == DivMode::kSeries) {  // c_i h^i for the Taylor shift
+    long double hp = 1.0L;
+    for (int i = 0; i < kMaxPolyCoeffs; ++i) {
+      q.coef_h[i] = i < p.ncoef ? static_cast<double>(static_cast<long double>(p.coef[i]) * hp)
+                                : 0.0;
+      hp *= static_cast<long double>(p.h);
+    }
+  }
   if ((f == Integrand::kSin || f == Integrand::kTrainVel) && eff == DivMode::kSeries) {
     const long double delta =
         f == Integrand::kSin ? static_cast<long double>(p.h)

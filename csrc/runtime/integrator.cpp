@@ -79,7 +79,7 @@ RiemannPlan::~RiemannPlan() {
 }
 
 DivMode RiemannPlan::effective_div() const {
-  return miint::effective_div(cfg_.div, params_.h, cfg_.integrand, cfg_.dtype);
+  return miint::effective_div(cfg_.div, params_.h, cfg_.integrand, cfg_.dtype, params_.ncoef);
 }
 
 size_t RiemannPlan::graph_nodes() const { return batch_ ? batch_->num_nodes() : 0; }

@@ -137,6 +137,25 @@ def test_train_series_matches_direct(cuda):
     assert a == pytest.approx(spec.analytic(), rel=1e-12)
 
 
+@pytest.mark.parametrize("degree", [3, 6, 7])
+@pytest.mark.parametrize("n", [10**9, 1_000_003])
+def test_poly_taylor_pairs_match_horner(cuda, degree, n):
+    """Random-coefficient polynomials: the Taylor-pair tiles (shift to each 32-sample
+    sub-tile centre, p(x_c +- k h) = E(k^2) +- k O(k^2)) against per-sample Horner at the same
+    index, per point within 16 ulp of sum |c_i| (the size of Horner's own rounding on [0, 1],
+    where the terms can cancel), and the sums to 1e-13."""
+    spec = integrands.poly(degree=degree, seed=degree)
+    scale = sum(abs(c) for c in spec.coef)
+    for i0 in (0, n // 3 + 17, n - (1 << 16)):
+        v = kernels.point_values(spec, n, rule="mid", div="series", i_begin=i0, n_local=1 << 16)
+        w = kernels.point_values(spec, n, rule="mid", div="ieee", i_begin=i0, n_local=1 << 16)
+        assert float((v - w).abs().max()) <= 16 * 2.0 ** -52 * scale
+    a = float(kernels.riemann(spec, n, rule="mid", div="series").item())
+    b = float(kernels.riemann(spec, n, rule="mid", div="ieee").item())
+    assert a == pytest.approx(b, rel=1e-13, abs=1e-15)
+    assert a == pytest.approx(spec.analytic(), rel=1e-9, abs=1e-12)
+
+
 @pytest.mark.parametrize("n", [10**9, 18_000_000, 1_000_003, 100_003])
 def test_table_segment_tiles_match_per_sample(cuda, n):
     """Velocity-table integrand: the segment-line tiles (one segment read per 64 samples,

@@ -4,7 +4,8 @@
 //   ./miint bench [--integrand pi4] [--n 1e9] [--dtype fp64] [--rule left] [--iters 200]
 //                 [--gpus G] [--div series|ieee] [--unfused] [--no-graph]      (JSON lines)
 //   ./miint sweep [--gpus G]     N in {1e6,1e9,1e10} x dtype {fp64,fp32} x integrand
-//   ./miint table2d [--grid 4096] [--gpus G]   2-D velocity-field integral (BASELINE #5)
+//   ./miint table2d [--grid 4096] [--gpus G] [--slice R/W]   2-D velocity-field integral
+//                                                           (BASELINE #5)
 //   ./miint selfcheck            every SURVEY §6.1 oracle on the GPU, exit 1 on mismatch
 //
 // The reference has no benchmark harness (its only artefact is a wall-clock
@@ -153,6 +154,14 @@ int main(int argc, char** argv) {
     if (cmd == "table2d") {  // BASELINE config #5: 2-D field, g x g samples, rows split
       Table2DConfig c;
       c.grid = static_cast<int>(a.integer("grid", 4096));
+      // --slice R/W: time only rank R's rows of a W-GPU split, on this GPU (no collective)
+      const std::string sl = a.str("slice", "");
+      if (!sl.empty()) {
+        const size_t k = sl.find('/');
+        if (k == std::string::npos) fail("--slice wants R/W", __FILE__, __LINE__);
+        c.rank = std::stoi(sl.substr(0, k));
+        c.world = std::stoi(sl.substr(k + 1));
+      }
       double value = 0.0, ms = 0.0;
       std::mutex mu;
       cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
@@ -163,7 +172,11 @@ int main(int argc, char** argv) {
         if (rank == topo.rank0) value = v;
         if (t > ms) ms = t;
       });
-      if (topo.rank0 == 0) {
+      if (topo.rank0 == 0 && c.world > 1) {
+        std::printf("{\"program\":\"table2d\",\"grid\":%d,\"slice\":\"%d/%d\",\"partial\":%.17g,"
+                    "\"ms_per_integration\":%.6f}\n",
+                    c.grid, c.rank, c.world, value, ms);
+      } else if (topo.rank0 == 0) {
         const double want = table2d_oracle(c.grid);
         const double exact = 122000.004 * 122000.004;
         std::printf("{\"program\":\"table2d\",\"grid\":%d,\"gpus\":%d,\"result\":%.17g,"

@@ -24,6 +24,9 @@ namespace miint {
 struct Table2DConfig {
   int grid = 4096;       // samples per axis
   double extent = 1800;  // [0, extent]^2
+  // Without a communicator: integrate only row slice `rank` of `world` (the share one GPU
+  // of a `world`-GPU run computes; the result is that partial). Ignored with a communicator.
+  int world = 1, rank = 0;
 };
 
 class Table2DPlan {

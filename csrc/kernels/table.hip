@@ -91,11 +91,14 @@ __global__ __launch_bounds__(kB) void outer_product_kernel(const double* __restr
 }
 
 // ---------------------------------------------------------------------------- table2d
-// Workgroup = 16x16 threads = one 64x64 tile of sample points (4x4 per thread).
-constexpr int kTile = 128;   // samples per workgroup and axis (16 x 16 threads, 8 x 8 each)
-constexpr int kPer = kTile / 16;
-constexpr int kLdsDim = 64;  // table footprint per tile in LDS: up to 64 x 64 doubles (33 KB:
-                             // 4 workgroups per CU, so a 4096^2 grid is one resident wave)
+// Workgroup = 16 x 16 threads = one TILE x TILE tile of sample points: TILE = 128 (8 x 8 per
+// thread) when the grid gives every CU at least 4 such tiles, else TILE = 64 (4 x 4 per
+// thread): an 8-GPU row slice of 4096^2 is 128 tiles of 128 for 256 CUs.
+// Table footprint per tile in LDS: up to 64 x 64 doubles for 128-sample tiles (33 KB: 4
+// workgroups per CU, so a 4096^2 grid is one resident wave), 32 x 32 for 64-sample tiles
+// (8.4 KB: the LDS no longer caps residency).
+template <int kTile>
+constexpr int lds_dim() { return kTile == 128 ? 64 : 32; }
 
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
@@ -105,9 +108,11 @@ __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? l
 // SQ_INSTS_VALU 1.07e7 for 16.8e6 samples) — leaving per sample one integer add, two
 // ds_read2_b64 and the bilinear blend. FUSED: the last workgroup reduces all partials
 // (handoff.hpp) and writes out[0]; otherwise one partial per workgroup for a finalize.
-template <bool USE_LDS, bool FUSED>
+template <int kTile, bool USE_LDS, bool FUSED>
 __global__ __launch_bounds__(kB) void table2d_kernel(Table2DParams p, double* partials,
                                                      unsigned* ticket, double* out) {
+  constexpr int kPer = kTile / 16;
+  constexpr int kLdsDim = lds_dim<kTile>();
   __shared__ double tile[kLdsDim * (kLdsDim + 1)];
   __shared__ double red[kB / kWave];
   __shared__ int is_last;
@@ -119,21 +124,23 @@ __global__ __launch_bounds__(kB) void table2d_kernel(Table2DParams p, double* pa
   const int tx0 = clampi(static_cast<int>(((c0 + 0.5) * sx) * cx), 0, p.nx - 2);
   const int ty0 = clampi(static_cast<int>(((r0 + 0.5) * sy) * cy), 0, p.ny - 2);
   if constexpr (USE_LDS) {
-    // One wave per table row (64 lanes = 64 columns, coalesced), rows wave + 4 j: all 16
-    // loads in flight before the LDS writes (a k / w loop issued them one latency at a time).
+    // kLdsDim consecutive lanes per table row (coalesced), kRowsPer rows per pass: all
+    // passes' loads in flight before the LDS writes (a k / w loop issued them one latency at
+    // a time).
+    constexpr int kRowsPer = kB / kLdsDim, kPasses = kLdsDim / kRowsPer;
     const int tx1 = clampi(static_cast<int>(((c0 + kTile - 0.5) * sx) * cx), 0, p.nx - 2) + 1;
     const int ty1 = clampi(static_cast<int>(((r0 + kTile - 0.5) * sy) * cy), 0, p.ny - 2) + 1;
     const int w = tx1 - tx0 + 1, hgt = ty1 - ty0 + 1;
-    const int lx = threadIdx.x & 63, ly = threadIdx.x >> 6;
-    double v[kLdsDim / 4];
+    const int lx = threadIdx.x % kLdsDim, ly = threadIdx.x / kLdsDim;
+    double v[kPasses];
 #pragma unroll
-    for (int j = 0; j < kLdsDim / 4; ++j) {
-      const int rr = ly + 4 * j;
+    for (int j = 0; j < kPasses; ++j) {
+      const int rr = ly + kRowsPer * j;
       v[j] = (lx < w && rr < hgt) ? p.table[static_cast<size_t>(ty0 + rr) * p.nx + tx0 + lx]
                                   : 0.0;
     }
 #pragma unroll
-    for (int j = 0; j < kLdsDim / 4; ++j) tile[(ly + 4 * j) * (kLdsDim + 1) + lx] = v[j];
+    for (int j = 0; j < kPasses; ++j) tile[(ly + kRowsPer * j) * (kLdsDim + 1) + lx] = v[j];
     __syncthreads();
   }
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
@@ -223,16 +230,24 @@ void launch_outer_product(const double* v, int n, double* table, hipStream_t str
   MIINT_HIP(hipGetLastError());
 }
 
-static bool table2d_fits_lds(const Table2DParams& p) {
-  // cells spanned by kTile samples (+2 for partial cells at both ends)
-  const double cells_x = kTile * (p.X / p.gx) * ((p.nx - 1) / p.X) + 2.0;
-  const double cells_y = kTile * (p.Y / p.gy) * ((p.ny - 1) / p.Y) + 2.0;
-  return cells_x + 1.0 <= kLdsDim && cells_y + 1.0 <= kLdsDim;
+// Tile edge for this launch: 128 unless that leaves fewer than 4 tiles per CU (1024).
+static int table2d_tile(const Table2DParams& p) {
+  const long t128 = static_cast<long>((p.gx + 127) / 128) * ((p.row1 - p.row0 + 127) / 128);
+  return t128 >= 1024 ? 128 : 64;
+}
+
+static bool table2d_fits_lds(const Table2DParams& p, int tile) {
+  // cells spanned by `tile` samples (+2 for partial cells at both ends)
+  const double cells_x = tile * (p.X / p.gx) * ((p.nx - 1) / p.X) + 2.0;
+  const double cells_y = tile * (p.Y / p.gy) * ((p.ny - 1) / p.Y) + 2.0;
+  const int dim = tile == 128 ? lds_dim<128>() : lds_dim<64>();
+  return cells_x + 1.0 <= dim && cells_y + 1.0 <= dim;
 }
 
 int table2d_grid(const Table2DParams& p) {
-  const int gxb = (p.gx + kTile - 1) / kTile;
-  const int gyb = (p.row1 - p.row0 + kTile - 1) / kTile;
+  const int t = table2d_tile(p);
+  const int gxb = (p.gx + t - 1) / t;
+  const int gyb = (p.row1 - p.row0 + t - 1) / t;
   return gxb * gyb;
 }
 
@@ -241,29 +256,34 @@ static void check_table2d(const Table2DParams& p) {
   MIINT_CHECK(p.row0 >= 0 && p.row1 <= p.gy && p.row0 < p.row1, "table2d row range");
 }
 
-static dim3 table2d_dims(const Table2DParams& p) {
-  return dim3((p.gx + kTile - 1) / kTile, (p.row1 - p.row0 + kTile - 1) / kTile);
+static dim3 table2d_dims(const Table2DParams& p, int t) {
+  return dim3((p.gx + t - 1) / t, (p.row1 - p.row0 + t - 1) / t);
+}
+
+template <bool FUSED>
+static void launch_table2d(const Table2DParams& p, double* partials, unsigned* ticket,
+                           double* out, hipStream_t stream) {
+  check_table2d(p);
+  const int t = table2d_tile(p);
+  const dim3 grid = table2d_dims(p, t);
+  const bool lds = table2d_fits_lds(p, t);
+  if (t == 128) {
+    if (lds) table2d_kernel<128, true, FUSED><<<grid, kB, 0, stream>>>(p, partials, ticket, out);
+    else table2d_kernel<128, false, FUSED><<<grid, kB, 0, stream>>>(p, partials, ticket, out);
+  } else {
+    if (lds) table2d_kernel<64, true, FUSED><<<grid, kB, 0, stream>>>(p, partials, ticket, out);
+    else table2d_kernel<64, false, FUSED><<<grid, kB, 0, stream>>>(p, partials, ticket, out);
+  }
+  MIINT_HIP(hipGetLastError());
 }
 
 void launch_table2d_partials(const Table2DParams& p, double* partials, hipStream_t stream) {
-  check_table2d(p);
-  const dim3 grid = table2d_dims(p);
-  if (table2d_fits_lds(p))
-    table2d_kernel<true, false><<<grid, kB, 0, stream>>>(p, partials, nullptr, nullptr);
-  else
-    table2d_kernel<false, false><<<grid, kB, 0, stream>>>(p, partials, nullptr, nullptr);
-  MIINT_HIP(hipGetLastError());
+  launch_table2d<false>(p, partials, nullptr, nullptr, stream);
 }
 
 void launch_table2d_fused(const Table2DParams& p, double* partials, unsigned* ticket,
                           double* out, hipStream_t stream) {
-  check_table2d(p);
-  const dim3 grid = table2d_dims(p);
-  if (table2d_fits_lds(p))
-    table2d_kernel<true, true><<<grid, kB, 0, stream>>>(p, partials, ticket, out);
-  else
-    table2d_kernel<false, true><<<grid, kB, 0, stream>>>(p, partials, ticket, out);
-  MIINT_HIP(hipGetLastError());
+  launch_table2d<true>(p, partials, ticket, out, stream);
 }
 
 }  // namespace miint

@@ -14,6 +14,10 @@ Table2DPlan::Table2DPlan(const Table2DConfig& cfg, int device, const Comm* comm)
   if (comm) {
     rank_ = comm->rank();
     world_ = comm->world();
+  } else {
+    MIINT_CHECK(cfg.world >= 1 && cfg.rank >= 0 && cfg.rank < cfg.world, "bad slice rank/world");
+    rank_ = cfg.rank;
+    world_ = cfg.world;
   }
   uint64_t b = 0, c = 0;
   rank_slice(static_cast<uint64_t>(cfg.grid), rank_, world_, &b, &c);
@@ -45,7 +49,7 @@ void Table2DPlan::enqueue(hipStream_t s) {
                           row0_, row1_};
     launch_table2d_fused(p, partials_.get(), ticket_.get(), out, s);
   } else {
-    MIINT_HIP(hipMemsetAsync(result_.get(), 0, sizeof(double), s));  // more ranks than rows
+    MIINT_HIP(hipMemsetAsync(out, 0, sizeof(double), s));  // more ranks than rows
   }
   if (!multi) return;
   comm_->allreduce_sum(result_.get(), result_.get(), 1, s);

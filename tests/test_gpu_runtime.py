@@ -126,6 +126,24 @@ def test_cli_trainscan(cli_built):
     assert js["timeout"] == 0
 
 
+def test_cli_table2d_slices_sum_to_whole(cli_built):
+    """miint table2d --slice R/W integrates one rank's rows of a W-GPU split on this GPU;
+    the partials of all ranks add up to the whole field. 2048^2 runs 64-sample tiles from
+    global memory (a 64-sample tile spans 56 cells, too many for the 32 x 32 LDS footprint),
+    the 8192^2 halves 128-sample tiles staged in LDS."""
+    exe = os.path.join(cli_built, "miint")
+    for g, w in ((2048, 3), (8192, 2)):
+        whole = _run([exe, "table2d", "--grid", str(g), "--iters", "2"])
+        assert whole.returncode == 0, whole.stderr
+        want = json.loads(whole.stdout.strip().splitlines()[-1])["result"]
+        parts = []
+        for r in range(w):
+            q = _run([exe, "table2d", "--grid", str(g), "--slice", f"{r}/{w}", "--iters", "2"])
+            assert q.returncode == 0, q.stderr
+            parts.append(json.loads(q.stdout.strip().splitlines()[-1])["partial"])
+        assert math.fsum(parts) == pytest.approx(want, rel=1e-13)
+
+
 def test_cli_selfcheck(cli_built):
     p = _run([os.path.join(cli_built, "miint"), "selfcheck"])
     assert p.returncode == 0, p.stdout + p.stderr

@@ -4,14 +4,17 @@
 //   Step size of 10000
 //   %lf seconds
 //   Total distance traveled = %lf
-// Per GPU: one fused interp+scan kernel (decoupled look-back) per phase; across GPUs an
-// allgather of one fp64 total per rank and an on-device carry add (no 144 MB gathers, no
-// serial carry loop on a root, no broadcast). --parity reproduces 4main's partitions and
+// Per GPU (default --algo fused): closed-form tile sums with in-block scans and a
+// last-workgroup block scan, then one write pass that generates the samples again and stores
+// both running integrals; across GPUs an allgather of one {T1, T2, count} triple per rank and
+// on-device carries (no 144 MB gathers, no serial carry loop on a root, no broadcast).
+// --algo lookback: one interp+scan kernel (decoupled look-back) per phase; onepass: a single
+// look-back pass over the two-component tile state. --parity reproduces 4main's partitions and
 // printed element (P=7 -> 0.000000, P=16 -> 117642.707174). --replicate allgathers the full
 // table to every rank like 4main.c:157.
 //
 //   ./trainscan [--gpus G] [--parity] [--replicate] [--no-phase2] [--algo onepass|fused|lookback]
-//               [--iters K] [--json]
+//               [--steps-per-sec S] [--iters K] [--json]
 #include <cstdio>
 
 #include "cli_common.hpp"

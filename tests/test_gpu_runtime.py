@@ -74,6 +74,18 @@ def test_trainscan_native(native, cuda):
     assert r["sum_of_sums"] / 1e8 == pytest.approx(109861003.621919, rel=1e-9)
 
 
+def test_trainscan_beyond_2e32_samples(native, cuda):
+    """3e6 samples/s: 5.4e9 samples (> 2^32), 86 GB of vel + pos on one GPU. 64-bit sample
+    indices end to end; the distance is unchanged and the sum of sums scales with sps^2."""
+    cfg = native.TrainScanConfig()
+    cfg.steps_per_sec = 3_000_000
+    r = native.TrainScan(cfg, 0).run()
+    assert r["timeout"] == 0
+    assert abs(r["distance"] - 122000.004) < 1e-6
+    want = 109861003.621919e8 * (3_000_000 / 10_000) ** 2
+    assert r["sum_of_sums"] == pytest.approx(want, rel=1e-9)
+
+
 def _run(args, env=None, timeout=300):
     e = dict(os.environ)
     e.update(env or {})

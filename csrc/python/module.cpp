@@ -125,8 +125,18 @@ PYBIND11_MODULE(_miint, m) {
         c.broadcast(ptr<double>(buf), count, root, stream(s));
       })
       .def("check_async", &Comm::check_async);
-  m.def("rendezvous_unique_id", &rendezvous_unique_id, py::arg("addr"), py::arg("port"),
-        py::arg("rank"), py::arg("world"), py::arg("timeout_s") = 120.0);
+  m.def(
+      "rendezvous_unique_id",
+      [](const std::string& addr, int port, int rank, int world, double timeout_s) {
+        std::string id;
+        {
+          py::gil_scoped_release rel;  // rank 0 blocks in accept() until the others connect
+          id = rendezvous_unique_id(addr, port, rank, world, timeout_s);
+        }
+        return py::bytes(id);  // 128 raw bytes, not text
+      },
+      py::arg("addr"), py::arg("port"), py::arg("rank"), py::arg("world"),
+      py::arg("timeout_s") = 120.0);
 
   // ------------------------------------------------------------------ Riemann plan
   py::class_<RiemannConfig>(m, "RiemannConfig")

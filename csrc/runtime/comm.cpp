@@ -5,6 +5,7 @@
 #include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
+#include <poll.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -128,6 +129,15 @@ std::string rendezvous_unique_id(const std::string& addr, int port, int rank, in
     }
     ::listen(srv, world);
     for (int served = 1; served < world; ++served) {
+      // wait for the next rank, but not forever: a rank that never starts must fail the job
+      pollfd pf{srv, POLLIN, 0};
+      const double left = timeout_s - (wall_seconds() - t0);
+      if (left <= 0 || ::poll(&pf, 1, static_cast<int>(left * 1e3) + 1) <= 0) {
+        ::close(srv);
+        fail("rendezvous timed out: " + std::to_string(served - 1) + " of " +
+                 std::to_string(world - 1) + " ranks connected",
+             __FILE__, __LINE__);
+      }
       int c = ::accept(srv, nullptr, nullptr);
       if (c < 0 || !send_all(c, id.data(), kLen)) {
         if (c >= 0) ::close(c);

@@ -180,8 +180,12 @@ struct Pi4F32 : TileDefaults<Pi4F32> {
             cc = pk_fma(f32x2{4.0f * j + 6.0f, 4.0f * j + 10.0f}, bb, cc);
         }
       }
-      // tile value in fp32 (the path's precision); lanes accumulate tiles in fp64
-      return acc + static_cast<double>(s * (static_cast<float>(UU) + (t.x + t.y)));
+      // Tile value s (U + sum e) folded in fp64: in fp32, U + sum e (|sum e| ~ U |e_m| ~ 4e-6)
+      // rounds at ulp(128) = 1.5e-5 and drops the seed's own correction e_m, leaving every
+      // tile at U fl(1/d_m): a -8e-9 relative bias at N = 1e9 (reproduced on the host by a
+      // numpy emulation of this tile). Folded in fp64 the fp32 path lands on the fp64 sum.
+      return fma(static_cast<double>(s), static_cast<double>(UU) + static_cast<double>(t.x + t.y),
+                 acc);
     } else {
       return acc + tile<UU, M>(xmd, h);
     }

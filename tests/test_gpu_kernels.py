@@ -214,10 +214,12 @@ def test_series_equals_ieee_sum(cuda, n):
 
 
 def test_fp32_error_vs_fp64(cuda):
+    """fp32 per-sample residuals (packed) with tiles folded in fp64: at N = 1e9 the midpoint
+    sum lands within 2.3e-11 of the fp64 one (folding tiles in fp32 was -2.5e-8 biased)."""
     spec = integrands.pi4()
     f32 = float(kernels.riemann(spec, 10**9, rule="mid", dtype="fp32").item())
     f64 = float(kernels.riemann(spec, 10**9, rule="mid", dtype="fp64").item())
-    assert abs(f32 - f64) < 1e-5
+    assert abs(f32 - f64) < 1e-9
     f32i = float(kernels.riemann(spec, 10**7, rule="mid", dtype="fp32", div="ieee").item())
     assert abs(f32i - math.pi) < 1e-5
 

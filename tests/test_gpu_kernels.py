@@ -156,6 +156,21 @@ def test_poly_taylor_pairs_match_horner(cuda, degree, n):
     assert a == pytest.approx(spec.analytic(), rel=1e-9, abs=1e-12)
 
 
+def test_table_segment_tiles_outside_the_profile(cuda):
+    """A domain that runs past both ends of the 1801-sample profile ([-50, 1900]): the
+    clamped end segments extrapolate linearly in the per-sample form, and the segment
+    tiles (line, kink and per-sample fallback) must do exactly the same."""
+    spec = integrands.IntegrandSpec("table", -50.0, 1900.0)
+    n = 19_500_001
+    for i0 in (0, 400_000, n // 2, n - 1_100_000, n - (1 << 16)):
+        v = kernels.point_values(spec, n, rule="mid", div="series", i_begin=i0, n_local=1 << 16)
+        w = kernels.point_values(spec, n, rule="mid", div="ieee", i_begin=i0, n_local=1 << 16)
+        assert float((v - w).abs().max()) <= 4 * 2.0 ** -52 * 128
+    a = float(kernels.riemann(spec, n, rule="mid", div="series").item())
+    b = float(kernels.riemann(spec, n, rule="mid", div="ieee").item())
+    assert a == pytest.approx(b, rel=1e-13, abs=1e-9)
+
+
 @pytest.mark.parametrize("n", [10**9, 18_000_000, 1_000_003, 100_003])
 def test_table_segment_tiles_match_per_sample(cuda, n):
     """Velocity-table integrand: the segment-line tiles (one segment read per 64 samples,

@@ -46,6 +46,8 @@ struct RiemannConfig {
   int waves_per_cu = 32;       // 8 x 256-thread workgroups per CU (the pi4 series kernel
                                // keeps <= 80 SGPRs for this): the default grid is one full wave
   bool fused = true;           // one launch (ticket reduction) vs partials + finalize
+  bool chain = true;           // fused graph batches: kernel k finalizes step k-1 (no ticket;
+                               // launch_riemann_chained), one finalize closes the batch
   bool host_direct = true;     // world == 1: kernel stores the result into pinned memory
   int slots = 16;              // steps per graph batch = result ring depth
   bool bucket = true;          // collective: ONE all-reduce of a batch's `slots` step results
@@ -131,9 +133,13 @@ class RiemannPlan {
   // True when this plan runs an RCCL reduction of its step results.
   bool collective() const { return comm_ && (world_ > 1 || cfg_.force_collective); }
   bool bucketed() const { return collective() && cfg_.bucket; }
+  // Graph batches run chained kernels (see RiemannConfig::chain): single GPU, or bucketed.
+  bool chained() const { return cfg_.fused && cfg_.chain && (!collective() || bucketed()); }
 
  private:
   void enqueue_batch(hipStream_t cs, hipStream_t rs, int nsteps, bool overlap);
+  void enqueue_chain(hipStream_t s, int nsteps) const;
+  double* result_ptr(int j) const { return direct_ ? host_.device_ptr() + j : result_.get() + j; }
   bool use_graphs(bool requested);
 
   RiemannConfig cfg_;
@@ -144,7 +150,7 @@ class RiemannPlan {
   RiemannParams params_{};
   double scale_ = 1.0;
   LaunchShape shape_{1, kRiemannBlock};
-  DeviceBuffer<double> partials_;
+  DeviceBuffer<double> partials_;  // 2 x grid: chained batches alternate halves
   DeviceBuffer<double> result_;
   DeviceBuffer<unsigned int> ticket_;
   DeviceBuffer<double> table_;

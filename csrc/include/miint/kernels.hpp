@@ -93,6 +93,16 @@ void launch_riemann_fused(const RiemannParams& p, DType dtype, DivMode div, Laun
                           const double* table, int table_n, double* partials,
                           unsigned int* ticket, double scale, double* out, hipStream_t stream);
 
+// Batched steps without the ticket: writes this step's partials into partials[0..grid) and,
+// if prev != nullptr, its last workgroup first stores scale * (index-ordered sum of
+// prev[0..nprev)) into out_prev[0] (the previous step's result; nprev == grid). Close a
+// batch with launch_finalize on the last step's partials. Same sums, bit for bit, as the
+// fused and two-kernel paths.
+void launch_riemann_chained(const RiemannParams& p, DType dtype, DivMode div, LaunchShape shape,
+                            const double* table, int table_n, double* partials,
+                            const double* prev, int nprev, double scale, double* out_prev,
+                            hipStream_t stream);
+
 // Debug/validation: write every sample's f value (as the hot tile path computes it) to
 // `out[0..p.n)`; fp64 only. Used by the per-point accuracy tests of the series division.
 void launch_riemann_point_values(const RiemannParams& p, DivMode div, const double* table,

@@ -362,6 +362,44 @@ __global__ __launch_bounds__(B) kFullOccupancy void riemann_fused_kernel_o8(
   fused_body<M, F>(p, table, table_n, partials, ticket, scale, out);
 }
 
+// ---------------------------------------------------------------------------- chained finalize
+// Graph batches of steps: kernel k writes step k's partials (plain stores, no ticket) and its
+// LAST workgroup first sums step k-1's partials (written by kernel k-1; the kernel boundary
+// makes them visible) into step k-1's result, in finalize_kernel's order (bitwise equal to
+// the fused and two-kernel paths). Lanes with the highest ids own one tile round fewer
+// whenever the tiles do not divide evenly over the grid (N = 1e9: 14 rounds instead of 15,
+// ~5 us of slack), so that workgroup absorbs the ~2 us of dependent loads inside the
+// kernel instead of every launch ending with the ticket round trips (fused 76.2 us vs
+// partials-only 73.6 us at N = 1e9). A trailing finalize_kernel closes the batch.
+template <DivMode M, class F>
+__device__ __forceinline__ void chained_body(const RiemannParams& p, const double* table,
+                                             int table_n, double* partials, const double* prev,
+                                             int nprev, double scale, double* out_prev) {
+  __shared__ double red[B / kWave];
+  __shared__ double lds[lds_words<M, F>()];
+  if (prev != nullptr && blockIdx.x == gridDim.x - 1) {
+    const double tot = block_sum<B>(ordered_partials<B, false>(prev, nprev), red);
+    if (threadIdx.x == 0) out_prev[0] = tot * scale;
+    __syncthreads();  // red is reused below
+  }
+  const F f = make_functor<M, F>(p, table, table_n, lds);
+  const double s = block_sum<B>(lane_sum<M>(p, f), red);
+  if (threadIdx.x == 0) partials[blockIdx.x] = s;
+}
+template <DivMode M, class F>
+__global__ __launch_bounds__(B) void riemann_chained_kernel(RiemannParams p, const double* table,
+                                                            int table_n, double* partials,
+                                                            const double* prev, int nprev,
+                                                            double scale, double* out_prev) {
+  chained_body<M, F>(p, table, table_n, partials, prev, nprev, scale, out_prev);
+}
+template <DivMode M, class F>
+__global__ __launch_bounds__(B) kFullOccupancy void riemann_chained_kernel_o8(
+    RiemannParams p, const double* table, int table_n, double* partials, const double* prev,
+    int nprev, double scale, double* out_prev) {
+  chained_body<M, F>(p, table, table_n, partials, prev, nprev, scale, out_prev);
+}
+
 // ---------------------------------------------------------------------------- validation
 // Writes every sample's f value exactly as the hot tile path evaluates it (one lane per
 // tile), so tests can compare the series division point by point against IEEE division.
@@ -420,6 +458,18 @@ void launch_fused_t(const RiemannParams& p, LaunchShape shape, const double* tab
         <<<shape.grid, B, 0, stream>>>(p, table, table_n, partials, ticket, scale, out);
 }
 
+template <DivMode M, class F>
+void launch_chained_t(const RiemannParams& p, LaunchShape shape, const double* table,
+                      int table_n, double* partials, const double* prev, int nprev, double scale,
+                      double* out_prev, hipStream_t stream) {
+  if constexpr (occupancy_hint<M, F>())
+    riemann_chained_kernel_o8<M, F><<<shape.grid, B, 0, stream>>>(p, table, table_n, partials,
+                                                                  prev, nprev, scale, out_prev);
+  else
+    riemann_chained_kernel<M, F><<<shape.grid, B, 0, stream>>>(p, table, table_n, partials,
+                                                               prev, nprev, scale, out_prev);
+}
+
 // Dispatch (integrand, dtype, division mode) to a template instantiation. Transcendental
 // integrands (sin/cos) and the table ignore the division mode (no division in them).
 template <template <DivMode, class> class Op, class... A>
@@ -465,6 +515,9 @@ template <DivMode M, class F> struct PartialsOp {
 };
 template <DivMode M, class F> struct FusedOp {
   template <class... A> static void run(A... a) { launch_fused_t<M, F>(a...); }
+};
+template <DivMode M, class F> struct ChainedOp {
+  template <class... A> static void run(A... a) { launch_chained_t<M, F>(a...); }
 };
 template <DivMode M, class F> struct TileLenOp {
   static void run(int* out) { *out = F::template tile_len<M>(); }
@@ -576,6 +629,20 @@ void launch_riemann_fused(const RiemannParams& p, DType dtype, DivMode div, Laun
   const DivMode eff = effective_div(p, div, dtype);
   dispatch<FusedOp>(p, dtype, eff, prepared(p, eff), shape, table, table_n, partials, ticket,
                     scale, out, stream);
+  MIINT_HIP(hipGetLastError());
+}
+
+void launch_riemann_chained(const RiemannParams& p, DType dtype, DivMode div, LaunchShape shape,
+                            const double* table, int table_n, double* partials,
+                            const double* prev, int nprev, double scale, double* out_prev,
+                            hipStream_t stream) {
+  check_shape(shape);
+  check_params(p, table, table_n);
+  MIINT_CHECK(prev == nullptr || (nprev == shape.grid && out_prev != nullptr),
+              "chained finalize: previous partials must come from the same grid");
+  const DivMode eff = effective_div(p, div, dtype);
+  dispatch<ChainedOp>(p, dtype, eff, prepared(p, eff), shape, table, table_n, partials, prev,
+                      nprev, scale, out_prev, stream);
   MIINT_HIP(hipGetLastError());
 }
 

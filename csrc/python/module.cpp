@@ -161,7 +161,8 @@ PYBIND11_MODULE(_miint, m) {
       .def_readwrite("world", &RiemannConfig::world)
       .def_readwrite("force_collective", &RiemannConfig::force_collective)
       .def_readwrite("timeout_s", &RiemannConfig::timeout_s)
-      .def_readwrite("host_direct", &RiemannConfig::host_direct);
+      .def_readwrite("host_direct", &RiemannConfig::host_direct)
+      .def_readwrite("chain", &RiemannConfig::chain);
 
   py::class_<RiemannPlan>(m, "RiemannPlan")
       .def(py::init<const RiemannConfig&, int, const Comm*>(), py::arg("config"),
@@ -199,6 +200,7 @@ PYBIND11_MODULE(_miint, m) {
       .def_property_readonly("host_capacity", &RiemannPlan::host_capacity)
       .def_property_readonly("slots", &RiemannPlan::slots)
       .def_property_readonly("bucketed", &RiemannPlan::bucketed)
+      .def_property_readonly("chained", &RiemannPlan::chained)
       .def_property_readonly("direct", &RiemannPlan::direct)
       .def_property_readonly("graph_nodes", &RiemannPlan::graph_nodes)
       .def_property_readonly("graphs_ready", &RiemannPlan::graphs_ready)

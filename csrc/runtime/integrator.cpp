@@ -54,7 +54,7 @@ RiemannPlan::RiemannPlan(const RiemannConfig& cfg, int device, const Comm* comm)
   const uint64_t need = std::max<uint64_t>(1, (tiles + kRiemannBlock - 1) / kRiemannBlock);
   shape_.grid = static_cast<int>(std::min<uint64_t>(static_cast<uint64_t>(shape_.grid), need));
 
-  partials_ = DeviceBuffer<double>(static_cast<size_t>(shape_.grid));
+  partials_ = DeviceBuffer<double>(2 * static_cast<size_t>(shape_.grid));
   result_ = DeviceBuffer<double>(static_cast<size_t>(cfg.slots));
   ticket_ = DeviceBuffer<unsigned int>(kTicketWords);
   MIINT_HIP(hipMemset(ticket_.get(), 0, ticket_.bytes()));
@@ -126,7 +126,31 @@ double RiemannPlan::run() {
 // Steps j < nsteps use device slot j and host slot j. With overlap (and something to
 // overlap), the reduce+copy chain runs on `rs` behind per-step events: a fork/join that
 // hipStreamBeginCapture turns into graph edges.
+// Chained batch: kernel j writes step j's partials into half j % 2 and finalizes step j-1
+// from the other half into result slot j-1; a finalize kernel closes step nsteps-1.
+void RiemannPlan::enqueue_chain(hipStream_t s, int nsteps) const {
+  const int g = shape_.grid;
+  const int tn = static_cast<int>(cfg_.table.size());
+  for (int j = 0; j < nsteps; ++j) {
+    double* cur = partials_.get() + static_cast<size_t>(j & 1) * g;
+    const double* prev = j ? partials_.get() + static_cast<size_t>((j - 1) & 1) * g : nullptr;
+    launch_riemann_chained(params_, cfg_.dtype, cfg_.div, shape_, table_.get(), tn, cur, prev, g,
+                           scale_, j ? result_ptr(j - 1) : nullptr, s);
+  }
+  launch_finalize(partials_.get() + static_cast<size_t>((nsteps - 1) & 1) * g, g, scale_,
+                  result_ptr(nsteps - 1), s);
+}
+
 void RiemannPlan::enqueue_batch(hipStream_t cs, hipStream_t rs, int nsteps, bool overlap) {
+  if (chained()) {
+    enqueue_chain(cs, nsteps);
+    if (bucketed()) {  // one all-reduce + one copy of all the batch's results
+      comm_->allreduce_sum(result_.get(), result_.get(), static_cast<size_t>(nsteps), cs);
+      MIINT_HIP(hipMemcpyAsync(host_.get(), result_.get(), sizeof(double) * nsteps,
+                               hipMemcpyDeviceToHost, cs));
+    }
+    return;
+  }
   if (bucketed()) {  // nsteps kernels, then one all-reduce + one copy of all their results
     for (int j = 0; j < nsteps; ++j) enqueue_compute(cs, j, j);
     comm_->allreduce_sum(result_.get(), result_.get(), static_cast<size_t>(nsteps), cs);

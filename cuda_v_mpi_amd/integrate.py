@@ -63,7 +63,7 @@ class Integrator:
                  backend: str = "hip", ctx: DistContext | None = None, comm: str = "native",
                  fused: bool = True, grid: int = 0, slots: int = 16, a: float | None = None,
                  b: float | None = None, force_collective: bool = False, bucket: bool = True,
-                 **spec_kw):
+                 chain: bool = True, **spec_kw):
         spec = integrands.get(integrand, **spec_kw) if isinstance(integrand, str) else integrand
         if a is not None or b is not None:
             spec = dataclasses.replace(spec, a=spec.a if a is None else a,
@@ -98,6 +98,7 @@ class Integrator:
             cfg.grid, cfg.fused, cfg.slots = grid, fused, slots
             cfg.force_collective = force_collective
             cfg.bucket = bucket
+            cfg.chain = chain
             if (self.ctx.world > 1 or force_collective) and comm == "native":
                 self._comm = native_comm(self.ctx)
                 self._plan = m.RiemannPlan(cfg, self.ctx.device, self._comm)

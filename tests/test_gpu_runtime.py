@@ -32,6 +32,24 @@ def test_plan_steps_graph_and_plain_agree(cuda, graphs, fused):
     assert it.plan.host_result(it.plan.host_index_of(8, graphs)) == one
 
 
+@pytest.mark.parametrize("name", ["pi4", "sin", "table", "poly", "train"])
+@pytest.mark.parametrize("collective", [False, True])
+def test_chained_batches_equal_fused_bitwise(cuda, name, collective):
+    """Graph batches of chained kernels (kernel k finalizes step k-1, a finalize closes the
+    batch; no ticket) give every step exactly the fused kernel's value: 21 steps in batches
+    of 8 (two graph replays + 5 enqueued directly), on one GPU and through the bucketed
+    1-rank RCCL stage."""
+    kw = dict(n=50_000_017, rule="mid", slots=8, force_collective=collective)
+    want = Integrator(name, n=50_000_017, rule="mid").run().value
+    for chain in (True, False):
+        it = Integrator(name, chain=chain, **kw)
+        assert it.plan.chained == chain
+        it.run_steps(21, pipeline=True, graphs=True)
+        assert it.plan.graphs_ready, it.plan.graph_error
+        for k in range(13, 21):
+            assert it.plan.host_result(it.plan.host_index_of(k, True)) == want, (chain, k)
+
+
 @pytest.mark.parametrize("bucket", [True, False])
 @pytest.mark.parametrize("graphs", [False, True])
 def test_plan_rccl_stage_on_one_gpu(cuda, graphs, bucket):

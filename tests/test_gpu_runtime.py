@@ -32,15 +32,17 @@ def test_plan_steps_graph_and_plain_agree(cuda, graphs, fused):
     assert it.plan.host_result(it.plan.host_index_of(8, graphs)) == one
 
 
-@pytest.mark.parametrize("name", ["pi4", "sin", "table", "poly", "train"])
+@pytest.mark.parametrize("name", ["pi4", "pi4_fp32", "sin", "table", "poly", "train"])
 @pytest.mark.parametrize("collective", [False, True])
 def test_chained_batches_equal_fused_bitwise(cuda, name, collective):
     """Graph batches of chained kernels (kernel k finalizes step k-1, a finalize closes the
     batch; no ticket) give every step exactly the fused kernel's value: 21 steps in batches
     of 8 (two graph replays + 5 enqueued directly), on one GPU and through the bucketed
     1-rank RCCL stage."""
-    kw = dict(n=50_000_017, rule="mid", slots=8, force_collective=collective)
-    want = Integrator(name, n=50_000_017, rule="mid").run().value
+    dtype = "fp32" if name.endswith("_fp32") else "fp64"
+    name = name.split("_")[0]
+    kw = dict(n=50_000_017, rule="mid", slots=8, force_collective=collective, dtype=dtype)
+    want = Integrator(name, n=50_000_017, rule="mid", dtype=dtype).run().value
     for chain in (True, False):
         it = Integrator(name, chain=chain, **kw)
         assert it.plan.chained == chain

@@ -53,6 +53,20 @@ RiemannPlan::RiemannPlan(const RiemannConfig& cfg, int device, const Comm* comm)
   const uint64_t tiles = (params_.n + tl - 1) / tl;
   const uint64_t need = std::max<uint64_t>(1, (tiles + kRiemannBlock - 1) / kRiemannBlock);
   shape_.grid = static_cast<int>(std::min<uint64_t>(static_cast<uint64_t>(shape_.grid), need));
+  // Small N (latency-bound): give lanes ~4 tiles each, but keep >= 1 workgroup per CU. At
+  // one tile per lane the launch, the partial stores and the final reduction over every
+  // workgroup cost more than the extra rounds (table at 18e6 samples: 7.9 -> 6.4 us; pi4 at
+  // 1e7: 6.0 -> 5.1 us; profiles/r1/small_n_grid.jsonl). N >= 2.7e8 keeps the full grid.
+  // The grid is also rounded down to a whole number of workgroups per CU: at 275 workgroups
+  // on 256 CUs, 19 CUs hold two and finish last (pi4 at 1e8: 17.9 us against 11.2 at 256).
+  if (cfg.grid <= 0) {
+    const uint64_t cus = static_cast<uint64_t>(info.num_cus);
+    const uint64_t four =
+        std::max<uint64_t>(cus, (tiles + 4 * kRiemannBlock - 1) / (4 * kRiemannBlock));
+    uint64_t g = std::min<uint64_t>(static_cast<uint64_t>(shape_.grid), four);
+    if (g > cus) g -= g % cus;
+    shape_.grid = static_cast<int>(g);
+  }
 
   partials_ = DeviceBuffer<double>(2 * static_cast<size_t>(shape_.grid));
   result_ = DeviceBuffer<double>(static_cast<size_t>(cfg.slots));

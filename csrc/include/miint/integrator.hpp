@@ -11,8 +11,10 @@
 //   copyout  : 8-byte hipMemcpyAsync of the slot into pinned memory  [world > 1]
 //
 // Steps are replayed from hipGraphs that hold a whole batch of `slots` steps (one graph
-// launch per batch; on >1 GPU the batch is a fork/join graph: kernels on the compute stream,
-// allreduce+copy of step k on the comm stream overlapping the kernel of step k+1).
+// launch per batch). By default a batch is `slots` chained kernels (kernel k finalizes step
+// k-1, no ticket) and one finalize kernel; on >1 GPU it then ends in ONE all-reduce of all
+// its step results and one copy to pinned memory (bucketed). With bucket = false each step's
+// all-reduce + copy runs on the comm stream (fork/join), overlapping the next kernel.
 //
 // Reference mapping: riemann.cpp:47-101 (MPI master/worker) and cintegrate.cu:101-150
 // (CUDA host driver) are both instances of this plan (see csrc/cli/).
@@ -43,8 +45,8 @@ struct RiemannConfig {
   double p0 = 0.0, p1 = 0.0;   // Integrand::kTrainVel (ts, vs)
   std::vector<double> table;   // Integrand::kTable (host copy, uploaded once)
   int grid = 0;                // workgroups; 0 = auto (waves_per_cu per CU)
-  int waves_per_cu = 32;       // 8 x 256-thread workgroups per CU (the pi4 series kernel
-                               // keeps <= 80 SGPRs for this): the default grid is one full wave
+  int waves_per_cu = 32;       // 8 x 256-thread workgroups per CU (every Riemann kernel fits 8
+                               // waves/SIMD): the default grid is one full wave
   bool fused = true;           // one launch (ticket reduction) vs partials + finalize
   bool chain = true;           // fused graph batches: kernel k finalizes step k-1 (no ticket;
                                // launch_riemann_chained), one finalize closes the batch

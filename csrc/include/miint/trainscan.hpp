@@ -66,14 +66,17 @@ struct TrainScanKernelParams {
 // live in it and every launch leaves them re-armed).
 size_t trainscan_workspace_bytes(uint64_t n);
 // K1 + K2: per-tile sums and tile prefixes into `ws`; totals[0..1] = {T1, T2} (device).
+// fold = true (one GPU, no carries): when the slice has at most 64 blocks of 256 tiles, stop
+// at the per-block aggregates and let launch_trainscan_write(fold = true) fold them per
+// workgroup; totals are then NOT written. Both calls must pass the same `fold`.
 void launch_trainscan_local(const TrainScanKernelParams& p, void* ws, double* totals,
-                            hipStream_t s);
+                            hipStream_t s, bool fold = false);
 // K3: rank carries {C1, C2} from world x {T1, T2, count} gathered triples.
 void launch_trainscan_rank_carry(const double* gathered, int rank, double* carries,
                                  hipStream_t s);
 // K4: write vel (running integral) and pos (its running integral); carries may be null.
 void launch_trainscan_write(const TrainScanKernelParams& p, const void* ws, const double* carries,
-                            double* vel, double* pos, hipStream_t s);
+                            double* vel, double* pos, hipStream_t s, bool fold = false);
 // One pass (K1 + K2 + K4 with a decoupled look-back): vel, pos and totals {T1, T2}.
 void launch_trainscan_onepass(const TrainScanKernelParams& p, void* ws, double* vel, double* pos,
                               double* totals, hipStream_t s);

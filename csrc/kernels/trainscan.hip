@@ -231,6 +231,12 @@ struct ClosedScan {
   unsigned* ticket;
 };
 
+// kHandoff = false (one GPU, <= kMaxFoldBlocks blocks): stop after the per-block aggregates;
+// ts_write folds the few aggregates before its own block itself, so this launch ends without
+// the ticket round trips and the last workgroup's serial block scan.
+constexpr uint32_t kMaxFoldBlocks = 64;  // blocks of kB tiles: 64 x 256 x 4096 = 67M samples
+
+template <bool kHandoff>
 __global__ __launch_bounds__(kB) void ts_tile_scan_closed(TrainScanKernelParams p, uint64_t sps,
                                                           uint32_t ntiles, ClosedScan cs,
                                                           double* totals) {
@@ -250,6 +256,15 @@ __global__ __launch_bounds__(kB) void ts_tile_scan_closed(TrainScanKernelParams 
   __syncthreads();
   block_inclusive_scan<kB>(cnt, red, &N);
   if (valid) cs.local[t] = f64x2{p1, ql};
+  if constexpr (!kHandoff) {
+    if (threadIdx.x == 0) {  // read by the next launch: the kernel boundary orders it
+      double* g = cs.agg + 4 * blockIdx.x;
+      g[0] = A;
+      g[1] = B;
+      g[2] = N;
+    }
+    return;
+  }
   if (threadIdx.x == 0) {
     double* g = cs.agg + 4 * blockIdx.x;
     __hip_atomic_store(g, A, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -359,15 +374,38 @@ __device__ __forceinline__ void store_tile(double* buf, const double (&v)[kItems
 }
 
 __global__ __launch_bounds__(kB) void ts_write(TrainScanKernelParams p, const f64x2* prefix,
-                                               const f64x2* blockpre, const double* carries,
-                                               double* vel, double* pos) {
+                                               const f64x2* blockpre, const double* fold_agg,
+                                               const double* carries, double* vel,
+                                               double* pos) {
   __shared__ double tab[kSpan];
   __shared__ double red[kB / kWave];
   __shared__ __attribute__((aligned(16))) double buf[kTile];
   const Sampler f = make_sampler(p, tab, blockIdx.x);
   const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kTile;
   f64x2 pr = prefix[blockIdx.x];
-  if (blockpre) {  // closed-form path: tile prefix = block prefix (+) in-block prefix
+  if (fold_agg) {  // fold mode: this tile's block prefix from the aggregates before it
+    __shared__ double agg[3 * kMaxFoldBlocks];
+    __shared__ double bpf[2];
+    const uint32_t b = blockIdx.x / kB;
+    if (threadIdx.x < b) {
+      agg[3 * threadIdx.x] = fold_agg[4 * threadIdx.x];
+      agg[3 * threadIdx.x + 1] = fold_agg[4 * threadIdx.x + 1];
+      agg[3 * threadIdx.x + 2] = fold_agg[4 * threadIdx.x + 2];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // same affine fold as ts_rank_carry: Q += N PB + B, PB += A
+      double pb = 0.0, qb = 0.0;
+      for (uint32_t i = 0; i < b; ++i) {
+        qb += fma(agg[3 * i + 2], pb, agg[3 * i + 1]);
+        pb += agg[3 * i];
+      }
+      bpf[0] = pb;
+      bpf[1] = qb;
+    }
+    __syncthreads();
+    const double before = static_cast<double>(blockIdx.x % kB) * kTile;
+    pr = f64x2{bpf[0] + pr.x, fma(before, bpf[0], bpf[1]) + pr.y};
+  } else if (blockpre) {  // closed-form path: tile prefix = block prefix (+) in-block prefix
     const f64x2 bp = blockpre[blockIdx.x / kB];
     const double before = static_cast<double>(blockIdx.x % kB) * kTile;
     pr = f64x2{bp.x + pr.x, fma(before, bp.x, bp.y) + pr.y};
@@ -586,8 +624,14 @@ unsigned trainscan_onepass_timeout(const void* ws, hipStream_t s) {
   return v;
 }
 
+static bool use_fold(const TrainScanKernelParams& p, bool fold) {
+  uint64_t sps = 0;
+  const uint64_t nt = (p.n + kTile - 1) / kTile;
+  return fold && closed_form_sps(p.dt, &sps) && (nt + kB - 1) / kB <= kMaxFoldBlocks;
+}
+
 void launch_trainscan_local(const TrainScanKernelParams& p, void* ws, double* totals,
-                            hipStream_t s) {
+                            hipStream_t s, bool fold) {
   MIINT_CHECK(p.n >= 1, "empty slice");
   MIINT_CHECK(p.table_n >= 2 && p.table_n <= kMaxTable, "table size must be in [2, 2048]");
   const uint64_t nt = (p.n + kTile - 1) / kTile;
@@ -596,8 +640,12 @@ void launch_trainscan_local(const TrainScanKernelParams& p, void* ws, double* to
   if (closed_form_sps(p.dt, &sps)) {  // dt = 1/sps: closed-form tile sums, one launch
     // the ticket is zero from allocation (workspace contract) and re-armed by the kernel
     const ClosedScan cs = closed_carve(ws, nt);
-    ts_tile_scan_closed<<<static_cast<unsigned>((nt + kB - 1) / kB), kB, 0, s>>>(
-        p, sps, static_cast<uint32_t>(nt), cs, totals);
+    if (use_fold(p, fold))
+      ts_tile_scan_closed<false><<<static_cast<unsigned>((nt + kB - 1) / kB), kB, 0, s>>>(
+          p, sps, static_cast<uint32_t>(nt), cs, totals);
+    else
+      ts_tile_scan_closed<true><<<static_cast<unsigned>((nt + kB - 1) / kB), kB, 0, s>>>(
+          p, sps, static_cast<uint32_t>(nt), cs, totals);
     MIINT_HIP(hipGetLastError());
     return;
   }
@@ -616,7 +664,7 @@ void launch_trainscan_rank_carry(const double* gathered, int rank, double* carri
 }
 
 void launch_trainscan_write(const TrainScanKernelParams& p, const void* ws, const double* carries,
-                            double* vel, double* pos, hipStream_t s) {
+                            double* vel, double* pos, hipStream_t s, bool fold) {
   MIINT_CHECK((reinterpret_cast<uintptr_t>(vel) & 15) == 0 &&
                   (reinterpret_cast<uintptr_t>(pos) & 15) == 0,
               "trainscan outputs need 16-B alignment");
@@ -624,11 +672,14 @@ void launch_trainscan_write(const TrainScanKernelParams& p, const void* ws, cons
   uint64_t sps = 0;
   if (closed_form_sps(p.dt, &sps)) {  // layout of launch_trainscan_local's closed-form path
     const ClosedScan cs = closed_carve(const_cast<void*>(ws), nt);
-    ts_write<<<static_cast<unsigned>(nt), kB, 0, s>>>(p, cs.local, cs.blockpre, carries, vel,
-                                                      pos);
+    const bool f = use_fold(p, fold);
+    MIINT_CHECK(!f || carries == nullptr, "fold mode is single-GPU (no rank carries)");
+    ts_write<<<static_cast<unsigned>(nt), kB, 0, s>>>(p, cs.local, f ? nullptr : cs.blockpre,
+                                                      f ? cs.agg : nullptr, carries, vel, pos);
   } else {
     const f64x2* prefix = static_cast<const f64x2*>(ws) + nt;
-    ts_write<<<static_cast<unsigned>(nt), kB, 0, s>>>(p, prefix, nullptr, carries, vel, pos);
+    ts_write<<<static_cast<unsigned>(nt), kB, 0, s>>>(p, prefix, nullptr, nullptr, carries, vel,
+                                                      pos);
   }
   MIINT_HIP(hipGetLastError());
 }

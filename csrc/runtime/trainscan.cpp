@@ -93,7 +93,8 @@ void TrainScan::enqueue_fused(hipStream_t s) {
   TrainScanKernelParams p{table_.get(), static_cast<int>(oracle::profile_table().size()),
                           1.0 / cfg_.steps_per_sec, begin_, count_, win_lo_, win_hi_};
   double* sc = scratch_.get();
-  launch_trainscan_local(p, state_.get(), sc + kTotals, s);
+  const bool fold = !(comm_ && world_ > 1);  // one GPU: no totals needed, no carries
+  launch_trainscan_local(p, state_.get(), sc + kTotals, s, fold);
   const double* carries = nullptr;
   if (comm_ && world_ > 1) {
     // one {T1, T2, count} triple per rank (count written at construction), then each rank
@@ -102,7 +103,7 @@ void TrainScan::enqueue_fused(hipStream_t s) {
     launch_trainscan_rank_carry(sc + kGather, rank_, sc + kCarry + 1, s);
     carries = sc + kCarry + 1;
   }
-  launch_trainscan_write(p, state_.get(), carries, vel_.get(), pos_.get(), s);
+  launch_trainscan_write(p, state_.get(), carries, vel_.get(), pos_.get(), s, fold);
 }
 
 void TrainScan::enqueue_onepass(hipStream_t s) {

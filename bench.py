@@ -198,6 +198,7 @@ def main() -> int:
                 "pipeline": pipeline,
                 "bucketed_allreduce": bool(plan.bucketed),
                 "fused_reduction": not args.unfused,
+                "chained_batches": bool(plan.chained) and graphs,
                 "grid": plan.grid,
             },
         }

@@ -100,6 +100,8 @@ PYBIND11_MODULE(_miint, m) {
   m.def("enable_tracing", &enable_tracing, "roctx ranges around runtime phases (MIINT_ROCTX=1)");
   m.def("tracing_enabled", &tracing_enabled);
   m.def("trace_mark", &trace_mark);
+  m.def("enable_tracing", &enable_tracing, py::arg("on"));
+  m.def("tracing_enabled", &tracing_enabled);
   m.def("wait_with_timeout", [](uintptr_t s, double timeout_s) {
     py::gil_scoped_release nogil;
     return wait_with_timeout(stream(s), timeout_s, nullptr);

@@ -71,6 +71,24 @@ def test_plan_rccl_stage_on_one_gpu(cuda, graphs, bucket):
         assert it.plan.host_result(it.plan.host_index_of(k, graphs)) == want
 
 
+def test_watchdog_times_out_on_a_busy_stream(native, cuda):
+    """The collective watchdog (wait_with_timeout: stream query, RCCL async-error check,
+    abort on timeout) raises when a stream is still busy after the timeout, and returns the
+    wait time once it drains. N = 2e10 keeps the stream busy for ~1.5 ms."""
+    import torch
+
+    from cuda_v_mpi_amd.models import integrands
+    from cuda_v_mpi_amd.ops import kernels
+
+    s = torch.cuda.current_stream().cuda_stream
+    kernels.riemann(integrands.pi4(), 2 * 10**10)
+    with pytest.raises(Exception, match="did not drain"):
+        native.wait_with_timeout(s, 1e-4)
+    kernels.riemann(integrands.pi4(), 10**6)
+    assert native.wait_with_timeout(s, 30.0) >= 0.0
+    torch.cuda.synchronize()
+
+
 def native_serial_pi4_left(n):
     from cuda_v_mpi_amd import native
     m = native()

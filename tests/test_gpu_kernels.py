@@ -43,6 +43,16 @@ def test_riemann_vs_torch(cuda, spec, n):
     assert got == pytest.approx(want, rel=1e-12, abs=1e-12)
 
 
+@pytest.mark.parametrize("n", [1, 63, 4097, 1_000_003, 40_000_001])
+def test_riemann_fp32_small_and_odd_n(cuda, n):
+    """fp32 path at odd N and N below the grid size (remainder samples, partial tiles, the
+    IEEE fallback below 3.2e7 and the series tiles above) against the fp64 torch reference."""
+    spec = integrands.pi4()
+    got = float(kernels.riemann(spec, n, rule="mid", dtype="fp32").item())
+    want = _ref_sum(spec, n, rule="mid")
+    assert got == pytest.approx(want, rel=2e-6)
+
+
 @pytest.mark.parametrize("spec", SPECS, ids=lambda s: s.name)
 def test_fused_equals_two_kernel_bitwise(cuda, spec):
     n = 3_000_017

@@ -7,6 +7,8 @@
 //   ./miint table2d [--grid 4096] [--gpus G] [--slice R/W]   2-D velocity-field integral
 //                                                           (BASELINE #5)
 //   ./miint selfcheck            every SURVEY §6.1 oracle on the GPU, exit 1 on mismatch
+//   ./miint comm [--gpus G] [--max-bytes 144e6] [--iters 20]
+//                                RCCL allreduce / allgather / broadcast sweep, 8 B .. 144 MB
 //
 // The reference has no benchmark harness (its only artefact is a wall-clock
 // "%lf seconds" line covering process start to print); this tool reports device time per
@@ -124,6 +126,64 @@ int selfcheck() {
   return bad ? 1 : 0;
 }
 
+// RCCL collective sweep (SURVEY §7.1 layer 7): the payloads the framework actually moves
+// (8 B Riemann partials, P x 8 B scan carries, the 144 MB table of 4main.c:157) and the sizes
+// between them. Algorithm bandwidth = bytes a rank ends up with / time; bus bandwidth uses
+// the usual ring factors (allreduce 2(P-1)/P, allgather (P-1)/P, broadcast 1), so it is the
+// per-link rate to compare against one xGMI link. Times are the slowest rank's.
+int comm_sweep(const cli::Topology& topo, double max_bytes, int iters) {
+  std::vector<size_t> counts;  // doubles per rank
+  for (size_t c = 1; c * 8.0 <= max_bytes; c *= 8) counts.push_back(c);
+  if (counts.empty() || counts.back() * 8.0 < max_bytes) counts.push_back(static_cast<size_t>(max_bytes / 8));
+  const char* ops[] = {"allreduce", "allgather", "broadcast"};
+  std::vector<double> ms(counts.size() * 3, 0.0);
+  std::mutex mu;
+  auto body = [&](int /*rank*/, int dev, const Comm* comm) {
+    DeviceGuard g(dev);
+    Stream s;
+    const size_t cmax = counts.back();
+    DeviceBuffer<double> a(cmax), b(cmax * static_cast<size_t>(comm->world()));
+    MIINT_HIP(hipMemsetAsync(a.get(), 0, a.bytes(), s.get()));
+    Event e0, e1;
+    for (size_t k = 0; k < counts.size(); ++k)
+      for (int op = 0; op < 3; ++op) {
+        auto issue = [&] {
+          if (op == 0) comm->allreduce_sum(a.get(), b.get(), counts[k], s.get());
+          else if (op == 1) comm->allgather(a.get(), b.get(), counts[k], s.get());
+          else comm->broadcast(a.get(), counts[k], 0, s.get());
+        };
+        for (int w = 0; w < 3; ++w) issue();
+        e0.record(s.get());
+        for (int i = 0; i < iters; ++i) issue();
+        e1.record(s.get());
+        e1.sync();
+        comm->check_async();
+        const double t = Event::elapsed_ms(e0, e1) / iters;
+        std::lock_guard<std::mutex> l(mu);
+        ms[k * 3 + op] = std::max(ms[k * 3 + op], t);
+      }
+  };
+  if (!topo.multiproc && topo.world == 1) {
+    auto one = Comm::init_all({0});
+    body(0, 0, one[0].get());
+  } else {
+    cli::run_ranks(topo, body);
+  }
+  if (topo.rank0 != 0) return 0;
+  const double P = topo.world;
+  for (size_t k = 0; k < counts.size(); ++k)
+    for (int op = 0; op < 3; ++op) {
+      const double bytes = counts[k] * 8.0 * (op == 1 ? P : 1.0);
+      const double t = ms[k * 3 + op];
+      const double alg = bytes / (t * 1e-3) / 1e9;
+      const double factor = op == 0 ? 2.0 * (P - 1) / P : (op == 1 ? (P - 1) / P : 1.0);
+      std::printf("{\"op\":\"%s\",\"gpus\":%d,\"bytes\":%.0f,\"us\":%.3f,"
+                  "\"algbw_GBps\":%.3f,\"busbw_GBps\":%.3f}\n",
+                  ops[op], topo.world, bytes, t * 1e3, alg, alg * factor);
+    }
+  return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -195,6 +255,7 @@ int main(int argc, char** argv) {
       }
       return 0;
     }
+    if (cmd == "comm") return comm_sweep(topo, a.num("max-bytes", 144e6), static_cast<int>(a.integer("iters", 20)));
     if (cmd == "sweep") {
       const std::vector<double> ns = {1e6, 1e9, 1e10};
       const std::vector<std::string> integs = {"pi4", "sin", "poly", "train"};
@@ -211,7 +272,7 @@ int main(int argc, char** argv) {
         }
       return 0;
     }
-    std::fprintf(stderr, "usage: miint info|bench|sweep|table2d|selfcheck [--flags]\n");
+    std::fprintf(stderr, "usage: miint info|bench|sweep|table2d|comm|selfcheck [--flags]\n");
     return 2;
   } catch (const std::exception& e) {
     std::fprintf(stderr, "miint: %s\n", e.what());

@@ -194,6 +194,18 @@ def test_cli_table2d_slices_sum_to_whole(cli_built):
         assert math.fsum(parts) == pytest.approx(want, rel=1e-13)
 
 
+def test_cli_comm_sweep(cli_built):
+    """miint comm: one-rank RCCL sweep of the three collectives; every size reports a
+    positive time, and the broadcast of 1 MB moves at a finite rate."""
+    p = _run([os.path.join(cli_built, "miint"), "comm", "--max-bytes", "1e6", "--iters", "3"])
+    assert p.returncode == 0, p.stdout + p.stderr
+    rows = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]  # RCCL banner
+    assert {r["op"] for r in rows} == {"allreduce", "allgather", "broadcast"}
+    assert {r["bytes"] for r in rows} == {8, 64, 512, 4096, 32768, 262144, 1e6}
+    for r in rows:
+        assert r["gpus"] == 1 and r["us"] > 0 and math.isfinite(r["algbw_GBps"])
+
+
 def test_cli_selfcheck(cli_built):
     p = _run([os.path.join(cli_built, "miint"), "selfcheck"])
     assert p.returncode == 0, p.stdout + p.stderr

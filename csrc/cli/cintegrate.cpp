@@ -95,9 +95,14 @@ int main(int argc, char** argv) {
     const double secs = wall_seconds() - process_start_seconds();
     std::printf("%lf seconds\n", secs);
     std::printf("final distance is:%lf\n", result);
-    if (a.flag("json"))
-      std::printf("{\"program\":\"cintegrate\",\"gpus\":%d,\"result\":%.17g,\"device_ms\":%.6f,"
-                  "\"seconds_wall\":%.6f}\n", topo.world, result, dev_ms, secs);
+    cli::emit(a, cli::JsonRecord()
+                     .add("program", "cintegrate")
+                     .add("gpus", topo.world)
+                     .add("parity", a.flag("parity"))
+                     .add("result", result)
+                     .add("device_ms", dev_ms)
+                     .add("seconds_device", dev_ms * 1e-3)
+                     .add("seconds_wall", secs));
     return 0;
   } catch (const std::exception& e) {
     std::fprintf(stderr, "cintegrate: %s\n", e.what());

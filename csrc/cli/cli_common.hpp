@@ -9,8 +9,10 @@
 //     MASTER_ADDR:MASTER_PORT+17)
 #pragma once
 
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <ctime>
 #include <functional>
 #include <map>
 #include <memory>
@@ -150,6 +152,54 @@ inline std::string json_escape(const std::string& s) {
     o += c;
   }
   return o;
+}
+
+// One flat JSON object, keys in insertion order (SURVEY §5 "Metrics / logging": the run
+// record of every tool). Doubles print round-trippable (%.17g); non-finite ones as null.
+class JsonRecord {
+ public:
+  JsonRecord& add(const std::string& k, double v) {
+    char b[40];
+    if (std::isfinite(v)) std::snprintf(b, sizeof b, "%.17g", v);
+    else std::snprintf(b, sizeof b, "null");
+    return raw(k, b);
+  }
+  JsonRecord& add(const std::string& k, int v) { return raw(k, std::to_string(v)); }
+  JsonRecord& add(const std::string& k, unsigned v) { return raw(k, std::to_string(v)); }
+  JsonRecord& add(const std::string& k, bool v) { return raw(k, v ? "true" : "false"); }
+  JsonRecord& add(const std::string& k, const std::string& v) {
+    return raw(k, "\"" + json_escape(v) + "\"");
+  }
+  JsonRecord& add(const std::string& k, const char* v) { return add(k, std::string(v)); }
+  std::string str() const { return "{" + body_ + "}"; }
+
+ private:
+  JsonRecord& raw(const std::string& k, const std::string& v) {
+    if (!body_.empty()) body_ += ",";
+    body_ += "\"" + json_escape(k) + "\":" + v;
+    return *this;
+  }
+  std::string body_;
+};
+
+// --json prints the record on stdout after the reference's lines; --jsonl PATH appends it
+// to PATH (one object per line; the results log the SURVEY §5 checkpoint row asks for, so
+// sweeps across launches accumulate in one file). Both may be given. Tools whose output IS
+// the record (miint) pass print = true.
+inline void emit(const Args& a, JsonRecord r, bool print = false) {
+  r.add("time_unix", static_cast<double>(std::time(nullptr)));
+  const std::string line = r.str();
+  if (print || a.flag("json")) {
+    std::printf("%s\n", line.c_str());
+    std::fflush(stdout);
+  }
+  const std::string path = a.str("jsonl", "");
+  if (!path.empty()) {
+    std::FILE* f = std::fopen(path.c_str(), "a");
+    if (!f) fail("--jsonl: cannot open " + path + " for appending", __FILE__, __LINE__);
+    std::fprintf(f, "%s\n", line.c_str());
+    std::fclose(f);
+  }
 }
 
 }  // namespace cli

@@ -9,6 +9,7 @@
 //   ./miint selfcheck            every SURVEY §6.1 oracle on the GPU, exit 1 on mismatch
 //   ./miint comm [--gpus G] [--max-bytes 144e6] [--iters 20]
 //                                RCCL allreduce / allgather / broadcast sweep, 8 B .. 144 MB
+// Every record is one JSON line on stdout; --jsonl FILE also appends it to FILE.
 //
 // The reference has no benchmark harness (its only artefact is a wall-clock
 // "%lf seconds" line covering process start to print); this tool reports device time per
@@ -77,13 +78,20 @@ BenchRow bench_one(const cli::Topology& topo, RiemannConfig cfg, int iters, bool
   return row;
 }
 
-void print_row(const BenchRow& r, const char* integ, const char* dtype, const char* rule) {
-  std::printf("{\"integrand\":\"%s\",\"dtype\":\"%s\",\"rule\":\"%s\",\"n\":%.0f,\"gpus\":%d,"
-              "\"ms_per_integration\":%.6f,\"subintervals_per_s\":%.6e,\"result\":%.17g,"
-              "\"analytic\":%.17g,\"abs_err\":%.3e}\n",
-              integ, dtype, rule, r.n, r.gpus, r.ms, r.n / (r.ms * 1e-3), r.result, r.exact,
-              std::fabs(r.result - r.exact));
-  std::fflush(stdout);
+void print_row(const cli::Args& a, const BenchRow& r, const char* integ, const char* dtype,
+               const char* rule) {
+  cli::emit(a, cli::JsonRecord()
+                   .add("integrand", integ)
+                   .add("dtype", dtype)
+                   .add("rule", rule)
+                   .add("n", r.n)
+                   .add("gpus", r.gpus)
+                   .add("ms_per_integration", r.ms)
+                   .add("subintervals_per_s", r.n / (r.ms * 1e-3))
+                   .add("result", r.result)
+                   .add("analytic", r.exact)
+                   .add("abs_err", std::fabs(r.result - r.exact)),
+            true);
 }
 
 int selfcheck() {
@@ -131,7 +139,7 @@ int selfcheck() {
 // between them. Algorithm bandwidth = bytes a rank ends up with / time; bus bandwidth uses
 // the usual ring factors (allreduce 2(P-1)/P, allgather (P-1)/P, broadcast 1), so it is the
 // per-link rate to compare against one xGMI link. Times are the slowest rank's.
-int comm_sweep(const cli::Topology& topo, double max_bytes, int iters) {
+int comm_sweep(const cli::Args& a, const cli::Topology& topo, double max_bytes, int iters) {
   std::vector<size_t> counts;  // doubles per rank
   for (size_t c = 1; c * 8.0 <= max_bytes; c *= 8) counts.push_back(c);
   if (counts.empty() || counts.back() * 8.0 < max_bytes) counts.push_back(static_cast<size_t>(max_bytes / 8));
@@ -177,9 +185,14 @@ int comm_sweep(const cli::Topology& topo, double max_bytes, int iters) {
       const double t = ms[k * 3 + op];
       const double alg = bytes / (t * 1e-3) / 1e9;
       const double factor = op == 0 ? 2.0 * (P - 1) / P : (op == 1 ? (P - 1) / P : 1.0);
-      std::printf("{\"op\":\"%s\",\"gpus\":%d,\"bytes\":%.0f,\"us\":%.3f,"
-                  "\"algbw_GBps\":%.3f,\"busbw_GBps\":%.3f}\n",
-                  ops[op], topo.world, bytes, t * 1e3, alg, alg * factor);
+      cli::emit(a, cli::JsonRecord()
+                       .add("op", ops[op])
+                       .add("gpus", topo.world)
+                       .add("bytes", bytes)
+                       .add("us", t * 1e3)
+                       .add("algbw_GBps", alg)
+                       .add("busbw_GBps", alg * factor),
+                true);
     }
   return 0;
 }
@@ -213,7 +226,7 @@ int main(int argc, char** argv) {
       c.waves_per_cu = static_cast<int>(a.integer("waves-per-cu", 32));
       const BenchRow r = bench_one(topo, c, iters, graphs);
       if (topo.rank0 == 0)
-        print_row(r, a.str("integrand", "pi4").c_str(), a.str("dtype", "fp64").c_str(),
+        print_row(a, r, a.str("integrand", "pi4").c_str(), a.str("dtype", "fp64").c_str(),
                   a.str("rule", "left").c_str());
       return 0;
     }
@@ -238,24 +251,27 @@ int main(int argc, char** argv) {
         if (rank == topo.rank0) value = v;
         if (t > ms) ms = t;
       });
-      if (topo.rank0 == 0 && c.world > 1) {
-        std::printf("{\"program\":\"table2d\",\"grid\":%d,\"slice\":\"%d/%d\",\"partial\":%.17g,"
-                    "\"ms_per_integration\":%.6f}\n",
-                    c.grid, c.rank, c.world, value, ms);
-      } else if (topo.rank0 == 0) {
-        const double want = table2d_oracle(c.grid);
-        const double exact = 122000.004 * 122000.004;
-        std::printf("{\"program\":\"table2d\",\"grid\":%d,\"gpus\":%d,\"result\":%.17g,"
-                    "\"midpoint_oracle\":%.17g,\"rel_err_vs_oracle\":%.3e,"
-                    "\"rel_err_vs_exact\":%.3e,\"ms_per_integration\":%.6f,"
-                    "\"samples_per_s\":%.6e}\n",
-                    c.grid, topo.world, value, want, std::fabs(value - want) / want,
-                    std::fabs(value - exact) / exact, ms,
-                    static_cast<double>(c.grid) * c.grid / (ms * 1e-3));
+      if (topo.rank0 == 0) {
+        cli::JsonRecord r;
+        r.add("program", "table2d").add("grid", c.grid);
+        if (c.world > 1) {
+          r.add("slice", std::to_string(c.rank) + "/" + std::to_string(c.world))
+              .add("partial", value);
+        } else {
+          const double want = table2d_oracle(c.grid);
+          const double exact = 122000.004 * 122000.004;
+          r.add("gpus", topo.world)
+              .add("result", value)
+              .add("midpoint_oracle", want)
+              .add("rel_err_vs_oracle", std::fabs(value - want) / want)
+              .add("rel_err_vs_exact", std::fabs(value - exact) / exact)
+              .add("samples_per_s", static_cast<double>(c.grid) * c.grid / (ms * 1e-3));
+        }
+        cli::emit(a, r.add("ms_per_integration", ms), true);
       }
       return 0;
     }
-    if (cmd == "comm") return comm_sweep(topo, a.num("max-bytes", 144e6), static_cast<int>(a.integer("iters", 20)));
+    if (cmd == "comm") return comm_sweep(a, topo, a.num("max-bytes", 144e6), static_cast<int>(a.integer("iters", 20)));
     if (cmd == "sweep") {
       const std::vector<double> ns = {1e6, 1e9, 1e10};
       const std::vector<std::string> integs = {"pi4", "sin", "poly", "train"};
@@ -267,7 +283,7 @@ int main(int argc, char** argv) {
             RiemannConfig c = make_cfg(integ, n, dt, "left", "series");
             const int it = n >= 1e10 ? 10 : (n >= 1e9 ? 50 : 500);
             const BenchRow r = bench_one(topo, c, it, graphs);
-            if (topo.rank0 == 0) print_row(r, integ.c_str(), dt, "left");
+            if (topo.rank0 == 0) print_row(a, r, integ.c_str(), dt, "left");
           }
         }
       return 0;

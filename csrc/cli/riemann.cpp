@@ -10,7 +10,7 @@
 // samples each, rank-order sum, P=1 -> 0) on the GPU.
 //
 //   ./riemann [--n 1e9] [--gpus G] [--integrand sin|pi4|poly|train] [--rule left|mid]
-//             [--dtype fp64|fp32] [--iters K] [--parity] [--json]
+//             [--dtype fp64|fp32] [--iters K] [--parity] [--json] [--jsonl FILE]
 #include <cmath>
 #include <cstdio>
 #include <iostream>
@@ -95,14 +95,23 @@ int main(int argc, char** argv) {
     std::cout.precision(15);
     std::cout << "The integral of f(x) from 0.0 to " << hi << " with " << nd << " steps is "
               << result << std::endl;
-    if (a.flag("json")) {
-      const double exact = oracle::analytic(f, lo, hi, cfg.coef, cfg.p0, cfg.p1);
-      std::printf("{\"program\":\"riemann\",\"n\":%.0f,\"gpus\":%d,\"result\":%.17g,"
-                  "\"analytic\":%.17g,\"abs_err\":%.3e,\"device_ms\":%.6f,"
-                  "\"subintervals_per_s\":%.6e,\"seconds_wall\":%.6f}\n",
-                  nd, topo.world, result, exact, std::fabs(result - exact), dev_ms,
-                  dev_ms > 0 ? nd / (dev_ms * 1e-3) : 0.0, secs);
-    }
+    const double exact = oracle::analytic(f, lo, hi, cfg.coef, cfg.p0, cfg.p1);
+    cli::emit(a, cli::JsonRecord()
+                     .add("program", "riemann")
+                     .add("integrand", a.str("integrand", "sin"))
+                     .add("dtype", a.str("dtype", "fp64"))
+                     .add("rule", a.str("rule", "left"))
+                     .add("n", nd)
+                     .add("gpus", topo.world)
+                     .add("parity", a.flag("parity"))
+                     .add("result", result)
+                     .add("analytic", exact)
+                     .add("abs_err", std::fabs(result - exact))
+                     .add("rel_err", std::fabs(result - exact) / std::fabs(exact))
+                     .add("device_ms", dev_ms)
+                     .add("seconds_device", dev_ms * 1e-3)
+                     .add("subintervals_per_s", dev_ms > 0 ? nd / (dev_ms * 1e-3) : 0.0)
+                     .add("seconds_wall", secs));
     return 0;
   } catch (const std::exception& e) {
     std::fprintf(stderr, "riemann: %s\n", e.what());

@@ -14,7 +14,7 @@
 // table to every rank like 4main.c:157.
 //
 //   ./trainscan [--gpus G] [--parity] [--replicate] [--no-phase2] [--algo onepass|fused|lookback]
-//               [--steps-per-sec S] [--iters K] [--json]
+//               [--steps-per-sec S] [--iters K] [--json] [--jsonl FILE]
 #include <cstdio>
 
 #include "cli_common.hpp"
@@ -58,10 +58,15 @@ int main(int argc, char** argv) {
     const double secs = wall_seconds() - process_start_seconds();
     std::printf("%lf seconds\n", secs);
     std::printf("Total distance traveled = %lf\n", res.distance);
-    if (a.flag("json"))
-      std::printf("{\"program\":\"trainscan\",\"gpus\":%d,\"distance\":%.17g,\"sum_of_sums\":%.17g,"
-                  "\"device_ms\":%.6f,\"timeout\":%u,\"seconds_wall\":%.6f}\n",
-                  topo.world, res.distance, res.sum_of_sums, res.device_ms, res.timeout, secs);
+    cli::emit(a, cli::JsonRecord()
+                     .add("program", "trainscan")
+                     .add("gpus", topo.world)
+                     .add("distance", res.distance)
+                     .add("sum_of_sums", res.sum_of_sums)
+                     .add("device_ms", res.device_ms)
+                     .add("seconds_device", res.device_ms * 1e-3)
+                     .add("timeout", static_cast<unsigned>(res.timeout))
+                     .add("seconds_wall", secs));
     return res.timeout ? 3 : 0;
   } catch (const std::exception& e) {
     std::fprintf(stderr, "trainscan: %s\n", e.what());

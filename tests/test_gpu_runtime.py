@@ -194,6 +194,27 @@ def test_cli_table2d_slices_sum_to_whole(cli_built):
         assert math.fsum(parts) == pytest.approx(want, rel=1e-13)
 
 
+def test_cli_jsonl_appends_run_records(cli_built, tmp_path):
+    """--jsonl FILE appends one record per run (SURVEY §5 metrics row), across tools; stdout
+    keeps only the reference's lines unless --json is also given."""
+    log = tmp_path / "runs.jsonl"
+    for args in (["riemann", "--integrand", "pi4", "--n", "1e6"],
+                 ["riemann", "--integrand", "pi4", "--n", "1e6", "--rule", "mid"],
+                 ["cintegrate"], ["trainscan"]):
+        p = _run([os.path.join(cli_built, args[0]), *args[1:], "--jsonl", str(log)])
+        assert p.returncode == 0, p.stderr
+        assert not any(l.startswith("{") for l in p.stdout.splitlines())
+    rows = [json.loads(l) for l in log.read_text().splitlines()]
+    assert [r["program"] for r in rows] == ["riemann", "riemann", "cintegrate", "trainscan"]
+    want = {"n", "integrand", "dtype", "rule", "gpus", "seconds_wall", "seconds_device",
+            "subintervals_per_s", "result", "abs_err", "rel_err"}
+    assert want <= set(rows[0])
+    assert rows[0]["abs_err"] == pytest.approx(1e-6, rel=1e-6)  # left rule: |err| = h
+    assert rows[1]["rule"] == "mid" and rows[1]["abs_err"] < 1e-12
+    assert rows[2]["result"] == pytest.approx(122000.004, abs=1e-6)
+    assert rows[3]["distance"] == pytest.approx(122000.004, abs=1e-6)
+
+
 def test_cli_comm_sweep(cli_built):
     """miint comm: one-rank RCCL sweep of the three collectives; every size reports a
     positive time, and the broadcast of 1 MB moves at a finite rate."""

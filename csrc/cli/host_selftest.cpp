@@ -5,13 +5,19 @@
 // uninitialised buffer B12, 288 MB of stack arrays B11, int overflow B9). The GPU-side
 // sanitizers are not available on the target pool, so this binary exercises every host
 // code path that needs no device — profile generation, oracles, parity emulation of all
-// three reference programs, 64-bit slicing, CLI argument parsing — under ASan/UBSan.
+// three reference programs, 64-bit slicing, CLI argument parsing, run records, the TCP
+// rendezvous of the native multi-process launch — under ASan/UBSan.
 #include <cmath>
 #include <cstdio>
+#include <fstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "cli_common.hpp"
+#include <unistd.h>
+
+#include "miint/comm.hpp"
 #include "miint/integrator.hpp"
 #include "miint/oracle.hpp"
 
@@ -70,6 +76,49 @@ int main() {
   expect(threw && cli::parse_integrand("pi") == Integrand::kPi4 &&
              cli::parse_integrand("table") == Integrand::kTable,
          "integrand names: aliases accepted, unknown names rejected");
+
+  // run records: escaping, non-finite values, --jsonl appends
+  const std::string path = "/tmp/miint_selftest_" + std::to_string(::getpid()) + ".jsonl";
+  const std::string jl = "--jsonl=" + path;
+  const char* argv2[] = {"x", jl.c_str()};
+  cli::Args b(2, const_cast<char**>(argv2));
+  cli::JsonRecord r;
+  r.add("s", "a\"b\\c").add("x", 0.1).add("inf", INFINITY).add("i", 7).add("t", true);
+  expect(r.str() == "{\"s\":\"a\\\"b\\\\c\",\"x\":0.10000000000000001,\"inf\":null,\"i\":7,"
+                    "\"t\":true}",
+         "json record: escapes, %.17g, non-finite -> null");
+  cli::emit(b, r);
+  cli::emit(b, cli::JsonRecord().add("k", 2));
+  std::ifstream in(path);
+  std::string l1, l2, l3;
+  std::getline(in, l1);
+  std::getline(in, l2);
+  expect(l1.rfind("{\"s\":", 0) == 0 && l2.rfind("{\"k\":2,\"time_unix\":", 0) == 0 &&
+             !std::getline(in, l3),
+         "--jsonl appends one line per record");
+  std::remove(path.c_str());
+
+  // TCP rendezvous transport (the RCCL id itself needs a GPU with this RCCL): 4 ranks as
+  // threads, rank 0 last to start, all receive rank 0's 128 bytes, zero bytes included
+  std::string id(128, '\0');
+  for (size_t k = 0; k < id.size(); ++k) id[k] = static_cast<char>(k * 37 + 11);
+  std::vector<std::string> ids(4);
+  std::vector<std::thread> th;
+  const int port = 20000 + ::getpid() % 20000;
+  for (int k = 3; k >= 0; --k)
+    th.emplace_back([&, k] {
+      ids[k] = rendezvous_share("127.0.0.1", port, k, 4, k == 0 ? id : std::string(), 128, 30.0);
+    });
+  for (auto& t : th) t.join();
+  expect(ids[0] == id && ids[1] == id && ids[2] == id && ids[3] == id,
+         "rendezvous: 4 ranks receive rank 0's 128-byte payload");
+  bool timed_out = false;
+  try {
+    (void)rendezvous_share("127.0.0.1", port + 1, 1, 2, std::string(), 128, 0.2);
+  } catch (const Error&) {
+    timed_out = true;
+  }
+  expect(timed_out, "rendezvous: a rank whose rank 0 never listens times out");
 
   std::printf("%s\n", g_bad ? "HOST SELFTEST FAILED" : "HOST SELFTEST OK");
   return g_bad ? 1 : 0;

@@ -72,5 +72,10 @@ class Comm {
 // to every other rank. Used when the CLI is launched by torchrun --no-python.
 std::string rendezvous_unique_id(const std::string& addr, int port, int rank, int world,
                                  double timeout_s = 120.0);
+// The transport underneath: rank 0 serves `payload` (exactly len bytes) to world - 1
+// connections and returns it; every other rank connects (retrying until rank 0 listens)
+// and returns the len bytes it received. Both sides fail after timeout_s.
+std::string rendezvous_share(const std::string& addr, int port, int rank, int world,
+                             const std::string& payload, size_t len, double timeout_s);
 
 }  // namespace miint

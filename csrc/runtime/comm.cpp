@@ -110,11 +110,18 @@ bool recv_all(int fd, char* p, size_t n) {
 
 std::string rendezvous_unique_id(const std::string& addr, int port, int rank, int world,
                                  double timeout_s) {
-  constexpr size_t kLen = sizeof(ncclUniqueId);
   if (world == 1) return Comm::unique_id();
+  return rendezvous_share(addr, port, rank, world, rank == 0 ? Comm::unique_id() : std::string(),
+                          sizeof(ncclUniqueId), timeout_s);
+}
+
+std::string rendezvous_share(const std::string& addr, int port, int rank, int world,
+                             const std::string& payload, size_t len, double timeout_s) {
+  const size_t kLen = len;
   const double t0 = wall_seconds();
   if (rank == 0) {
-    const std::string id = Comm::unique_id();
+    MIINT_CHECK(payload.size() == kLen, "rendezvous payload must be " + std::to_string(kLen) + " bytes");
+    const std::string& id = payload;
     int srv = ::socket(AF_INET, SOCK_STREAM, 0);
     MIINT_CHECK(srv >= 0, "socket()");
     int one = 1;

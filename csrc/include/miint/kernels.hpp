@@ -160,6 +160,9 @@ struct Table2DParams {
   int row0, row1;    // sample rows owned by this launch
 };
 int table2d_grid(const Table2DParams& p);
+// Which kernel a launch runs: "stream" (LDS footprint + row streaming, fine grids) or
+// "tile" (coarse grids, table read from global memory).
+const char* table2d_path(const Table2DParams& p);
 void launch_table2d_partials(const Table2DParams& p, double* partials, hipStream_t stream);
 // One launch: partials + last-workgroup reduction into out[0] (ticket: kTicketWords words,
 // zero before the first launch, re-armed by the kernel; partials: table2d_grid(p) doubles).

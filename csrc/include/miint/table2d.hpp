@@ -4,9 +4,10 @@
 // Field: F(x, y) = v(x) v(y) on [0, 1800]^2, materialised as the 1801 x 1801 fp64 outer
 // product of the generated profile (25.9 MB, built on the device), integrated with a
 // midpoint rule on a g x g sample grid using bilinear interpolation of the table. The
-// kernel (table.hip) gives each workgroup a 64 x 64 block of samples and stages the table
-// footprint of that block in LDS (2-D LDS tiling). Ranks split the sample rows; the
-// per-rank partials meet in one RCCL all-reduce.
+// kernel (table.hip) gives each workgroup 256 sample columns by 4 R sample rows, stages the
+// table footprint of that block in LDS (2-D LDS tiling) and streams each wave down its R
+// rows (coarse grids: a tile kernel reading the table from global memory). Ranks split the
+// sample rows; the per-rank partials meet in one RCCL all-reduce.
 //
 // Oracle: bilinear interpolation of a separable product of piecewise-linear factors is
 // exactly v(x) v(y), so the midpoint sum equals (sum_j v(x_j) dx)^2 — a 1-D computation —

@@ -10,7 +10,8 @@
 // (global_store_dwordx4 / global_load_dwordx4), grid-stride over 64-bit indices.
 // The 2-D config (BASELINE.json #5) has no reference counterpart: it integrates a
 // ny x nx fp64 field with bilinear interpolation, each workgroup staging the table
-// footprint of its 64x64 sample tile in LDS (2-D LDS tiling).
+// footprint of its 256-column block of sample rows in LDS (2-D LDS tiling) and streaming
+// down the rows.
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
@@ -91,84 +92,50 @@ __global__ __launch_bounds__(kB) void outer_product_kernel(const double* __restr
 }
 
 // ---------------------------------------------------------------------------- table2d
-// Workgroup = 16 x 16 threads = one TILE x TILE tile of sample points: TILE = 128 (8 x 8 per
-// thread) when the grid gives every CU at least 4 such tiles, else TILE = 64 (4 x 4 per
-// thread): an 8-GPU row slice of 4096^2 is 128 tiles of 128 for 256 CUs.
-// Table footprint per tile in LDS: up to 64 x 64 doubles for 128-sample tiles (33 KB: 4
-// workgroups per CU, so a 4096^2 grid is one resident wave), 32 x 32 for 64-sample tiles
-// (8.4 KB: the LDS no longer caps residency).
-template <int kTile>
-constexpr int lds_dim() { return kTile == 128 ? 64 : 32; }
-
+// Two kernels. Fine sample grids (spacing below ~half a table cell in x, so a workgroup's
+// table footprint fits its LDS tile: 4096^2 and up on the 1801^2 field) run the row stream
+// below. Coarser grids run this tile kernel, reading the table straight from global memory
+// (through L2 and the MALL): workgroup = 16 x 16 threads = one TILE x TILE tile of
+// sample points, TILE = 128 (8 x 8 per thread) when the grid gives every CU at least 4
+// such tiles, else 64 (4 x 4 per thread).
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
-// Per thread: 8 x 8 samples (columns c0 + tx + 16 b, rows r0 + ty + 16 a). The column
-// terms (LDS column, fraction) and row terms (LDS row offset, fraction) are computed once
-// per thread — 16 index computations instead of 64 (the first form spent 41 VALU per sample,
-// SQ_INSTS_VALU 1.07e7 for 16.8e6 samples) — leaving per sample one integer add, two
-// ds_read2_b64 and the bilinear blend. FUSED: the last workgroup reduces all partials
-// (handoff.hpp) and writes out[0]; otherwise one partial per workgroup for a finalize.
-template <int kTile, bool USE_LDS, bool FUSED>
+// Per thread: columns c0 + tx + 16 b, rows r0 + ty + 16 a. The column terms (table column,
+// fraction) and row terms (row offset, fraction) are computed once per thread — 2 kPer
+// index computations instead of kPer^2 (the first form spent 41 VALU per sample) — leaving
+// per sample four loads and the bilinear blend. FUSED: the last workgroup reduces all
+// partials (handoff.hpp) and writes out[0]; otherwise one partial per workgroup for a
+// finalize.
+template <int kTile, bool FUSED>
 __global__ __launch_bounds__(kB) void table2d_kernel(Table2DParams p, double* partials,
                                                      unsigned* ticket, double* out) {
   constexpr int kPer = kTile / 16;
-  constexpr int kLdsDim = lds_dim<kTile>();
-  __shared__ double tile[kLdsDim * (kLdsDim + 1)];
   __shared__ double red[kB / kWave];
   __shared__ int is_last;
   const double sx = p.X / p.gx, sy = p.Y / p.gy;          // sample spacing
   const double cx = (p.nx - 1) / p.X, cy = (p.ny - 1) / p.Y;  // table cells per unit
   const int c0 = blockIdx.x * kTile;
   const int r0 = p.row0 + blockIdx.y * kTile;
-  // Table footprint of this tile: cells touched by its first and last sample.
-  const int tx0 = clampi(static_cast<int>(((c0 + 0.5) * sx) * cx), 0, p.nx - 2);
-  const int ty0 = clampi(static_cast<int>(((r0 + 0.5) * sy) * cy), 0, p.ny - 2);
-  if constexpr (USE_LDS) {
-    // kLdsDim consecutive lanes per table row (coalesced), kRowsPer rows per pass: all
-    // passes' loads in flight before the LDS writes (a k / w loop issued them one latency at
-    // a time).
-    constexpr int kRowsPer = kB / kLdsDim, kPasses = kLdsDim / kRowsPer;
-    const int tx1 = clampi(static_cast<int>(((c0 + kTile - 0.5) * sx) * cx), 0, p.nx - 2) + 1;
-    const int ty1 = clampi(static_cast<int>(((r0 + kTile - 0.5) * sy) * cy), 0, p.ny - 2) + 1;
-    const int w = tx1 - tx0 + 1, hgt = ty1 - ty0 + 1;
-    const int lx = threadIdx.x % kLdsDim, ly = threadIdx.x / kLdsDim;
-    double v[kPasses];
-#pragma unroll
-    for (int j = 0; j < kPasses; ++j) {
-      const int rr = ly + kRowsPer * j;
-      v[j] = (lx < w && rr < hgt) ? p.table[static_cast<size_t>(ty0 + rr) * p.nx + tx0 + lx]
-                                  : 0.0;
-    }
-#pragma unroll
-    for (int j = 0; j < kPasses; ++j) tile[(ly + kRowsPer * j) * (kLdsDim + 1) + lx] = v[j];
-    __syncthreads();
-  }
   const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
-  constexpr int kRow = kLdsDim + 1;
-  using Off = typename std::conditional<USE_LDS, int, size_t>::type;  // 32-bit LDS offsets
-  Off col[kPer], row[kPer];
+  size_t col[kPer], row[kPer];
   double fx[kPer], fy[kPer];
 #pragma unroll
   for (int b = 0; b < kPer; ++b) {
-    const int c = c0 + tx + 16 * b;
-    const double xx = ((c + 0.5) * sx) * cx;
+    const double xx = ((c0 + tx + 16 * b + 0.5) * sx) * cx;
     const int ix = clampi(static_cast<int>(xx), 0, p.nx - 2);
     fx[b] = xx - ix;
-    col[b] = USE_LDS ? ix - tx0 : ix;
+    col[b] = ix;
   }
 #pragma unroll
   for (int a = 0; a < kPer; ++a) {
-    const int r = r0 + ty + 16 * a;
-    const double yy = ((r + 0.5) * sy) * cy;
+    const double yy = ((r0 + ty + 16 * a + 0.5) * sy) * cy;
     const int iy = clampi(static_cast<int>(yy), 0, p.ny - 2);
     fy[a] = yy - iy;
-    row[a] = USE_LDS ? static_cast<Off>((iy - ty0) * kRow) : static_cast<Off>(iy) * p.nx;
+    row[a] = static_cast<size_t>(iy) * p.nx;
   }
-  const double* base = USE_LDS ? tile : p.table;
-  const Off stride = USE_LDS ? static_cast<Off>(kRow) : static_cast<Off>(p.nx);
   auto sample = [&](int a, int b) {
-    const double* t = base + (row[a] + col[b]);
-    const double v00 = t[0], v01 = t[1], v10 = t[stride], v11 = t[stride + 1];
+    const double* t = p.table + (row[a] + col[b]);
+    const double v00 = t[0], v01 = t[1], v10 = t[p.nx], v11 = t[p.nx + 1];
     const double top = fma(v01 - v00, fx[b], v00);
     const double bot = fma(v11 - v10, fx[b], v10);
     return fma(bot - top, fy[a], top);
@@ -187,6 +154,155 @@ __global__ __launch_bounds__(kB) void table2d_kernel(Table2DParams p, double* pa
         if (r0 + ty + 16 * a < p.row1 && c0 + tx + 16 * b < p.gx) acc += sample(a, b);
   }
   const double s = block_sum<kB>(acc, red) * (sx * sy);
+  const unsigned bid = blockIdx.y * gridDim.x + blockIdx.x;
+  if constexpr (!FUSED) {
+    if (threadIdx.x == 0) partials[bid] = s;
+  } else {
+    const unsigned nb = gridDim.x * gridDim.y;
+    if (!publish_and_ticket(s, partials, ticket, bid, nb, &is_last)) return;
+    const double tot = block_sum<kB>(ordered_partials<kB, true>(partials, static_cast<int>(nb)), red);
+    if (threadIdx.x == 0) out[0] = tot;
+    rearm_ticket(ticket, nb);
+  }
+}
+
+// ------------------------------------------------------------------- table2d, row stream
+// For fine sample grids (spacing below half a table cell: 4096^2 and up for the 1801^2
+// field). Every lane of a wave owns kSCols columns (c0 + lane + 64 b) and all lanes walk the
+// SAME rows, so the table row a sample falls in, and its fraction fy, are wave-uniform:
+// lane k computes row k's (iy, fy) once, and row k's values come back as SGPRs through
+// v_readlane. Per column a lane keeps the x-interpolated lines of the current table row
+// pair, Lc (row iy) and D = Ln - Lc (Ln: row iy + 1); each sample is then
+//   v = fma(D, fy, Lc),  acc += v                       (2 VALU, fy an SGPR operand)
+// — the same value the tile kernel forms (top + fy (bot - top)) — and only when iy moves
+// (a scalar compare and branch, once per ~2.3 sample rows at 4096^2) does the lane read
+// one ds_read2_b64 for the new line. The tile kernel reads 32 B of LDS and spends ~15 VALU
+// per sample; this one reads ~7 B and ~4 VALU.
+constexpr int kSCols = 4;                 // columns per lane: a workgroup spans 256 columns
+constexpr int kSW = kWave * kSCols / 2;   // LDS footprint width (cells), 128
+constexpr int kSH = 32;                   // LDS footprint height (cells)
+
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const long long bits = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_readlane(static_cast<int>(bits), lane);
+  const int hi = __builtin_amdgcn_readlane(static_cast<int>(bits >> 32), lane);
+  return __builtin_bit_cast(double, (static_cast<long long>(hi) << 32) |
+                                        static_cast<unsigned int>(lo));
+}
+
+// fma(a, s, c) with s in an SGPR pair as one VOP3 v_fma_f64: left to itself hipcc emits
+// v_mov_b64 + v_fmac_f64 (c is still live), 3 VALU per sample instead of 2.
+__device__ __forceinline__ double fma_sv(double a, double s, double c) {
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "s"(s), "v"(c));
+  return r;
+}
+
+template <bool FUSED>
+__global__ __launch_bounds__(kB) void table2d_stream_kernel(Table2DParams p, int rows_per_wave,
+                                                            double* partials, unsigned* ticket,
+                                                            double* out) {
+  __shared__ double tile[kSH * kSW];
+  __shared__ double red[kB / kWave];
+  __shared__ int is_last;
+  const double sx = p.X / p.gx, sy = p.Y / p.gy;
+  const double cx = (p.nx - 1) / p.X, cy = (p.ny - 1) / p.Y;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) / kWave);
+  const int lane = static_cast<int>(threadIdx.x) % kWave;
+  const int c0 = blockIdx.x * (kWave * kSCols);
+  const int r0 = p.row0 + blockIdx.y * (4 * rows_per_wave);
+  const int r1 = min(r0 + 4 * rows_per_wave, p.row1);
+  // table footprint of the workgroup's samples (first / last column and row)
+  // (computed on the VALU: readfirstlane moves the uniform results to SGPRs, so the staging
+  // addresses below are an SGPR base plus 32-bit lane offsets)
+  const int clast = min(c0 + kWave * kSCols, p.gx) - 1;
+  const int tx0 = __builtin_amdgcn_readfirstlane(
+      clampi(static_cast<int>(((c0 + 0.5) * sx) * cx), 0, p.nx - 2));
+  const int ty0 = __builtin_amdgcn_readfirstlane(
+      clampi(static_cast<int>(((r0 + 0.5) * sy) * cy), 0, p.ny - 2));
+  const int tx1 = __builtin_amdgcn_readfirstlane(
+      clampi(static_cast<int>(((clast + 0.5) * sx) * cx), 0, p.nx - 2) + 1);
+  const int ty1 = __builtin_amdgcn_readfirstlane(
+      clampi(static_cast<int>(((r1 - 1 + 0.5) * sy) * cy), 0, p.ny - 2) + 1);
+  {
+    // kSW consecutive lanes per table row, 2 rows per pass; every pass's load in flight
+    // before the LDS writes. Branch-free: a lane outside the footprint loads the corner
+    // (its LDS slot is never read), and addresses are a uniform base plus 32-bit offsets.
+    constexpr int kRowsPer = kB / kSW, kPasses = kSH / kRowsPer;
+    const int w = tx1 - tx0 + 1, hgt = ty1 - ty0 + 1;
+    const int lx = threadIdx.x % kSW, ly = threadIdx.x / kSW;
+    const double* tb = p.table + static_cast<size_t>(ty0) * p.nx + tx0;
+    double v[kPasses];
+#pragma unroll
+    for (int j = 0; j < kPasses; ++j) {
+      const int rr = ly + kRowsPer * j;
+      const unsigned off = (lx < w && rr < hgt) ? static_cast<unsigned>(rr * p.nx + lx) * 8u : 0u;
+      v[j] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(tb) + off);
+    }
+#pragma unroll
+    for (int j = 0; j < kPasses; ++j) tile[(ly + kRowsPer * j) * kSW + lx] = v[j];
+  }
+  // per-lane columns: LDS column and x fraction, computed once
+  int col[kSCols];
+  double fx[kSCols];
+  bool ok[kSCols];
+#pragma unroll
+  for (int b = 0; b < kSCols; ++b) {
+    const int c = c0 + lane + kWave * b;
+    ok[b] = c < p.gx;
+    const double xx = ((min(c, p.gx - 1) + 0.5) * sx) * cx;
+    const int ix = clampi(static_cast<int>(xx), 0, p.nx - 2);
+    fx[b] = xx - ix;
+    col[b] = ix - tx0;
+  }
+  // this wave's rows; lane k holds row k's table row and fraction
+  const int rbase = r0 + wave * rows_per_wave;
+  const int nrows = max(0, min(rows_per_wave, r1 - rbase));
+  int iyl;
+  double fyl;
+  {
+    const int r = rbase + min(lane, max(nrows - 1, 0));
+    const double yy = ((r + 0.5) * sy) * cy;
+    iyl = clampi(static_cast<int>(yy), 0, p.ny - 2);
+    fyl = yy - iyl;
+  }
+  __syncthreads();
+  auto line = [&](int j, int b) {  // table row j interpolated at column b's x
+    const double* t = tile + (j - ty0) * kSW + col[b];
+    return fma(t[1] - t[0], fx[b], t[0]);
+  };
+  double acc[kSCols], lc[kSCols], ln[kSCols], d[kSCols];
+#pragma unroll
+  for (int b = 0; b < kSCols; ++b) acc[b] = lc[b] = ln[b] = d[b] = 0.0;
+  int cur = -2;
+  for (int k = 0; k < nrows; ++k) {
+    const int iy = __builtin_amdgcn_readlane(iyl, k);
+    const double fy = readlane_f64(fyl, k);
+    if (iy != cur) {  // wave-uniform
+      if (iy == cur + 1) {
+#pragma unroll
+        for (int b = 0; b < kSCols; ++b) {
+          lc[b] = ln[b];
+          ln[b] = line(iy + 1, b);
+          d[b] = ln[b] - lc[b];
+        }
+      } else {
+#pragma unroll
+        for (int b = 0; b < kSCols; ++b) {
+          lc[b] = line(iy, b);
+          ln[b] = line(iy + 1, b);
+          d[b] = ln[b] - lc[b];
+        }
+      }
+      cur = iy;
+    }
+#pragma unroll
+    for (int b = 0; b < kSCols; ++b) acc[b] += fma_sv(d[b], fy, lc[b]);
+  }
+  double a = 0.0;
+#pragma unroll
+  for (int b = 0; b < kSCols; ++b) a += ok[b] ? acc[b] : 0.0;
+  const double s = block_sum<kB>(a, red) * (sx * sy);
   const unsigned bid = blockIdx.y * gridDim.x + blockIdx.x;
   if constexpr (!FUSED) {
     if (threadIdx.x == 0) partials[bid] = s;
@@ -230,25 +346,54 @@ void launch_outer_product(const double* v, int n, double* table, hipStream_t str
   MIINT_HIP(hipGetLastError());
 }
 
-// Tile edge for this launch: 128 unless that leaves fewer than 4 tiles per CU (1024).
-static int table2d_tile(const Table2DParams& p) {
-  const long t128 = static_cast<long>((p.gx + 127) / 128) * ((p.row1 - p.row0 + 127) / 128);
-  return t128 >= 1024 ? 128 : 64;
-}
+// Launch shape. Row stream when a workgroup's footprint (256 columns x 4 R rows) fits the
+// kSW x kSH LDS tile, with R (rows per wave) the largest of 32, 16, 8, 4 that fits and
+// still gives at least 512 workgroups (else the smallest that fits). Measured on 4096^2 and
+// 8192^2 fields and their 1/2, 1/4, 1/8 row slices: more rows per lane beat more
+// workgroups down to ~512 of them (profiles/r1/table2d_stream_rows.jsonl). Otherwise the
+// tile kernel, 128-sample tiles unless that leaves fewer than 4 per CU (1024).
+namespace {
+struct Table2DShape {
+  bool stream;
+  int rows_per_wave;  // stream
+  int tile;           // tile kernel: 128 or 64
+  dim3 grid;
+};
 
-static bool table2d_fits_lds(const Table2DParams& p, int tile) {
-  // cells spanned by `tile` samples (+2 for partial cells at both ends)
-  const double cells_x = tile * (p.X / p.gx) * ((p.nx - 1) / p.X) + 2.0;
-  const double cells_y = tile * (p.Y / p.gy) * ((p.ny - 1) / p.Y) + 2.0;
-  const int dim = tile == 128 ? lds_dim<128>() : lds_dim<64>();
-  return cells_x + 1.0 <= dim && cells_y + 1.0 <= dim;
+Table2DShape table2d_shape(const Table2DParams& p) {
+  const double step_x = (p.X / p.gx) * ((p.nx - 1) / p.X);  // cells per sample
+  const double step_y = (p.Y / p.gy) * ((p.ny - 1) / p.Y);
+  const int rows = p.row1 - p.row0;
+  const int gxs = (p.gx + kWave * kSCols - 1) / (kWave * kSCols);
+  Table2DShape sh{};
+  // cells spanned by n samples, + 2 for partial cells at both ends, + 1 for the +1 neighbour
+  auto span = [](int n, double step) { return n * step + 3.0; };
+  if (span(kWave * kSCols, step_x) <= kSW) {
+    for (int r : {32, 16, 8, 4}) {
+      if (span(4 * r, step_y) > kSH) continue;
+      const long nwg = static_cast<long>(gxs) * ((rows + 4 * r - 1) / (4 * r));
+      sh.stream = true;
+      sh.rows_per_wave = r;
+      sh.grid = dim3(gxs, (rows + 4 * r - 1) / (4 * r));
+      if (nwg >= 512) break;
+    }
+    if (sh.stream) return sh;
+  }
+  const long t128 = static_cast<long>((p.gx + 127) / 128) * ((rows + 127) / 128);
+  sh.tile = t128 >= 1024 ? 128 : 64;
+  sh.grid = dim3((p.gx + sh.tile - 1) / sh.tile, (rows + sh.tile - 1) / sh.tile);
+  return sh;
 }
+}  // namespace
 
 int table2d_grid(const Table2DParams& p) {
-  const int t = table2d_tile(p);
-  const int gxb = (p.gx + t - 1) / t;
-  const int gyb = (p.row1 - p.row0 + t - 1) / t;
-  return gxb * gyb;
+  const Table2DShape sh = table2d_shape(p);
+  return static_cast<int>(sh.grid.x * sh.grid.y);
+}
+
+const char* table2d_path(const Table2DParams& p) {
+  const Table2DShape sh = table2d_shape(p);
+  return sh.stream ? "stream" : "tile";
 }
 
 static void check_table2d(const Table2DParams& p) {
@@ -256,24 +401,18 @@ static void check_table2d(const Table2DParams& p) {
   MIINT_CHECK(p.row0 >= 0 && p.row1 <= p.gy && p.row0 < p.row1, "table2d row range");
 }
 
-static dim3 table2d_dims(const Table2DParams& p, int t) {
-  return dim3((p.gx + t - 1) / t, (p.row1 - p.row0 + t - 1) / t);
-}
-
 template <bool FUSED>
 static void launch_table2d(const Table2DParams& p, double* partials, unsigned* ticket,
                            double* out, hipStream_t stream) {
   check_table2d(p);
-  const int t = table2d_tile(p);
-  const dim3 grid = table2d_dims(p, t);
-  const bool lds = table2d_fits_lds(p, t);
-  if (t == 128) {
-    if (lds) table2d_kernel<128, true, FUSED><<<grid, kB, 0, stream>>>(p, partials, ticket, out);
-    else table2d_kernel<128, false, FUSED><<<grid, kB, 0, stream>>>(p, partials, ticket, out);
-  } else {
-    if (lds) table2d_kernel<64, true, FUSED><<<grid, kB, 0, stream>>>(p, partials, ticket, out);
-    else table2d_kernel<64, false, FUSED><<<grid, kB, 0, stream>>>(p, partials, ticket, out);
-  }
+  const Table2DShape sh = table2d_shape(p);
+  if (sh.stream)
+    table2d_stream_kernel<FUSED><<<sh.grid, kB, 0, stream>>>(p, sh.rows_per_wave, partials,
+                                                             ticket, out);
+  else if (sh.tile == 128)
+    table2d_kernel<128, FUSED><<<sh.grid, kB, 0, stream>>>(p, partials, ticket, out);
+  else
+    table2d_kernel<64, FUSED><<<sh.grid, kB, 0, stream>>>(p, partials, ticket, out);
   MIINT_HIP(hipGetLastError());
 }
 

@@ -272,6 +272,10 @@ PYBIND11_MODULE(_miint, m) {
     Table2DParams p{nullptr, nx, ny, X, Y, gx, gy, row0, row1};
     return table2d_grid(p);
   });
+  m.def("table2d_path", [](int nx, int ny, double X, double Y, int gx, int gy, int row0, int row1) {
+    Table2DParams p{nullptr, nx, ny, X, Y, gx, gy, row0, row1};
+    return std::string(table2d_path(p));
+  });
   m.def("launch_table2d_partials", [](uintptr_t table, int nx, int ny, double X, double Y, int gx,
                                       int gy, int row0, int row1, uintptr_t partials, uintptr_t s) {
     Table2DParams p{ptr<const double>(table), nx, ny, X, Y, gx, gy, row0, row1};

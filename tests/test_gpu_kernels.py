@@ -455,17 +455,38 @@ def _bilinear_midpoint_sum(T, X, Y, gx, gy):
     return float((top + (bot - top) * fy).sum()) * (X / gx) * (Y / gy)
 
 
-@pytest.mark.parametrize("shape,grid", [((37, 53), (300, 211)),      # LDS-tiled path
-                                        ((1801, 1801), (64, 96))])   # coarse: global path
-def test_table2d_general_table_vs_torch(cuda, shape, grid):
-    """A random (non-separable) table: the 2-D kernel is a general bilinear integrator."""
+@pytest.mark.parametrize("shape,grid,path", [
+    ((37, 53), (300, 211), "stream"),         # partial workgroups in x and y
+    ((1801, 1801), (4100, 4099), "stream"),   # rows per wave 16, odd edges
+    ((37, 53), (300, 8), "tile"),             # rows coarser than the stream footprint
+    ((1801, 1801), (64, 96), "tile"),         # coarse: table read from global memory
+])
+def test_table2d_general_table_vs_torch(native, cuda, shape, grid, path):
+    """A random (non-separable) table: the 2-D kernels are general bilinear integrators.
+    Each launch shape is pinned to the kernel it is meant to exercise."""
     g = torch.Generator(device="cpu").manual_seed(shape[0])
     T = torch.rand(shape, generator=g, dtype=torch.float64).cuda()
     X, Y = 3.7, 2.1
+    assert native.table2d_path(shape[1], shape[0], X, Y, grid[0], grid[1], 0, grid[1]) == path
     got = float(kernels.table2d(T, X, Y, grid[0], grid[1]).item())
     assert got == pytest.approx(_bilinear_midpoint_sum(T, X, Y, grid[0], grid[1]), rel=1e-13)
     unfused = float(kernels.table2d(T, X, Y, grid[0], grid[1], fused=False).item())
     assert got == unfused  # same partials, same index-ordered final sum
+
+
+def test_table2d_stream_row_split(native, cuda):
+    """Row slices of a 4096^2 field at odd boundaries (rows per wave 16 / 8 / 4 by slice
+    height) add up to the whole."""
+    v = torch.as_tensor(fixtures.profile_table(), device="cuda")
+    T = kernels.outer_product(v)
+    g = 4096
+    whole = float(kernels.table2d(T, 1800.0, 1800.0, g, g).item())
+    cuts = [0, 1000, 2731, 3500, 3777, 4096]
+    parts = []
+    for r0, r1 in zip(cuts, cuts[1:]):
+        assert native.table2d_path(1801, 1801, 1800.0, 1800.0, g, g, r0, r1) == "stream"
+        parts.append(float(kernels.table2d(T, 1800.0, 1800.0, g, g, r0, r1).item()))
+    assert math.fsum(parts) == pytest.approx(whole, rel=1e-13)
 
 
 def test_table2d_row_split(cuda):

@@ -4,8 +4,9 @@
 //   ./miint bench [--integrand pi4] [--n 1e9] [--dtype fp64] [--rule left] [--iters 200]
 //                 [--gpus G] [--div series|ieee] [--unfused] [--no-graph]      (JSON lines)
 //   ./miint sweep [--gpus G]     N in {1e6,1e9,1e10} x dtype {fp64,fp32} x integrand
-//   ./miint table2d [--grid 4096] [--gpus G] [--slice R/W]   2-D velocity-field integral
-//                                                           (BASELINE #5)
+//   ./miint table2d [--grid 4096] [--gpus G] [--slice R/W] [--no-graph]
+//                                2-D velocity-field integral (BASELINE #5); timed as
+//                                replays of a hipGraph of 32 integrations
 //   ./miint selfcheck            every SURVEY §6.1 oracle on the GPU, exit 1 on mismatch
 //   ./miint comm [--gpus G] [--max-bytes 144e6] [--iters 20]
 //                                RCCL allreduce / allgather / broadcast sweep, 8 B .. 144 MB
@@ -246,7 +247,7 @@ int main(int argc, char** argv) {
       cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
         Table2DPlan plan(c, dev, comm);
         const double v = plan.run();
-        const double t = plan.time(iters);
+        const double t = plan.time(iters, graphs);
         std::lock_guard<std::mutex> g(mu);
         if (rank == topo.rank0) value = v;
         if (t > ms) ms = t;

@@ -36,8 +36,11 @@ class Table2DPlan {
   // One integration: one fused kernel (result straight into pinned host memory on one
   // rank) or kernel -> RCCL all-reduce -> 8-byte copy. Returns the value.
   double run();
-  // `iters` back-to-back integrations; returns device ms per integration.
-  double time(int iters);
+  // `iters` back-to-back integrations; returns device ms per integration. With graphs,
+  // kGraphSteps integrations are captured once into a hipGraph and replayed (iters rounded
+  // up to whole replays): one launch per kGraphSteps instead of one per integration.
+  double time(int iters, bool graphs = true);
+  static constexpr int kGraphSteps = 32;
   int row0() const { return row0_; }
   int row1() const { return row1_; }
 
@@ -53,6 +56,7 @@ class Table2DPlan {
   DeviceBuffer<unsigned int> ticket_;
   PinnedBuffer<double> host_;
   Event e0_, e1_;
+  Graph graph_;
 };
 
 // Host oracle for the midpoint sum on a g x g grid: (sum_j v(x_j) dx)^2.

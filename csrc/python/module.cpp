@@ -324,7 +324,8 @@ PYBIND11_MODULE(_miint, m) {
            py::arg("grid") = 4096, py::arg("extent") = 1800.0, py::arg("device") = 0,
            py::arg("comm") = nullptr, py::keep_alive<1, 5>())
       .def("run", &Table2DPlan::run, py::call_guard<py::gil_scoped_release>())
-      .def("time", &Table2DPlan::time, py::call_guard<py::gil_scoped_release>())
+      .def("time", &Table2DPlan::time, py::arg("iters"), py::arg("graphs") = true,
+           py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("row0", &Table2DPlan::row0)
       .def_property_readonly("row1", &Table2DPlan::row1);
   m.def("table2d_oracle", &table2d_oracle, py::arg("grid"), py::arg("extent") = 1800.0);

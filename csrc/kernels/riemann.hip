@@ -491,8 +491,11 @@ void dispatch(const RiemannParams& p, DType dtype, DivMode m, A&&... a) {
       if (m == DivMode::kSeries) Op<DivMode::kSeries, Sin>::run(a...);
       else Op<DivMode::kIeee, Sin>::run(a...);
       return;
-    case Integrand::kPoly:  // coefficient bucket: 4, 8 or 16 (zero-padded)
+    case Integrand::kPoly:  // coefficient bucket (zero-padded): series 4, 6, 7, 8; Horner 4, 8, 16
+      // (degree 5 and 6 get exact buckets: a padded degree-7 pair costs 11 VALU instead of 10)
       if (m == DivMode::kSeries && p.ncoef <= 4) Op<DivMode::kSeries, Poly<4>>::run(a...);
+      else if (m == DivMode::kSeries && p.ncoef <= 6) Op<DivMode::kSeries, Poly<6>>::run(a...);
+      else if (m == DivMode::kSeries && p.ncoef == 7) Op<DivMode::kSeries, Poly<7>>::run(a...);
       else if (m == DivMode::kSeries && p.ncoef <= 8) Op<DivMode::kSeries, Poly<8>>::run(a...);
       else if (p.ncoef <= 4) Op<DivMode::kIeee, Poly<4>>::run(a...);
       else if (p.ncoef <= 8) Op<DivMode::kIeee, Poly<8>>::run(a...);

@@ -147,7 +147,7 @@ def test_train_series_matches_direct(cuda):
     assert a == pytest.approx(spec.analytic(), rel=1e-12)
 
 
-@pytest.mark.parametrize("degree", [3, 6, 7])
+@pytest.mark.parametrize("degree", [3, 4, 5, 6, 7])  # buckets 4, 6, 6, 7, 8
 @pytest.mark.parametrize("n", [10**9, 1_000_003])
 def test_poly_taylor_pairs_match_horner(cuda, degree, n):
     """Random-coefficient polynomials: the Taylor-pair tiles (shift to each 32-sample

@@ -1,0 +1,16 @@
+#!/usr/bin/env bash
+# bench.py for every integrand and path, one JSON line each (profiles/r1/bench_all_integrands.jsonl).
+# Each run under its own time limit; stops at the first failure.
+set -euo pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+run() { timeout -k 10 120 python bench.py "$@" | grep '^{'; }
+run
+run --rule mid
+run --div ieee
+run --dtype fp32
+run --dtype fp32 --rule mid
+run --samples 1e10 --steps 100
+run --integrand sin
+run --integrand train
+run --integrand table
+run --integrand poly

@@ -176,8 +176,9 @@ __global__ __launch_bounds__(kB) void table2d_kernel(Table2DParams p, double* pa
 //   v = fma(D, fy, Lc),  acc += v                       (2 VALU, fy an SGPR operand)
 // — the same value the tile kernel forms (top + fy (bot - top)) — and only when iy moves
 // (a scalar compare and branch, once per ~2.3 sample rows at 4096^2) does the lane read
-// one ds_read2_b64 for the new line. The tile kernel reads 32 B of LDS and spends ~15 VALU
-// per sample; this one reads ~7 B and ~4 VALU.
+// one ds_read2_b64 for the new line. The LDS tile kernel this replaced read 32 B of LDS and
+// spent ~15 VALU per sample; this loop reads ~7 B and ~4 VALU (~11 VALU per sample in all,
+// counting staging, column setup and the hand-off at 64 samples per lane).
 constexpr int kSCols = 4;                 // columns per lane: a workgroup spans 256 columns
 constexpr int kSW = kWave * kSCols / 2;   // LDS footprint width (cells), 128
 constexpr int kSH = 32;                   // LDS footprint height (cells)

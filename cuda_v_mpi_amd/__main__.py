@@ -7,6 +7,7 @@ SURVEY §2.6) on top of the Python API, and adds JSON output:
     cintegrate  train distance from the profile (cintegrate.cu)  [--parity --sp 32 --sm 2]
     trainscan   two-phase prefix scan (4main.c)                   [--parity --algo lookback]
     integrate   any integrand, JSON result                        [--integrand --n --rule ...]
+    table2d     2-D velocity field v(x) v(y), bilinear, JSON      [--grid 4096 --iters 100]
     oracle      print every SURVEY §6.1 oracle value (CPU only)
     info        devices and build
 
@@ -107,6 +108,39 @@ def cmd_integrate(a) -> int:
     return 0
 
 
+def cmd_table2d(a) -> int:
+    """BASELINE #5: the separable field v(x) v(y) over [0, 1800]^2 on a grid x grid midpoint
+    grid, bilinear interpolation of the 1801^2 outer-product table; ranks split the rows."""
+    from ._native import native
+
+    ctx = _ctx()
+    m = native()
+    want = m.table2d_oracle(a.grid)
+    rec = {"program": "table2d", "grid": a.grid, "gpus": ctx.world, "backend": a.backend}
+    if a.backend == "cpu":
+        import torch
+
+        from .ops.kernels import table2d_reference
+        from .utils import fixtures
+
+        v = torch.as_tensor(fixtures.profile_table(), dtype=torch.float64)
+        rec["result"] = table2d_reference(torch.outer(v, v), 1800.0, 1800.0, a.grid, a.grid)
+    else:
+        from .parallel.dist import native_comm
+
+        comm = native_comm(ctx) if ctx.world > 1 else None
+        plan = m.Table2DPlan(a.grid, 1800.0, ctx.device, comm)
+        rec["result"] = plan.run()
+        rec["ms_per_integration"] = plan.time(a.iters, True)
+        rec["samples_per_s"] = a.grid * a.grid / (rec["ms_per_integration"] * 1e-3)
+    rec["midpoint_oracle"] = want
+    rec["rel_err_vs_oracle"] = abs(rec["result"] - want) / want
+    if ctx.is_root:
+        print(json.dumps(rec))
+    ctx.destroy()
+    return 0
+
+
 def cmd_oracle(a) -> int:
     from ._native import native
 
@@ -168,11 +202,16 @@ def main(argv=None) -> int:
     t.add_argument("--algo", default="fused", choices=["fused", "onepass", "lookback"])
     t.add_argument("--json", action="store_true")
     common(sub.add_parser("integrate"), integrand="pi4")
+    t2 = sub.add_parser("table2d")
+    t2.add_argument("--grid", type=int, default=4096)
+    t2.add_argument("--iters", type=int, default=100)
+    t2.add_argument("--backend", default="hip", choices=["hip", "cpu"])
     sub.add_parser("oracle")
     sub.add_parser("info")
     a = p.parse_args(argv)
     return {"riemann": cmd_riemann, "cintegrate": cmd_cintegrate, "trainscan": cmd_trainscan,
-            "integrate": cmd_integrate, "oracle": cmd_oracle, "info": cmd_info}[a.cmd](a)
+            "integrate": cmd_integrate, "table2d": cmd_table2d, "oracle": cmd_oracle,
+            "info": cmd_info}[a.cmd](a)
 
 
 if __name__ == "__main__":

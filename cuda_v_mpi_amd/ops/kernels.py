@@ -276,6 +276,29 @@ def table2d(table: torch.Tensor, X: float, Y: float, gx: int, gy: int, row0: int
     return out
 
 
+def table2d_reference(table: torch.Tensor, X: float, Y: float, gx: int, gy: int,
+                      row0: int = 0, row1: int | None = None, rows_per_chunk: int = 256) -> float:
+    """Plain torch fp64 form of `table2d` (any device, CPU included): the same midpoint
+    samples and bilinear blend, summed in row chunks of at most rows_per_chunk x gx."""
+    ny, nx = table.shape
+    row1 = gy if row1 is None else row1
+    t = table.to(torch.float64)
+    xs = (torch.arange(gx, dtype=torch.float64, device=t.device) + 0.5) * (X / gx) * ((nx - 1) / X)
+    ix = xs.long().clamp(0, nx - 2)
+    fx = (xs - ix).unsqueeze(0)
+    total = 0.0
+    for r in range(row0, row1, rows_per_chunk):
+        rows = torch.arange(r, min(r + rows_per_chunk, row1), dtype=torch.float64, device=t.device)
+        ys = (rows + 0.5) * (Y / gy) * ((ny - 1) / Y)
+        iy = ys.long().clamp(0, ny - 2)
+        fy = (ys - iy).unsqueeze(1)
+        lo, hi = t[iy], t[iy + 1]
+        top = lo[:, ix] + (lo[:, ix + 1] - lo[:, ix]) * fx
+        bot = hi[:, ix] + (hi[:, ix + 1] - hi[:, ix]) * fx
+        total += float((top + (bot - top) * fy).sum())
+    return total * (X / gx) * (Y / gy)
+
+
 def wave_ops(x: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
     """(per-wave sums, per-wave inclusive scans) via the DPP primitives."""
     f32 = x.dtype == torch.float32

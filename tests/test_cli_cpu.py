@@ -31,6 +31,15 @@ def test_python_cli_cintegrate_parity_cpu():
     assert p.stdout.strip().splitlines()[1] == "final distance is:121999.800663"
 
 
+def test_python_cli_table2d_cpu_matches_oracle():
+    """The torch reference form of the 2-D field integral against the separable host oracle
+    (sum_j v(x_j) dx)^2."""
+    p = _py("table2d", "--backend", "cpu", "--grid", "300")
+    assert p.returncode == 0, p.stderr
+    js = json.loads(p.stdout.strip().splitlines()[-1])
+    assert js["grid"] == 300 and js["rel_err_vs_oracle"] < 1e-13
+
+
 def test_python_cli_oracle():
     p = _py("oracle")
     assert p.returncode == 0, p.stderr

@@ -227,6 +227,15 @@ def test_cli_jsonl_appends_run_records(cli_built, tmp_path):
     assert rows[3]["distance"] == pytest.approx(122000.004, abs=1e-6)
 
 
+def test_python_cli_table2d_hip(cli_built):
+    p = _run(["python", "-m", "cuda_v_mpi_amd", "table2d", "--grid", "4096", "--iters", "32"],
+             env={"PYTHONPATH": REPO})
+    assert p.returncode == 0, p.stderr
+    js = json.loads(p.stdout.strip().splitlines()[-1])
+    assert js["backend"] == "hip" and js["rel_err_vs_oracle"] < 1e-13
+    assert js["ms_per_integration"] > 0
+
+
 def test_cli_comm_sweep(cli_built):
     """miint comm: one-rank RCCL sweep of the three collectives; every size reports a
     positive time, and the broadcast of 1 MB moves at a finite rate."""

@@ -34,10 +34,10 @@ def _elapsed() -> float:
     return time.time() - psutil.Process().create_time()
 
 
-def _ctx():
+def _ctx(backend=None):
     from .parallel import dist as mdist
 
-    return mdist.init()
+    return mdist.init(backend=backend)
 
 
 def cmd_riemann(a) -> int:
@@ -113,7 +113,7 @@ def cmd_table2d(a) -> int:
     grid, bilinear interpolation of the 1801^2 outer-product table; ranks split the rows."""
     from ._native import native
 
-    ctx = _ctx()
+    ctx = _ctx("gloo" if a.backend == "cpu" else None)  # cpu: host tensors, host collective
     m = native()
     want = m.table2d_oracle(a.grid)
     rec = {"program": "table2d", "grid": a.grid, "gpus": ctx.world, "backend": a.backend}
@@ -123,8 +123,12 @@ def cmd_table2d(a) -> int:
         from .ops.kernels import table2d_reference
         from .utils import fixtures
 
+        from .parallel.decomposition import rank_slice
+
         v = torch.as_tensor(fixtures.profile_table(), dtype=torch.float64)
-        rec["result"] = table2d_reference(torch.outer(v, v), 1800.0, 1800.0, a.grid, a.grid)
+        b, c = rank_slice(a.grid, ctx.rank, ctx.world)  # this rank's sample rows
+        part = table2d_reference(torch.outer(v, v), 1800.0, 1800.0, a.grid, a.grid, b, b + c)
+        rec["result"] = float(ctx.all_reduce_sum(torch.tensor([part], dtype=torch.float64))[0])
     else:
         from .parallel.dist import native_comm
 

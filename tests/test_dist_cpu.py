@@ -105,3 +105,24 @@ def test_cintegrate_coverage():
     assert decomposition.coverage_seconds(60) == 1800
     ch = decomposition.cintegrate_chunks(32, 2)
     assert ch[1][0] - ch[0][0] == 280_000
+
+
+def test_torchrun_table2d_cpu_rows_split_over_ranks():
+    """`python -m cuda_v_mpi_amd table2d` under torchrun (3 gloo ranks on the CPU): each rank
+    integrates its row slice (rows not divisible by 3) and the all-reduced sum is the whole
+    field's midpoint sum."""
+    import json
+    import subprocess
+    import sys
+
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node=3", "--master-addr", "127.0.0.1",
+                        f"--master-port={_free_port()}", "-m", "cuda_v_mpi_amd", "table2d",
+                        "--backend", "cpu", "--grid", "301"],
+                       cwd=repo, capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, PYTHONPATH=repo))
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    rows = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(rows) == 1 and rows[0]["gpus"] == 3  # rank 0 prints
+    assert rows[0]["rel_err_vs_oracle"] < 1e-13

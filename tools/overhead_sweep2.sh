@@ -1,4 +1,6 @@
 #!/usr/bin/env bash
+# bench.py at small N: grid size sweep at 1e6 and 1e8 samples, then the unfused and no-graph
+# launch variants. One JSON line per run.
 set -euo pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 run() { timeout -k 10 120 python bench.py "$@" 2>/dev/null | grep '^{"metric"' | python3 -c "

@@ -236,6 +236,30 @@ def test_python_cli_table2d_hip(cli_built):
     assert js["ms_per_integration"] > 0
 
 
+def test_bench_two_ranks_share_one_gpu_over_gloo():
+    """bench.py in the driver's launch shape (torch.distributed.run, 2 processes) on one
+    GPU: torch.distributed over gloo, kernels on each rank's torch stream and one
+    all_reduce per step (TorchStepper). Checks rank slicing, MAX-over-ranks timing and the
+    rank-0-only JSON line; not speed (two processes time-share the card)."""
+    import socket
+    import sys
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    p = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+              "--master-addr", "127.0.0.1", f"--master-port={port}",
+              os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo", "--comm",
+              "torch", "--steps", "24", "--warmup", "4", "--settle-ms", "0"],
+             env={"PYTHONPATH": REPO})
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-2000:]
+    rows = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(rows) == 1
+    js = rows[0]
+    assert js["verified"] and js["n_gpus"] == 2 and js["config"]["comm"] == "torch"
+    assert js["config"]["N"] == 2 * 10**9 and js["config"]["n_per_gpu"] == 10**9
+
+
 def test_cli_comm_sweep(cli_built):
     """miint comm: one-rank RCCL sweep of the three collectives; every size reports a
     positive time, and the broadcast of 1 MB moves at a finite rate."""

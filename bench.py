@@ -66,6 +66,7 @@ def parse() -> argparse.Namespace:
     p.add_argument("--force-collective", action="store_true",
                    help="run the RCCL all-reduce stage even on 1 GPU (tests the multi-GPU graph)")
     p.add_argument("--verbose", action="store_true")
+    p.add_argument("--jsonl", default="", help="also append the JSON line to this file")
     return p.parse_args()
 
 
@@ -203,6 +204,9 @@ def main() -> int:
             },
         }
         print(json.dumps(out), flush=True)
+        if args.jsonl:
+            with open(args.jsonl, "a") as f:
+                f.write(json.dumps(out) + "\n")
     ctx.destroy()
     return 0 if ok else 1
 

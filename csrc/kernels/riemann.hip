@@ -119,16 +119,19 @@ struct Pi4F32 : TileDefaults<Pi4F32> {
     }
   }
 
-  // Default series path, midpoint-anchored, 128-sample tiles of four 32-sample sub-tiles
-  // (centres at -48, -16, 16, 48 steps; e_c = e_m + c0 A + c0^2 B, A' = A + 2 c0 B: one seed
-  // per 128 samples; 64-sample tiles of two sub-tiles spent ~29 VALU of seed, coordinate and
-  // fp64 fold per 80 of pair work). The pair residuals (e_{+k}, e_{-k}) = c_k + (k, -k) * A'
+  // Default series path, midpoint-anchored, 192-sample tiles of six 32-sample sub-tiles
+  // (centres at -80, -48, ..., 48, 80 steps; e_c = e_m + c0 A + c0^2 B, A' = A + 2 c0 B: one
+  // seed per 192 samples). Tile length vs overhead: 64-sample tiles spent ~29 VALU of seed,
+  // coordinate and fp64 fold per 80 of pair work; at N = 1e9 on 2048 x 256 lanes, 128 / 192 /
+  // 320-sample tiles ran 2.34e13 / 2.44e13 / 2.48e13 subint/s, and 320 doubled the
+  // midpoint-rule error (4.1e-11 vs 2.1e-11: wider sub-tile offsets), so 192. (256 would
+  // leave 7.45 tiles per lane, i.e. 8 on the busiest.) The pair residuals (e_{+k}, e_{-k}) = c_k + (k, -k) * A'
   // are one v_pk_fma_f32 (op_sel broadcasts c_k), summed by one v_pk_add_f32, and the shared
   // c_k of TWO consecutive pairs advance together by one v_pk_fma_f32 with the exact steps
   // (k_{j+2}^2 - k_j^2, k_{j+3}^2 - k_{j+1}^2) = (4j+6, 4j+10) times B: 1.25 VALU per sample.
   // In fp32 the e^2 term (< 3e-16) is far below the format's 6e-8 and is not carried.
   static constexpr int kSubLen = 32;
-  static constexpr int kSubs = 4;
+  static constexpr int kSubs = 6;
   template <DivMode M>
   __host__ __device__ static constexpr int tile_len() {
     return M == DivMode::kSeries ? kSubs * kSubLen : 32;
@@ -140,7 +143,7 @@ struct Pi4F32 : TileDefaults<Pi4F32> {
   template <int UU, DivMode M>
   __device__ __forceinline__ double tile_acc(double xmd, double h, double acc) const {
     if constexpr (M == DivMode::kSeries) {
-      static_assert(UU == kSubs * kSubLen, "fp32 series tiles are four 32-sample sub-tiles");
+      static_assert(UU == kSubs * kSubLen, "fp32 series tiles are kSubs 32-sample sub-tiles");
       const float xm = static_cast<float>(xmd);
       const float hf = static_cast<float>(h);
       const float dm = fmaf(xm, xm, 1.0f);
@@ -153,7 +156,7 @@ struct Pi4F32 : TileDefaults<Pi4F32> {
       const f32x2 aa = {a, a};
       const f32x2 emv = {em, em};
       // Sub-tile centre residuals and slopes, two sub-tiles per packed op:
-      // (e_c, e_c') = c0 (c0 B + A) + e_m and (A', A'') = 2 c0 B + A for c0 = (-48, -16), (16, 48).
+      // (e_c, e_c') = c0 (c0 B + A) + e_m and (A', A'') = 2 c0 B + A for c0 pairs (-80, -48), ...
       f32x2 ecs[kSubs / 2], aqs[kSubs / 2];
 #pragma unroll
       for (int p2 = 0; p2 < kSubs / 2; ++p2) {

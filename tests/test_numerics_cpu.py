@@ -1,8 +1,8 @@
 """Host emulations of device numerics (CPU only).
 
-The fp32 Pi4 path (csrc/kernels/riemann.hip, Pi4F32::tile_acc) evaluates each 128-sample
+The fp32 Pi4 path (csrc/kernels/riemann.hip, Pi4F32::tile_acc) evaluates each 192-sample
 tile as s (U + sum e) from an fp32 seed s ~ 1/d(x_m) and fp32 residuals e. This emulates the
-tile with numpy float32 arithmetic: folding s (U + sum e) in fp32 drops the seed's own
+tile with numpy float32 arithmetic (at 128 samples, the length it had when this was found): folding s (U + sum e) in fp32 drops the seed's own
 correction (U + sum e rounds at ulp(128) = 1.5e-5 while |sum e| ~ U |e_m| ~ 4e-6) and biases
 the integral by ~-8e-9 relative, which is what the GPU printed (3.1415926288, |err| 2.5e-8 at
 N = 1e9) before the fold moved to fp64 (|err| 1.0e-9 = h, the left rule's truncation).

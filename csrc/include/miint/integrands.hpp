@@ -67,14 +67,15 @@ struct TileDefaults {
 // g_{+-k} = c_k +- k A. c_k is formed directly with one fma from an SGPR k^2 (no running
 // recurrence: increments of ~1e-17 would be lost against ulp(1/2)). Per PAIR of samples:
 // 1 fma for c_k, 2 for g, 2 accumulations = 2.5 VALU per sample.
-// A 128-sample tile is 4 sub-tiles of 32 whose centres sit at c0 = -48, -16, 16, 48 steps
-// from x_m; re-expanding the exact quadratic there gives e_c = e_m + c0 A + c0^2 B and
+// A 192-sample tile is 6 sub-tiles of 32 whose centres sit at c0 = -80, -48, ..., 48, 80
+// steps from x_m; re-expanding the exact quadratic there gives e_c = e_m + c0 A + c0^2 B and
 // slope A' = A + 2 c0 B (3 fma per sub-tile, against ~10 for a fresh seed). The 16 pair
-// constants k_j and k_j^2 - kMeanK2 take 23 SGPR pairs plus 9 VGPR pairs: 89 SGPRs
-// (96 allocated) and 60 VGPRs, 8 resident workgroups per CU.
-// Measured (gfx950 .s, tools/isa_count.py): 342 VALU per 128-sample tile = 2.67 per sample
-// (8 sub-tiles of 16: 354 = 2.77; 64-sample tiles with a Newton step: 183 per 64 = 2.86;
-// the first form, t += e; t = fma(e, e, t) with one seed per 32 samples: 127 per 32 = 3.97).
+// constants k_j and k_j^2 - kMeanK2 and the centre tables fill 96 SGPRs, 11 of the
+// k_j^2 - kMeanK2 sit in VGPRs: 64 VGPRs, 8 resident workgroups per CU.
+// Measured (gfx950 .s, tools/isa_count.py): 508 VALU per 192-sample tile = 2.65 per sample
+// (128-sample tiles of 4: 342 = 2.67; 8 sub-tiles of 16: 354 per 128 = 2.77; 64-sample
+// tiles with a Newton step: 183 per 64 = 2.86; the first form, t += e; t = fma(e, e, t) with
+// one seed per 32 samples: 127 per 32 = 3.97).
 //
 // Accuracy: every sample still gets its own residual and its own contribution. Per point,
 // g is rounded at ulp(1/2) scale: <= 5 ulp vs IEEE division, 92 % within 1 ulp, 99.5 %
@@ -84,8 +85,11 @@ struct Pi4 : TileDefaults<Pi4> {
   static constexpr double kScale = 4.0;
   static constexpr int kPairs = 16;                 // sample pairs per sub-tile
   static constexpr int kSub = 2 * kPairs;           // 32 samples per sub-tile
-  static constexpr int kSubs = 4;                   // sub-tiles per series tile
-  static constexpr int kSeriesTile = kSub * kSubs;  // 128 samples per seed
+  // Sub-tiles per series tile: 6 (192 samples per seed; 128-sample tiles of 4 ran 342 VALU
+  // per 128 samples, these 508 per 192: 1.35e13 -> 1.36e13 subint/s at N = 1e9, and 1e9 /
+  // 192 deals 9.93 tiles per lane of the 2048 x 256 grid, as even as 128's 14.9).
+  static constexpr int kSubs = 6;
+  static constexpr int kSeriesTile = kSub * kSubs;  // 192 samples per seed
 
   template <DivMode M>
   __host__ __device__ static constexpr int tile_len() {
@@ -101,10 +105,10 @@ struct Pi4 : TileDefaults<Pi4> {
   // per SIMD), loaded once per kernel.
   // Mean of k_j^2 over a sub-tile's pairs: sum_j (j + 1/2)^2 / 16 = 1364/16.
   static constexpr double kMeanK2 = 85.25;
-  static constexpr int kPk2Sgpr = 7;  // pk2[j < 7] in SGPRs: fills the 96 (89 + 6 reserved)
+  static constexpr int kPk2Sgpr = 5;  // pk2[j < 5] in SGPRs: with the 6-sub-tile tables fills the 96
   double pk[kPairs];         // k_j = j + 1/2                          (SGPR)
   double pk2[kPairs];        // k_j^2 - kMeanK2                        (VGPR)
-  double pc[kSubs / 2];      // |sub-tile centre offset| c0: 16, 48    (SGPR)
+  double pc[kSubs / 2];      // |sub-tile centre offset| c0: 16, 48, 80 (SGPR)
   double pcm[kSubs / 2];     // c0 + kMeanK2 / c0                      (SGPR)
   double c15;                // 3/2 (e_m + 1/2 = 3/2 - d_m s in one fma)
 

@@ -19,7 +19,7 @@ enum class DType : int { kF64 = 0, kF32 = 1 };
 // Tile (unroll) size of the Riemann kernels: U consecutive samples per lane per step.
 constexpr int kRiemannTile = 32;     // default samples per lane tile (Pi4 series: 64)
 constexpr int kRiemannBlock = 256;
-constexpr int kSeriesHalfSpan = 64;  // max |sample offset| from a Pi4 series seed, in steps
+constexpr int kSeriesHalfSpan = 96;  // max |sample offset| from a Pi4 series seed, in steps
 
 constexpr int kDirectHalfSpan = 16;  // the same for kSeriesDirect's 32-sample tiles
 
@@ -27,8 +27,8 @@ constexpr int kDirectHalfSpan = 16;  // the same for kSeriesDirect's 32-sample t
 inline bool series_ok(double h) { return kSeriesHalfSpan * (h < 0 ? -h : h) <= 2e-6; }
 inline bool direct_ok(double h) { return kDirectHalfSpan * (h < 0 ? -h : h) <= 2e-6; }
 
-// Division mode actually used for step h: a step too coarse for the 128-sample series tiles
-// (N < 3.2e7 on [0, 1]) still fits the 32-sample kSeriesDirect tiles down to N = 8e6 (5 VALU
+// Division mode actually used for step h: a step too coarse for the 192-sample series tiles
+// (N < 4.8e7 on [0, 1]) still fits the 32-sample kSeriesDirect tiles down to N = 8e6 (5 VALU
 // per sample against ~14 for IEEE division); coarser steps use IEEE division.
 inline DivMode effective_div(DivMode d, double h) {
   if (d == DivMode::kIeee) return d;
@@ -47,7 +47,7 @@ inline DivMode effective_div(DivMode d, double h, Integrand f) {
 
 constexpr int kPolySeriesMaxCoeffs = 8;  // polynomials up to degree 7 have a series path
 
-// With the dtype (the fp32 path has one series form, 128-sample tiles of first order, and
+// With the dtype (the fp32 path has one series form, 192-sample tiles of first order, and
 // otherwise IEEE division) and the polynomial's coefficient count (Taylor-pair tiles for up
 // to kPolySeriesMaxCoeffs coefficients, exact for any h; Horner per sample otherwise).
 inline DivMode effective_div(DivMode d, double h, Integrand f, DType t, int ncoef = 0) {

@@ -194,6 +194,11 @@ struct Pi4F32 : TileDefaults<Pi4F32> {
     }
   }
 };
+// The host's series validity check (series_ok: kSeriesHalfSpan * h <= 2e-6) must bound the
+// farthest sample offset of both Pi4 series tiles.
+static_assert(Pi4::kSeriesTile / 2 == kSeriesHalfSpan &&
+                  Pi4F32::kSubs * Pi4F32::kSubLen / 2 == kSeriesHalfSpan,
+              "kSeriesHalfSpan must be half the Pi4 series tile length");
 
 // ---------------------------------------------------------------------------- functor makers
 // Each integrand gets its own kernel instantiation (own register allocation); only the

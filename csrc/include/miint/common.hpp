@@ -72,7 +72,7 @@ inline double rule_offset(Rule r) {
 constexpr int kMaxPolyCoeffs = 16;
 
 // Everything a Riemann kernel needs, passed by value (kernarg segment, lands in SGPRs).
-constexpr int kSinTrig = 24;  // 8 x {cos, sin}(k_j h) + 4 x {cos, sin}(c0 h), c0 = 8, 24, 40, 56
+constexpr int kSinTrig = 28;  // 8 x {cos, sin}(k_j h) + 6 x {cos, sin}(c0 h), c0 = 8, 24, ..., 88
 
 struct RiemannParams {
   double a;             // integration lower bound
@@ -89,7 +89,7 @@ struct RiemannParams {
   double p0, p1;        // integrand parameters (train: ts, vs)
   // Sin series path, filled on the host by the launchers (long double): trig[j] = cos(k_j h),
   // trig[8 + j] = sin(k_j h) for k_j = j + 1/2 (j < 8), then cos(c0 h), sin(c0 h) for the
-  // sub-tile centres c0 = 8, 24, 40, 56 (integrands.hpp, struct AngleSeries)
+  // sub-tile centres c0 = 8, 24, ..., 88 (integrands.hpp, struct AngleSeries)
   double trig[kSinTrig];
 };
 

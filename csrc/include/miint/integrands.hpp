@@ -301,8 +301,8 @@ __device__ __forceinline__ void tile_sincos(double th, double& S, double& C) {
 
 // ------------------------------------------------------------------ sin / cos by angle addition
 // Shared series path of Sin and TrainVel (both evaluate sin or cos of theta = w x):
-// one sin/cos pair per 128-sample tile at the midpoint theta_m (tile_sincos), re-centred to
-// eight 16-sample sub-tiles (centres theta_m + c0 delta, c0 = +-8, +-24, +-40, +-56;
+// one sin/cos pair per tile at the midpoint theta_m (tile_sincos), re-centred to Subs
+// 16-sample sub-tiles (centres theta_m + c0 delta, c0 = +-8, +-24, +-40, ...;
 // delta = w h), then every sample by the exact angle-addition formula
 //   sin(theta_c +- k delta) = S_c cos(k delta) +- C_c sin(k delta)
 //   cos(theta_c +- k delta) = C_c cos(k delta) -+ S_c sin(k delta)
@@ -312,14 +312,18 @@ __device__ __forceinline__ void tile_sincos(double th, double& S, double& C) {
 // seed and the 4-op re-centring per sub-tile add the rest (388 VALU per 128-sample tile).
 // Every centre comes straight from the tile midpoint (one rounding), so the per-point error
 // does not grow with the tile. No truncation (valid for any h).
+// Subs sub-tiles per seed: Sin runs 12 (192-sample tiles, 1.20e13 -> 1.25e13 subint/s over
+// 8), TrainVel keeps 8 (12 measured 1.18e13 -> 1.15e13). The host fills the centre table for
+// the largest Subs; a smaller Subs reads its prefix (the same c0 = 8, 24, ... values).
+template <int Subs>
 struct AngleSeries {
   static constexpr int kPairs = 8;
   static constexpr int kSub = 2 * kPairs;
-  static constexpr int kSubs = 8;
+  static constexpr int kSubs = Subs;
   static constexpr int kSeriesTile = kSub * kSubs;
-  static_assert(2 * kPairs + kSubs == kSinTrig, "RiemannParams::trig layout");
+  static_assert(2 * kPairs + kSubs <= kSinTrig, "RiemannParams::trig layout");
   double ck[kPairs], sk[kPairs];       // cos(k_j delta), sin(k_j delta)
-  double cc[kSubs / 2], sc[kSubs / 2];  // cos/sin(c0 delta), c0 = 8, 24, 40, 56
+  double cc[kSubs / 2], sc[kSubs / 2];  // cos/sin(c0 delta), c0 = 8, 24, ..., 88
 
   __device__ __forceinline__ void init_trig(const double* trig) {
 #pragma unroll
@@ -333,7 +337,7 @@ struct AngleSeries {
       sc[i] = trig[2 * kPairs + 2 * i + 1];
     }
   }
-  // sin and cos at the centre of sub-tile q (centre offsets -56, -40, ..., 40, 56 steps)
+  // sin and cos at the centre of sub-tile q (centre offsets -88, -72, ..., 72, 88 steps)
   __device__ __forceinline__ void centre(double S, double C, int q, double& Sq,
                                          double& Cq) const {
     const int i = q < kSubs / 2 ? kSubs / 2 - 1 - q : q - kSubs / 2;
@@ -381,7 +385,7 @@ struct AngleSeries {
 // kSeries (default): AngleSeries with w = 1. Per point: absolute error vs ocml sin
 // <= 7.2e-16 measured (tests allow 4 ulp(1)); the sum agrees with the kIeee path to 2e-15
 // relative. N = 1e9 on [0, pi]: 103.5 us per integration (9.66e12 subint/s) vs 1.53 ms.
-struct Sin : TileDefaults<Sin>, AngleSeries {
+struct Sin : TileDefaults<Sin>, AngleSeries<12> {
   static constexpr double kScale = 1.0;
   template <DivMode M>
   __host__ __device__ static constexpr int tile_len() {
@@ -548,7 +552,7 @@ struct Poly : TileDefaults<Poly<NC>> {
 // v(t) = (1 - cos(t/ts)) * vs   (riemann.cpp:108-111). Integral over [0,1800] is
 // dis_function(1800) = vs*(1800 - ts*sin(1800/ts)) ~= 121999.99983.
 // kSeries: AngleSeries with w = 1/ts on cos; tile value vs (U - sum cos).
-struct TrainVel : TileDefaults<TrainVel>, AngleSeries {
+struct TrainVel : TileDefaults<TrainVel>, AngleSeries<8> {
   double inv_ts, vs;
   static constexpr double kScale = 1.0;
   template <DivMode M>

@@ -196,6 +196,7 @@ struct Pi4F32 : TileDefaults<Pi4F32> {
 };
 // The host's series validity check (series_ok: kSeriesHalfSpan * h <= 2e-6) must bound the
 // farthest sample offset of both Pi4 series tiles.
+static_assert(2 * AngleSeries<12>::kPairs + 12 == kSinTrig, "trig table sized for Sin");
 static_assert(Pi4::kSeriesTile / 2 == kSeriesHalfSpan &&
                   Pi4F32::kSubs * Pi4F32::kSubLen / 2 == kSeriesHalfSpan,
               "kSeriesHalfSpan must be half the Pi4 series tile length");
@@ -595,15 +596,15 @@ static RiemannParams prepared(const RiemannParams& p, DivMode eff) {
     const long double delta =
         f == Integrand::kSin ? static_cast<long double>(p.h)
                              : static_cast<long double>(p.h) / static_cast<long double>(p.p0);
-    for (int j = 0; j < AngleSeries::kPairs; ++j) {
+    for (int j = 0; j < AngleSeries<12>::kPairs; ++j) {
       const long double k = j + 0.5L;
       q.trig[j] = static_cast<double>(cosl(k * delta));
-      q.trig[AngleSeries::kPairs + j] = static_cast<double>(sinl(k * delta));
+      q.trig[AngleSeries<12>::kPairs + j] = static_cast<double>(sinl(k * delta));
     }
-    for (int i = 0; i < AngleSeries::kSubs / 2; ++i) {
-      const long double c0 = AngleSeries::kSub * (i + 0.5L);
-      q.trig[2 * AngleSeries::kPairs + 2 * i] = static_cast<double>(cosl(c0 * delta));
-      q.trig[2 * AngleSeries::kPairs + 2 * i + 1] = static_cast<double>(sinl(c0 * delta));
+    for (int i = 0; i < AngleSeries<12>::kSubs / 2; ++i) {
+      const long double c0 = AngleSeries<12>::kSub * (i + 0.5L);
+      q.trig[2 * AngleSeries<12>::kPairs + 2 * i] = static_cast<double>(cosl(c0 * delta));
+      q.trig[2 * AngleSeries<12>::kPairs + 2 * i + 1] = static_cast<double>(sinl(c0 * delta));
     }
   }
   return q;

@@ -78,7 +78,7 @@ clean:
 SAN := -fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-omit-frame-pointer -g -O1
 .PHONY: sanitize
 sanitize: $(BIN)/host_selftest_asan
-$(BIN)/host_selftest_asan: csrc/cli/host_selftest.cpp csrc/runtime/oracle.cpp csrc/runtime/comm.cpp csrc/runtime/runtime.cpp csrc/cli/cli_common.hpp $(HDRS) | $(BIN)
+$(BIN)/host_selftest_asan: csrc/cli/host_selftest.cpp csrc/runtime/oracle.cpp csrc/runtime/profile_data.cpp csrc/runtime/comm.cpp csrc/runtime/runtime.cpp csrc/cli/cli_common.hpp $(HDRS) | $(BIN)
 	$(HIPCC) -x c++ -std=c++17 -Icsrc/include -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ $(SAN) \
-	  -o $@ csrc/cli/host_selftest.cpp csrc/runtime/oracle.cpp csrc/runtime/comm.cpp csrc/runtime/runtime.cpp \
+	  -o $@ csrc/cli/host_selftest.cpp csrc/runtime/oracle.cpp csrc/runtime/profile_data.cpp csrc/runtime/comm.cpp csrc/runtime/runtime.cpp \
 	  -L/opt/rocm/lib -lamdhip64 -lrccl -lpthread

@@ -3,22 +3,35 @@
 
 Metric and config come from BASELINE.json ("Riemann subintervals/sec at N=1e9 fp64; |error|
 vs analytic pi"). One step = one complete integration of N samples per GPU: gfx950 kernel
-(every sample evaluated, fp64) -> in-kernel DPP/LDS/ticket reduction -> RCCL all-reduce of
-the per-GPU partial over xGMI -> D2H into pinned memory. Steps are hipGraph replays of
-batches of --slots (48) steps; with >1 GPU each batch ends in ONE all-reduce of its 48 step
-results (bucketed: every step still gets its own global sum; --no-bucket = one 8-byte
-all-reduce per step, overlapped on a side stream).
+(every sample evaluated, fp64) -> in-kernel DPP/LDS reduction -> RCCL all-reduce of the
+per-GPU partial over xGMI -> D2H into pinned memory. Steps are hipGraph replays of batches
+of --slots (48) steps plus one replay of a remainder-sized batch (every graph is captured
+before the warmup, so the timed region only replays); with >1 GPU each batch ends in ONE
+all-reduce of its step results (bucketed: every step still gets its own global sum;
+--no-bucket = one 8-byte all-reduce per step, overlapped on a side stream).
 
-Warmup: the W warmup steps, then at least --settle-ms (60) more untimed steps so the timed
-region starts at steady clocks (from idle the GPU ramps from ~90 to 76.8 us per step over
-~25 ms; the JSON line reports the settle steps run as "warmup_settle_steps").
+Launch (the reference's `mpirun -np P ./riemann`, riemann.cpp:62-86: one command, P ranks,
+one gathered result):
+
+    python bench.py                          # 1 GPU, in this process
+    python bench.py --gpus 8                 # spawns 8 rank processes (one per GPU)
+    torchrun --nproc-per-node 8 bench.py --gpus 8     # the same ranks under torchrun
+
+With --gpus N > 1 and no torchrun environment, this process only spawns N children with
+RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT set and relays their exit status; it
+never imports torch or touches the GPU itself. Every child runs the torchrun path.
+
+Warmup: the W warmup steps, then untimed repeats of the timed K-step pattern for at least
+--settle-ms (60) so the timed region starts at steady clocks (from idle the GPU ramps from
+~90 to 76.8 us per step over ~25 ms); the JSON line reports those as "warmup_settle_steps".
 
 Weak scaling: every GPU integrates its own 1e9-sample slice of a global N = 1e9 x n_gpus
 (N = 8e9 on 8 GPUs). The results of the last batch of timed steps (every rank holds the
-global sums) are checked on the host against pi.
-
-    python bench.py                          # 1 GPU
-    torchrun --nproc-per-node 8 bench.py --gpus 8
+global sums) are checked on the host against pi. After the timed region (outside it) the
+record also gets: the same config with IEEE division per sample ("ieee_div"), the series
+path's per-point error against IEEE division on a 64 K-sample window ("per_point_max_ulp"),
+and BASELINE config #3 — N = 1e10 in total, strong-scaled over the same GPUs
+("baseline3_strong_1e10").
 """
 from __future__ import annotations
 
@@ -26,22 +39,29 @@ import argparse
 import json
 import math
 import os
+import signal
+import socket
+import subprocess
 import sys
 import time
 
-# Reference CPU number for the same metric/config (4/(1+x^2), N=1e9, left rule,
-# 8 Xeon workers, -O2): 0.203 s -> 4.94e9 subintervals/s, |err| 1.000e-9.
+# Reference-algorithm number for the same metric/config, measured by the survey on a CPU
+# (the reference's left-Riemann loop, riemann.cpp:29-44, applied to 4/(1+x^2),
+# N=1e9, 8 Xeon workers, -O2): 0.203 s -> 4.94e9 subintervals/s, |err| 1.000e-9. The
+# reference publishes no numbers of its own (BASELINE.json "published": {}).
 BASELINE_SUBINT_PER_S = 4.94e9
+BASELINE_SOURCE = ("CPU reimplementation of the reference algorithm (8 Xeon cores, -O2, "
+                   "BASELINE.md); the reference publishes no numbers")
 
 
-def parse() -> argparse.Namespace:
+def parse(argv=None) -> argparse.Namespace:
     p = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=400)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--settle-ms", type=float, default=60.0,
-                   help="after the W warmup steps, keep stepping (untimed) for at least this "
-                        "long so the timed steps run at steady clocks (0 = off)")
+                   help="after the W warmup steps, repeat the timed K-step pattern (untimed) "
+                        "for at least this long so the timed steps run at steady clocks (0 = off)")
     # (--n is a prefix of torchrun's own --nnodes/--nproc-per-node: use --samples under torchrun)
     p.add_argument("--samples", "--n", dest="n", type=float, default=1e9,
                    help="samples per GPU (weak) or total (strong)")
@@ -54,7 +74,11 @@ def parse() -> argparse.Namespace:
                    help="native: C++ RCCL communicator captured in the step graph; "
                         "torch: torch.distributed all_reduce of each step's partial")
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
-                   help="process-group backend (gloo only for functional tests on shared GPUs)")
+                   help="process-group backend (gloo only for functional tests on shared GPUs "
+                        "or with --device cpu)")
+    p.add_argument("--device", default="gpu", choices=["gpu", "cpu"],
+                   help="cpu: torch fp64 evaluation + gloo (launcher / decomposition tests "
+                        "on a GPU-less box; not a performance configuration)")
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--no-pipeline", action="store_true")
     p.add_argument("--unfused", action="store_true", help="partials + finalize (2 launches)")
@@ -65,97 +89,187 @@ def parse() -> argparse.Namespace:
                    help="one all-reduce per step instead of one per graph batch of steps")
     p.add_argument("--force-collective", action="store_true",
                    help="run the RCCL all-reduce stage even on 1 GPU (tests the multi-GPU graph)")
+    p.add_argument("--no-extras", action="store_true",
+                   help="skip the post-timing extras (IEEE run, per-point ulp, N=1e10 strong)")
     p.add_argument("--verbose", action="store_true")
     p.add_argument("--jsonl", default="", help="also append the JSON line to this file")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
-def main() -> int:
-    args = parse()
+# ------------------------------------------------------------------ launcher (no GPU here)
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv: list[str]) -> int:
+    """Start n rank processes of this script and wait for them (mpirun -np n analogue).
+
+    Runs before anything imports torch or the native extension, so this process never
+    initialises HIP (a GPU-initialised parent may not fork/exec on the pool). The first rank
+    that fails ends the others; the exit status is the first non-zero one.
+    """
+    port = _free_port()
+    base = dict(os.environ)
+    base.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n),
+                LOCAL_WORLD_SIZE=str(n), MIINT_BENCH_LAUNCHER="spawn",
+                MIINT_BENCH_PARENT_TORCH="1" if "torch" in sys.modules else "0")
+    procs = []
+    for r in range(n):
+        env = dict(base, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv],
+                                      env=env))
+
+    def stop_all(sig=signal.SIGTERM):
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(sig)
+
+    def on_signal(signum, _frame):
+        stop_all()
+        raise SystemExit(128 + signum)
+
+    old = {s: signal.signal(s, on_signal) for s in (signal.SIGTERM, signal.SIGINT)}
+    rc = 0
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad and rc == 0:
+                rc = bad[0]
+                print(f"bench.py: a rank exited with {rc}; stopping the others", file=sys.stderr)
+                stop_all()
+                t_end = time.time() + 15
+                while any(p.poll() is None for p in procs) and time.time() < t_end:
+                    time.sleep(0.1)
+                stop_all(signal.SIGKILL)
+            if all(c is not None for c in (p.poll() for p in procs)):
+                break
+            time.sleep(0.05)
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+    return rc
+
+
+# ------------------------------------------------------------------ per-rank benchmark
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and world_env == 1 and "RANK" not in os.environ:
+        return spawn_ranks(args.gpus, argv)
+    if world_env != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world_env}", file=sys.stderr)
+        return 2
+    launcher = os.environ.get("MIINT_BENCH_LAUNCHER",
+                              "torchrun" if "TORCHELASTIC_RUN_ID" in os.environ or world_env > 1
+                              else "single")
+
     import torch
-    import torch.distributed as dist
 
     from cuda_v_mpi_amd import Integrator
     from cuda_v_mpi_amd.parallel import dist as mdist
 
-    world_env = int(os.environ.get("WORLD_SIZE", "1"))
-    if world_env != args.gpus:
-        if world_env == 1 and args.gpus > 1:
-            print(f"bench.py: --gpus {args.gpus} needs torchrun with {args.gpus} processes",
-                  file=sys.stderr)
-            return 2
-    if args.backend == "gloo" and args.comm == "native" and world_env > 1:
+    cpu = args.device == "cpu"
+    if cpu and args.backend != "gloo" and world_env > 1:
+        print("bench.py: --device cpu needs --backend gloo", file=sys.stderr)
+        return 2
+    if args.backend == "gloo" and args.comm == "native" and world_env > 1 and not cpu:
         print("bench.py: --backend gloo shares GPUs between ranks; use --comm torch", file=sys.stderr)
         return 2
-    ctx = mdist.init(backend=args.backend)
+    ctx = mdist.init(backend=args.backend, force=False)
     world = ctx.world
+    for k, want in (("RANK", ctx.rank), ("LOCAL_RANK", ctx.local_rank), ("WORLD_SIZE", world)):
+        assert int(os.environ.get(k, str(want))) == want, (k, os.environ.get(k), want)
     n_per = int(args.n)
     n_total = n_per * world if args.scaling == "weak" else n_per
+    dev = "cpu" if (cpu or ctx.backend != "nccl") else "cuda"
 
-    use_torch = args.comm == "torch" and world > 1
+    def sync_dev():
+        if not cpu:
+            torch.cuda.synchronize()
+
+    use_torch = args.comm == "torch" and world > 1 and not cpu
     integ = Integrator(args.integrand, n=n_total, rule=args.rule, dtype=args.dtype, div=args.div,
-                       backend="hip", ctx=ctx, comm=args.comm, fused=not args.unfused,
-                       grid=args.grid, slots=args.slots, force_collective=args.force_collective,
-                       bucket=not args.no_bucket)
+                       backend="cpu" if cpu else "hip", ctx=ctx, comm=args.comm,
+                       fused=not args.unfused, grid=args.grid, slots=args.slots,
+                       force_collective=args.force_collective, bucket=not args.no_bucket)
     plan = integ.plan
-    graphs = not args.no_graph and not use_torch
+    graphs = not args.no_graph and not use_torch and not cpu
     pipeline = not args.no_pipeline and (world > 1 or args.force_collective)
 
-    if use_torch:  # kernels on the torch stream + torch.distributed all_reduce per step
+    if cpu:  # torch fp64 evaluation of the rank slice + gloo all_reduce per step
+        cpu_vals: list[float] = []
+
+        def launch(k):
+            for _ in range(k):
+                cpu_vals.append(integ.run().value)
+        finish = lambda: None  # noqa: E731
+        result = lambda k: cpu_vals[len(cpu_vals) - args.steps + k]  # noqa: E731
+    elif use_torch:  # kernels on the torch stream + torch.distributed all_reduce per step
         from cuda_v_mpi_amd.parallel.torch_steps import TorchStepper
 
         stepper = TorchStepper(integ.spec, n_total, ctx, rule=args.rule, dtype=args.dtype,
                                div=args.div, grid=args.grid or None)
         launch, finish, result = stepper.launch_steps, stepper.sync, stepper.result
     else:
+        if graphs:  # capture every graph the timed pattern replays, before anything is timed
+            plan.prepare_steps(args.steps)
+            if not plan.graphs_ready:
+                print(f"bench.py: hipGraph capture failed ({plan.graph_error}); "
+                      "running with direct stream enqueue", file=sys.stderr)
+                graphs = False
         launch = lambda k: plan.launch_steps(k, pipeline, graphs)  # noqa: E731
         finish = plan.sync
         result = lambda k: plan.host_result(plan.host_index_of(k, graphs))  # noqa: E731
 
-    # ---- warmup (includes graph capture and RCCL channel setup)
+    # ---- warmup (RCCL channel setup, code-object load, first replays)
     launch(max(1, args.warmup))
     finish()
-    if graphs and not plan.graphs_ready:
-        print(f"bench.py: hipGraph capture failed ({plan.graph_error}); "
-              "running with direct stream enqueue", file=sys.stderr)
-        graphs = False
     # ---- clock settle: from idle the MI355X needs ~25 ms of continuous work before its
-    # per-step time is steady (90 -> 76.8 us per step; profiles/r1/clock_ramp.jsonl). The W
-    # warmup steps alone (20 x 85 us) end inside that ramp, so the warmup also runs at least
-    # --settle-ms of back-to-back steps. The step count comes from one calibration batch,
-    # agreed across ranks (MAX) so every rank runs the same collectives.
+    # per-step time is steady (90 -> 76.8 us per step; profiles/r1/clock_ramp.jsonl). The
+    # settle phase repeats exactly the timed K-step pattern (same graphs, same remainder
+    # batch), for at least --settle-ms; the repeat count is calibrated once and agreed across
+    # ranks (MAX) so every rank runs the same collectives.
     settle_steps = 0
-    if args.settle_ms > 0:
+    if args.settle_ms > 0 and not cpu:
         t_c = time.perf_counter()
-        launch(plan.slots)
+        launch(args.steps)
         finish()
-        per_step = (time.perf_counter() - t_c) / plan.slots
-        want = torch.tensor([math.ceil(args.settle_ms * 1e-3 / max(per_step, 1e-7))],
-                            dtype=torch.float64, device="cuda" if ctx.backend == "nccl" else "cpu")
+        per_call = time.perf_counter() - t_c
+        want = torch.tensor([math.ceil(args.settle_ms * 1e-3 / max(per_call, 1e-7))],
+                            dtype=torch.float64, device=dev)
         ctx.all_reduce_max(want)
-        settle_steps = plan.slots + int(want.item())
-        launch(settle_steps - plan.slots)
+        calls = int(want.item())
+        for _ in range(calls):
+            launch(args.steps)
         finish()
+        settle_steps = (1 + calls) * args.steps
 
     # ---- timed region: barrier + device sync on both sides, K steps in between
+    g0 = plan.graph_launches if plan is not None else 0
+    d0 = plan.direct_steps if plan is not None else 0
     ctx.barrier()
-    torch.cuda.synchronize()
+    sync_dev()
     t0 = time.perf_counter()
     launch(args.steps)
     finish()
-    torch.cuda.synchronize()
+    sync_dev()
     t1 = time.perf_counter()
     ctx.barrier()
     elapsed = t1 - t0
+    graph_replays = (plan.graph_launches - g0) if plan is not None else 0
+    direct_timed = (plan.direct_steps - d0) if plan is not None else args.steps
 
-    t = torch.tensor([elapsed], dtype=torch.float64,
-                     device="cuda" if ctx.backend == "nccl" else "cpu")
-    ctx.all_reduce_max(t)
-    elapsed_max = float(t.item())
+    per_rank_ms = ctx.all_gather_scalars(elapsed / args.steps * 1e3, device=dev)
+    elapsed_max = max(per_rank_ms) * args.steps * 1e-3
 
     # ---- verify the results of the last steps (every rank holds the global value)
     analytic = integ.spec.analytic()
-    last = range(max(0, args.steps - min(args.steps, plan.slots)), args.steps)
+    slots = plan.slots if plan is not None else args.slots
+    last = range(max(0, args.steps - min(args.steps, slots)), args.steps)
     vals = [result(k) for k in last]
     errs = [abs(v - analytic) for v in vals]
     abs_err = max(errs)
@@ -165,6 +279,19 @@ def main() -> int:
 
     ms_per_step = elapsed_max / args.steps * 1e3
     value = n_total * args.steps / elapsed_max
+
+    # ---- outside the timed region: transport facts and the extras
+    comm = getattr(integ, "_comm", None)
+    rccl_world = comm.transport_world if comm is not None else None
+    rccl_version = None
+    if not cpu:
+        from cuda_v_mpi_amd import native
+
+        rccl_version = native().Comm.version()
+    extras = {}
+    if not cpu and not use_torch and not args.no_extras:
+        extras = run_extras(args, ctx, integ, n_total, pipeline, dev)
+
     if ctx.is_root:
         out = {
             "metric": "Riemann subintervals/sec at N=1e9 fp64; |error| vs analytic pi",
@@ -178,29 +305,41 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": args.scaling,
             "vs_baseline": value / BASELINE_SUBINT_PER_S,
+            "baseline_source": BASELINE_SOURCE,
             "dtype": args.dtype,
             "data": "synthetic (analytic integrand 4/(1+x^2); no dataset)",
             "abs_err": abs_err,
             "result": vals[-1],
             "verified": ok,
+            "launcher": launcher,
+            "parent_imported_torch": os.environ.get("MIINT_BENCH_PARENT_TORCH") == "1",
+            "rccl_world": rccl_world,
+            "rccl_version": rccl_version,
+            "per_rank_ms": per_rank_ms,
+            "per_rank_spread_ms": max(per_rank_ms) - min(per_rank_ms),
+            "graph_replays_timed": graph_replays,
+            "direct_steps_timed": direct_timed,
+            **extras,
             "config": {
                 "model": f"riemann_{args.integrand}_{args.dtype}",
                 "integrand": "4/(1+x^2) on [0,1]" if args.integrand == "pi4" else args.integrand,
                 "N": n_total,
-                "n_per_gpu": n_total // world if args.scaling == "weak" else n_total // world,
+                "n_per_gpu": n_total // world,
                 "rule": args.rule,
-                "division": str(plan.effective_div).split(".")[-1],
+                "division": str(plan.effective_div).split(".")[-1] if plan is not None else "ieee",
                 "global_batch": n_total,
                 "seq_len": 1,
                 "parallelism": f"dp{world}",
-                "comm": args.comm if (world > 1 or args.force_collective) else "none",
-                "graphs": graphs,
-                "graph_nodes": plan.graph_nodes if graphs else 0,
+                "comm": (args.comm if (world > 1 or args.force_collective) else "none"),
+                # true only when the timed region ran as graph replays and nothing else
+                "graphs": bool(graphs and graph_replays > 0 and direct_timed == 0),
+                "graph_nodes": plan.graph_nodes if (graphs and plan is not None) else 0,
                 "pipeline": pipeline,
-                "bucketed_allreduce": bool(plan.bucketed),
+                "bucketed_allreduce": bool(plan.bucketed) if plan is not None else False,
                 "fused_reduction": not args.unfused,
-                "chained_batches": bool(plan.chained) and graphs,
-                "grid": plan.grid,
+                "chained_batches": bool(plan.chained) and graphs if plan is not None else False,
+                "grid": plan.grid if plan is not None else 0,
+                "device": args.device,
             },
         }
         print(json.dumps(out), flush=True)
@@ -209,6 +348,73 @@ def main() -> int:
                 f.write(json.dumps(out) + "\n")
     ctx.destroy()
     return 0 if ok else 1
+
+
+def _timed_steps(ctx, plan, steps, pipeline, dev) -> float:
+    """ms per step of `steps` graph-replayed steps (slowest rank), warmed and bracketed."""
+    import torch
+
+    plan.prepare_steps(steps)
+    plan.launch_steps(steps, pipeline, True)
+    plan.sync()
+    ctx.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    plan.launch_steps(steps, pipeline, True)
+    plan.sync()
+    torch.cuda.synchronize()
+    t = torch.tensor([(time.perf_counter() - t0) / steps * 1e3], dtype=torch.float64, device=dev)
+    ctx.all_reduce_max(t)
+    return float(t.item())
+
+
+def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
+    """Measured after (never inside) the timed region; every rank takes part."""
+    from cuda_v_mpi_amd import Integrator
+    from cuda_v_mpi_amd.ops import kernels
+
+    out: dict = {}
+    kw = dict(rule=args.rule, dtype=args.dtype, ctx=ctx, comm=args.comm, slots=args.slots,
+              bucket=not args.no_bucket, force_collective=args.force_collective)
+    # (1) the same config with correctly rounded division for every sample
+    if args.integrand == "pi4" and args.div != "ieee":
+        ie = Integrator(args.integrand, n=n_total, div="ieee", **kw)
+        steps = 40
+        ms = _timed_steps(ctx, ie.plan, steps, pipeline, dev)
+        v = ie.plan.host_result(ie.plan.host_index_of(steps - 1, True))
+        out["ieee_div"] = {"value": n_total / (ms * 1e-3), "ms_per_step": ms, "steps": steps,
+                           "result": v, "abs_err": abs(v - math.pi)}
+        out["ieee_div_value"] = out["ieee_div"]["value"]
+        del ie
+    # (2) per-point accuracy of the division the headline used, on one 64 K-sample window
+    #     of this rank's slice (rank 0's is reported)
+    eff = str(integ.plan.effective_div).split(".")[-1]
+    if args.integrand == "pi4" and args.dtype == "fp64" and eff != "ieee":
+        import torch
+
+        i0 = integ.plan.begin + integ.plan.count // 8 + 12_345
+        w = min(1 << 16, integ.plan.begin + integ.plan.count - i0)
+        v = kernels.point_values(integ.spec, n_total, rule=args.rule, div=eff, i_begin=i0,
+                                 n_local=w)
+        r = kernels.point_values(integ.spec, n_total, rule=args.rule, div="ieee", i_begin=i0,
+                                 n_local=w)
+        spacing = torch.nextafter(r.abs(), torch.full_like(r, math.inf)) - r.abs()
+        u = ((v - r) / spacing).abs()
+        out["per_point_max_ulp"] = float(u.max())
+        out["per_point_frac_within_1ulp"] = float((u <= 1.0).double().mean())
+        out["per_point_window"] = [int(i0), int(w)]
+    # (3) BASELINE config #3: N = 1e10 in total over the same GPUs (strong scaling)
+    if args.integrand == "pi4" and args.scaling == "weak":
+        n3 = 10**10
+        st = Integrator("pi4", n=n3, div=args.div, **kw)
+        steps = 20
+        ms = _timed_steps(ctx, st.plan, steps, pipeline, dev)
+        v = st.plan.host_result(st.plan.host_index_of(steps - 1, True))
+        out["baseline3_strong_1e10"] = {"N": n3, "value": n3 / (ms * 1e-3), "ms_per_step": ms,
+                                        "steps": steps, "result": v, "abs_err": abs(v - math.pi),
+                                        "n_per_gpu": n3 // ctx.world, "scaling": "strong"}
+        del st
+    return out
 
 
 if __name__ == "__main__":

@@ -7,6 +7,8 @@
 //   * one process per GPU via torchrun: torchrun --no-python --nproc-per-node 8 ./riemann
 //     (RANK/WORLD_SIZE/LOCAL_RANK from the env, RCCL unique id over a TCP rendezvous on
 //     MASTER_ADDR:MASTER_PORT+17)
+//   * W logical ranks on one GPU:      ./riemann --loopback 8   (LoopbackComm, threads;
+//     exercises every world > 1 path on a one-GPU box)
 #pragma once
 
 #include <cmath>
@@ -74,12 +76,24 @@ struct Topology {
   int rank0 = 0;        // first rank handled by this process
   int local = 1;        // ranks (threads) in this process
   bool multiproc = false;
+  bool loopback = false;  // --loopback W: W logical ranks on device 0 (LoopbackComm)
 };
 
 // Decide who runs what: torchrun env -> one rank per process; else --gpus threads.
 inline Topology topology(const Args& a) {
   Topology t;
   const int ws = env_int("WORLD_SIZE", 1);
+  if (a.has("loopback")) {
+    // every multi-rank code path (slicing, collectives, group graphs, parity windows) with
+    // W ranks on the one GPU of the test pool; not a performance configuration
+    t.world = static_cast<int>(a.integer("loopback", 2));
+    MIINT_CHECK(t.world >= 1 && t.world <= kMaxLoopbackRanks, "--loopback W needs 1 <= W <= 16");
+    MIINT_CHECK(ws == 1, "--loopback runs in one process (no torchrun)");
+    MIINT_CHECK(device_count() >= 1, "--loopback needs a HIP device (no HIP devices visible)");
+    t.local = t.world;
+    t.loopback = true;
+    return t;
+  }
   if (ws > 1) {
     t.world = ws;
     t.rank0 = env_int("RANK", 0);
@@ -101,12 +115,16 @@ inline Topology topology(const Args& a) {
 inline void run_ranks(const Topology& t,
                       const std::function<void(int rank, int device, const Comm* comm)>& fn) {
   std::vector<std::unique_ptr<Comm>> comms;
+  if (t.loopback) {
+    run_loopback(t.world, 0, [&](int r, const Comm* c) { fn(r, 0, t.world > 1 ? c : nullptr); });
+    return;
+  }
   if (t.multiproc) {
     const char* addr = std::getenv("MASTER_ADDR");
     const int port = env_int("MASTER_PORT", 29500) + 17;
     const std::string id = rendezvous_unique_id(addr ? addr : "127.0.0.1", port, t.rank0, t.world);
     const int dev = env_int("LOCAL_RANK", 0);
-    comms.emplace_back(new Comm(id, t.rank0, t.world, dev));
+    comms.emplace_back(new RcclComm(id, t.rank0, t.world, dev));
     fn(t.rank0, dev, comms[0].get());
     return;
   }
@@ -116,7 +134,7 @@ inline void run_ranks(const Topology& t,
   }
   std::vector<int> devs(t.world);
   for (int i = 0; i < t.world; ++i) devs[i] = i;
-  comms = Comm::init_all(devs);
+  comms = RcclComm::init_all(devs);
   std::vector<std::thread> th;
   std::mutex mu;
   std::string err;

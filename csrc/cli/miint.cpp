@@ -173,7 +173,7 @@ int comm_sweep(const cli::Args& a, const cli::Topology& topo, double max_bytes, 
       }
   };
   if (!topo.multiproc && topo.world == 1) {
-    auto one = Comm::init_all({0});
+    auto one = RcclComm::init_all({0});
     body(0, 0, one[0].get());
   } else {
     cli::run_ranks(topo, body);
@@ -206,7 +206,7 @@ int main(int argc, char** argv) {
     const std::string cmd = a.positional().empty() ? "info" : a.positional()[0];
     if (cmd == "info") {
       const int nd = device_count();
-      std::printf("miint: %d HIP device(s), RCCL %s\n", nd, nd ? Comm::version().c_str() : "-");
+      std::printf("miint: %d HIP device(s), RCCL %s\n", nd, nd ? RcclComm::version().c_str() : "-");
       for (int d = 0; d < nd; ++d) {
         const DeviceInfo i = device_info(d);
         std::printf("  [%d] %s %s  %d CUs  %.1f GHz  %.1f GB  L2 %d KB\n", d, i.name.c_str(),

@@ -19,6 +19,7 @@
 #include "cli_common.hpp"
 #include "miint/integrator.hpp"
 #include "miint/oracle.hpp"
+#include "miint/trace.hpp"
 
 using namespace miint;
 
@@ -35,6 +36,7 @@ Rule parse_rule(const std::string& s) {
 
 int main(int argc, char** argv) {
   try {
+    install_crash_handler_from_env();
     cli::Args a(argc, argv);
     const Integrand f = cli::parse_integrand(a.str("integrand", "sin"));
     const double pi = 3.14159265358979323846;
@@ -80,6 +82,7 @@ int main(int argc, char** argv) {
       std::mutex mu;
       cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
         RiemannPlan plan(cfg, dev, comm);
+        if (a.has("prepare")) plan.prepare_steps(static_cast<int>(a.integer("prepare", iters)));
         plan.run_steps(1, comm != nullptr, false);  // cold: code-object load, first launch
         StepTiming t = plan.run_steps(iters, comm != nullptr, iters > 1);
         std::lock_guard<std::mutex> g(mu);

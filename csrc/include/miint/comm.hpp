@@ -1,4 +1,4 @@
-// RCCL communicator wrapper (collectives over xGMI between the GPUs of one node).
+// Communicators: the collectives every multi-rank plan runs on a stream.
 //
 // Replaces every MPI call site of the reference:
 //   riemann.cpp:76,82-85   worker MPI_Send + root MPI_Recv loop  -> allreduce_sum(1 x f64)
@@ -7,20 +7,44 @@
 //                          -> allgather of P block totals (P x 8 B) + on-device carry add;
 //                             optional allgather of the full table when every rank needs it
 //   4main.c:137 Barrier    -> stream order (or a 0-byte-equivalent allreduce)
-// Two bootstrap modes: one process per GPU (unique id exchanged out of band, e.g. through
-// torch.distributed's store or miint's TCP rendezvous) and one process driving all GPUs
-// (ncclCommInitAll). Collectives are enqueued on the caller's stream so they can be
-// captured into a hipGraph together with the kernels that feed them.
+//
+// `Comm` is the interface the plans (RiemannPlan, TrainScan, Table2DPlan) program against:
+// stream-ordered fp64 collectives plus two graph hooks (capture / launch), because how a
+// batch of steps that contains collectives becomes a hipGraph depends on the transport.
+//
+//   RcclComm      production: RCCL over xGMI, one rank per GPU. Two bootstraps: one process
+//                 per GPU (unique id shared out of band: torch.distributed's store or miint's
+//                 TCP rendezvous) and one process driving every GPU (ncclCommInitAll).
+//                 Collectives are RCCL kernels on the caller's stream, so a rank's graph
+//                 simply captures them.
+//   LoopbackComm  W logical ranks on ONE device, one host thread per rank (test transport:
+//                 the gpurun pool has one GPU and RCCL refuses two ranks on a device). Every
+//                 collective is a host barrier at ENQUEUE time plus cross-stream events, a
+//                 fixed-rank-order sum kernel and device copies, all stream-ordered; nothing
+//                 spins on the device, and every event a stream waits on was recorded before
+//                 the wait was enqueued, so no interleaving of the ranks' streams on the
+//                 hardware queues can deadlock. Graph capture is group-wide: rank 0 opens one
+//                 capture on a group stream and every rank enqueues its batch onto THAT
+//                 stream (HIP calls serialised, the collectives' barriers order the ranks'
+//                 work), so the W ranks' batches, collectives included, become ONE graph,
+//                 launched once per batch for the whole group. (Ranks capturing on their own
+//                 streams joined by cross-stream event waits crash the ROCm 7.0 runtime that
+//                 PyTorch bundles, and need no more coverage than this: the per-rank stream
+//                 choreography is what the direct, uncaptured path exercises.)
 #pragma once
 
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <condition_variable>
+#include <functional>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
 #include "miint/common.hpp"
+#include "miint/runtime.hpp"
 
 #define MIINT_RCCL(expr)                                                                 \
   do {                                                                                   \
@@ -34,38 +58,173 @@ namespace miint {
 
 class Comm {
  public:
-  // 128-byte RCCL unique id (raw bytes), created by rank 0 and shared out of band.
-  static std::string unique_id();
-  // One process per GPU.
-  Comm(const std::string& id, int rank, int world, int device);
-  // One process, all listed devices (rank i <-> devices[i]).
-  static std::vector<std::unique_ptr<Comm>> init_all(const std::vector<int>& devices);
-  ~Comm();
+  virtual ~Comm() = default;
   Comm(const Comm&) = delete;
   Comm& operator=(const Comm&) = delete;
 
   int rank() const { return rank_; }
   int world() const { return world_; }
   int device() const { return device_; }
+  virtual const char* kind() const = 0;
+  // Ranks the transport itself reports (ncclCommCount for RCCL): what the collectives
+  // actually span, independent of how the launcher counted processes.
+  virtual int transport_world() const = 0;
 
-  void allreduce_sum(const double* send, double* recv, size_t count, hipStream_t s) const;
-  void allgather(const double* send, double* recv, size_t count_per_rank, hipStream_t s) const;
-  void broadcast(double* buf, size_t count, int root, hipStream_t s) const;
-  void reduce_sum(const double* send, double* recv, size_t count, int root, hipStream_t s) const;
-  // Throws if RCCL reported an asynchronous error (e.g. a peer died).
-  void check_async() const;
+  virtual void allreduce_sum(const double* send, double* recv, size_t count,
+                             hipStream_t s) const = 0;
+  // recv holds world x count_per_rank values in rank order.
+  virtual void allgather(const double* send, double* recv, size_t count_per_rank,
+                         hipStream_t s) const = 0;
+  virtual void broadcast(double* buf, size_t count, int root, hipStream_t s) const = 0;
+  virtual void reduce_sum(const double* send, double* recv, size_t count, int root,
+                          hipStream_t s) const = 0;
+  // Throws if the transport reported an asynchronous error (e.g. a peer died).
+  virtual void check_async() const {}
   // Abort outstanding collectives (watchdog path); the communicator is unusable afterwards.
-  void abort() const;
+  virtual void abort() const {}
+
+  // Capture everything `body` enqueues on `s` into `g` / replay it. Every rank of a
+  // communicator calls these collectively (same order, same batches).
+  virtual void capture(Graph& g, hipStream_t s,
+                       const std::function<void(hipStream_t)>& body) const {
+    g.capture(s, body);
+  }
+  virtual void launch(const Graph& g, hipStream_t s) const { g.launch(s); }
+  // True if capture() hands its body ONE stream shared by the whole group: the body must
+  // then enqueue everything on that stream (no fork/join onto side streams).
+  virtual bool capture_single_stream() const { return false; }
+
+ protected:
+  Comm(int rank, int world, int device) : rank_(rank), world_(world), device_(device) {}
+  int rank_ = 0, world_ = 1, device_ = 0;
+};
+
+// Capture / launch through `comm` when there is one (group-wide graphs), else plainly.
+inline void capture_with(const Comm* comm, Graph& g, hipStream_t s,
+                         const std::function<void(hipStream_t)>& body) {
+  if (comm) comm->capture(g, s, body);
+  else g.capture(s, body);
+}
+inline void launch_with(const Comm* comm, const Graph& g, hipStream_t s) {
+  if (comm) comm->launch(g, s);
+  else g.launch(s);
+}
+
+class RcclComm final : public Comm {
+ public:
+  // 128-byte RCCL unique id (raw bytes), created by rank 0 and shared out of band.
+  static std::string unique_id();
+  // One process per GPU.
+  RcclComm(const std::string& id, int rank, int world, int device);
+  // One process, all listed devices (rank i <-> devices[i]).
+  static std::vector<std::unique_ptr<Comm>> init_all(const std::vector<int>& devices);
+  ~RcclComm() override;
+
+  const char* kind() const override { return "rccl"; }
+  int transport_world() const override;
+  void allreduce_sum(const double* send, double* recv, size_t count, hipStream_t s) const override;
+  void allgather(const double* send, double* recv, size_t count_per_rank,
+                 hipStream_t s) const override;
+  void broadcast(double* buf, size_t count, int root, hipStream_t s) const override;
+  void reduce_sum(const double* send, double* recv, size_t count, int root,
+                  hipStream_t s) const override;
+  void check_async() const override;
+  void abort() const override;
 
   static void group_start();
   static void group_end();
   static std::string version();
 
  private:
-  Comm() = default;
+  RcclComm(ncclComm_t c, int rank, int world, int device)
+      : Comm(rank, world, device), comm_(c) {}
   mutable ncclComm_t comm_ = nullptr;  // nulled by abort()
-  int rank_ = 0, world_ = 1, device_ = 0;
 };
+
+// ------------------------------------------------------------------ loopback transport
+constexpr int kMaxLoopbackRanks = 16;
+
+class LoopbackGroup;
+
+class LoopbackComm final : public Comm {
+ public:
+  LoopbackComm(LoopbackGroup* g, int rank);
+  const char* kind() const override { return "loopback"; }
+  int transport_world() const override { return world_; }
+  void allreduce_sum(const double* send, double* recv, size_t count, hipStream_t s) const override;
+  void allgather(const double* send, double* recv, size_t count_per_rank,
+                 hipStream_t s) const override;
+  void broadcast(double* buf, size_t count, int root, hipStream_t s) const override;
+  void reduce_sum(const double* send, double* recv, size_t count, int root,
+                  hipStream_t s) const override;
+  void check_async() const override;
+  void abort() const override;
+  void capture(Graph& g, hipStream_t s,
+               const std::function<void(hipStream_t)>& body) const override;
+  void launch(const Graph& g, hipStream_t s) const override;
+  bool capture_single_stream() const override { return true; }
+  LoopbackGroup& group() const { return *g_; }
+
+ private:
+  LoopbackGroup* g_;  // the group owns its comms
+};
+
+// Shared state of W logical ranks on one device. Create it, hand comm(r) to the thread
+// driving rank r (run_loopback does both).
+class LoopbackGroup {
+ public:
+  static std::shared_ptr<LoopbackGroup> create(int world, int device, double timeout_s = 120.0);
+  ~LoopbackGroup();
+  int world() const { return world_; }
+  int device() const { return device_; }
+  const Comm* comm(int rank) const { return comms_.at(rank).get(); }
+  // Host barrier over the W rank threads; throws after timeout_s or once the group is
+  // broken (a rank failed: the others must not wait for it forever).
+  void barrier(int rank);
+  void mark_broken(const std::string& why);
+  bool broken() const;
+  // Collectives issued so far (rank 0's count) and group graph launches.
+  long collectives() const { return collectives_; }
+  long graph_launches() const { return graph_launches_; }
+
+ private:
+  friend class LoopbackComm;
+  LoopbackGroup(int world, int device, double timeout_s);
+  double* staging(int rank, size_t count, hipStream_t s);
+  // s is the open group capture's stream: stream order replaces the event choreography
+  bool shared(hipStream_t s) const { return capture_stream_ != nullptr && s == capture_stream_; }
+
+  int world_, device_;
+  double timeout_s_;
+  std::vector<std::unique_ptr<Comm>> comms_;
+  // barrier
+  mutable std::mutex mu_;
+  std::condition_variable cv_;
+  int arrived_ = 0;
+  long generation_ = 0;
+  bool broken_ = false;
+  std::string why_;
+  // Group captures: HIP's stream capture is not safe against several threads adding nodes
+  // to one capture graph at once (heap corruption in launch-under-capture), so a rank holds
+  // capture_mu_ for every HIP call it makes inside a group capture and drops it only while
+  // it waits at a barrier.
+  std::mutex capture_mu_;
+  // collective state: pointers posted by each rank before the first barrier
+  std::vector<const double*> send_;
+  std::vector<double*> recv_;
+  std::vector<std::unique_ptr<Event>> ready_, done_, pre_;
+  Event post_;
+  std::unique_ptr<Stream> origin_;
+  std::vector<DeviceBuffer<double>> staging_;
+  std::shared_ptr<Graph> captured_;  // rank 0's group capture, handed to every rank
+  hipStream_t capture_stream_ = nullptr;  // origin_ while a group capture is open
+  long collectives_ = 0, graph_launches_ = 0;
+};
+
+// Drive W logical ranks on `device`: one thread per rank runs fn(rank, comm). The first
+// failure breaks the group (so no rank waits on a dead peer) and is rethrown.
+void run_loopback(int world, int device, const std::function<void(int, const Comm*)>& fn,
+                  double timeout_s = 120.0);
 
 // Minimal TCP rendezvous for native multi-process launches (no MPI in the image, and the
 // CLI must not depend on Python): rank 0 listens on addr:port and hands the RCCL unique id
@@ -77,5 +236,12 @@ std::string rendezvous_unique_id(const std::string& addr, int port, int rank, in
 // and returns the len bytes it received. Both sides fail after timeout_s.
 std::string rendezvous_share(const std::string& addr, int port, int rank, int world,
                              const std::string& payload, size_t len, double timeout_s);
+
+// Loopback kernels (loopback.hip): out[i] = sum over q < w of src[q][i], q in rank order.
+struct LoopbackPtrs {
+  const double* p[kMaxLoopbackRanks];
+};
+void launch_loopback_sum(const LoopbackPtrs& src, int w, size_t count, double* out,
+                         hipStream_t s);
 
 }  // namespace miint

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <map>
 #include <memory>
 #include <string>
 #include <vector>
@@ -112,13 +113,23 @@ class RiemannPlan {
   // Capture one batch of `slots` steps into a hipGraph (fork/join over two streams when
   // world > 1). Done lazily by the step runners.
   void capture_graphs();
-  bool graphs_ready() const { return batch_ != nullptr; }
+  // Capture every graph launch_steps(steps, ., true) will replay: the `slots`-step batch
+  // and, when slots does not divide steps, a batch of the remainder (so a timed run of any
+  // length replays graphs only, and no capture lands inside it). Collective over ranks.
+  void prepare_steps(int steps);
+  // A batch graph has been captured (and no capture failed).
+  bool graphs_ready() const { return !graphs_.empty() && graph_error_.empty(); }
   // Non-empty if graph capture failed (the plan then enqueues directly).
   const std::string& graph_error() const { return graph_error_; }
   size_t graph_nodes() const;
+  // hipGraph replays issued so far (every launch_steps / run_steps call).
+  long graph_launches() const { return graph_launches_; }
+  // Steps enqueued directly (not from a graph) so far.
+  long direct_steps() const { return direct_steps_; }
 
-  // Run `steps` complete integrations back to back. graphs=true: whole batches as graph
-  // replays (results of step k in host slot k % slots), remainder enqueued directly.
+  // Run `steps` complete integrations back to back. graphs=true: whole batches of `slots`
+  // steps as graph replays, then one replay of a remainder-sized batch graph (results of
+  // step k in host slot k % slots).
   // graphs=false: direct enqueue (result of step k in host slot k % host_capacity); with
   // pipeline=true and world > 1 the reduce/copy of step k overlaps compute of step k+1.
   // bucketed(): batches of `slots` steps, one all-reduce each, host slot k % slots.
@@ -127,7 +138,10 @@ class RiemannPlan {
   // synchronize); call sync() before reading host results.
   void launch_steps(int steps, bool pipeline, bool graphs);
   void sync() const;
-  // Host slot holding the result of step k of the last launch_steps/run_steps call.
+  // Host slot holding the result of step k of the last launch_steps/run_steps call (the
+  // slot follows how that call actually ran: graph replays and bucketed batches use slot
+  // k % slots, direct per-step enqueue k % host_capacity; `graphs` is only a fallback
+  // before any call).
   int host_index_of(int k, bool graphs) const;
   hipStream_t compute_stream() const { return compute_.get(); }
   hipStream_t comm_stream() const { return comm_stream_.get(); }
@@ -141,8 +155,9 @@ class RiemannPlan {
  private:
   void enqueue_batch(hipStream_t cs, hipStream_t rs, int nsteps, bool overlap);
   void enqueue_chain(hipStream_t s, int nsteps) const;
+  const Graph* batch_graph(int nsteps);  // captured lazily; null if capture failed
+  bool use_graphs(bool requested, int steps);
   double* result_ptr(int j) const { return direct_ ? host_.device_ptr() + j : result_.get() + j; }
-  bool use_graphs(bool requested);
 
   RiemannConfig cfg_;
   int device_;
@@ -162,8 +177,10 @@ class RiemannPlan {
   std::vector<std::unique_ptr<Event>> ev_computed_, ev_drained_;
   Event ev_fork_, ev_join_;
   Event ev_t0_, ev_t1_;
-  std::unique_ptr<Graph> batch_;  // `slots` steps
+  std::map<int, std::unique_ptr<Graph>> graphs_;  // batch graphs by step count
   std::string graph_error_;
+  long graph_launches_ = 0, direct_steps_ = 0;
+  int last_mode_ = -1;  // last launch_steps: -1 none, 0 direct per-step, 1 batches/graphs
 };
 
 }  // namespace miint

@@ -2,9 +2,9 @@
 //
 // The reference has no tests; its only checks are eyeballing printed values.
 // This module provides the numbers every test and CLI self-check compares against:
-//   * the 1801-sample velocity profile, *generated* from its
-//     7-phase jerk-limited definition instead of copied (max |delta| vs the shipped table
-//     is 1.1e-13; tests compare against /root/reference/ex4vel.h when it is present);
+//   * the 1801-sample velocity profile: bit-exact data
+//     (profile_data.cpp, sha256-pinned), plus a generator of the same profile from its
+//     7-phase jerk-limited definition (within 1.1e-13 of the data) as a cross-check;
 //   * serial long-double Riemann sums and analytic integrals;
 //   * exact emulations of the reference programs' partition arithmetic, bugs included
 //     (SURVEY §2.7 B5/B10/B13), behind --parity switches in the CLIs.
@@ -26,10 +26,13 @@ constexpr int kProfileSeconds = 1800;
 constexpr int kStepsPerSec = 10000;      // cintegrate.cu:19, 4main.c:26
 constexpr double kJerk = 0.002904762;    // m/s^3 per 1-s step of the profile
 
-// Generated DefaultProfile: v[0]=0, v[i+1]=v[i]+a_i with a_i the jerk-limited
-// acceleration (ramp 100 s, hold 200 s, ramp-down 100 s, cruise 1000 s, mirrored braking),
-// rounded to 15 significant digits like the Excel export it came from (ex4vel.h:1-5).
+// DefaultProfile (ex4vel.h:10-210), bit-exact: what every kernel, plan and oracle uses.
 const std::vector<double>& profile_table();
+// The same profile generated from its definition: v[0]=0, v[i+1]=v[i]+a_i with a_i the
+// jerk-limited acceleration (ramp 100 s, hold 200 s, ramp-down 100 s, cruise 1000 s,
+// mirrored braking), rounded to 15 significant digits (ex4vel.h:1-5 "Excel ... 15 digits").
+// Within 1.1e-13 of profile_table(); kept as an independent check of the data.
+const std::vector<double>& generated_profile_table();
 
 // Linear interpolation of a 1-s-spaced table at t, segment index clamped to the table.
 double interp(const std::vector<double>& table, double t);
@@ -72,6 +75,8 @@ struct TrainScanParity {
   double sum_of_sums;   // default_sum_of_sums[T-1] on root after phase 2 (never printed)
 };
 TrainScanParity trainscan_parity(int comm_size);
+// The reference's faccel (4main.c:262-269) bit-for-bit: no clamping, no FMA.
+double faccel_ref(const std::vector<double>& table, double time);
 
 }  // namespace oracle
 }  // namespace miint

@@ -14,6 +14,7 @@
 #include <cstddef>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <string>
 #include <utility>
 
@@ -148,6 +149,10 @@ class PinnedBuffer {
 };
 
 // Captured work on one stream, instantiated once and replayed.
+//
+// A Graph can also *adopt* a graph that a communicator captured for a whole group of
+// ranks (LoopbackComm: one graph holds every logical rank's batch); such a graph is
+// replayed through that communicator (launch_with), never directly.
 class Graph {
  public:
   Graph() = default;
@@ -156,15 +161,27 @@ class Graph {
   Graph& operator=(const Graph&) = delete;
   // Capture everything `body` enqueues on `s` (global capture mode: any illegal
   // synchronising call inside body fails loudly instead of silently breaking capture).
-  void capture(hipStream_t s, const std::function<void(hipStream_t)>& body);
+  // Relaxed mode lets other threads enqueue onto streams that joined the capture
+  // (group-wide captures).
+  void capture(hipStream_t s, const std::function<void(hipStream_t)>& body,
+               hipStreamCaptureMode mode = hipStreamCaptureModeGlobal);
+  // Start / finish a capture whose body is enqueued by the caller (possibly from several
+  // threads onto streams that joined `s`'s capture sequence).
+  void begin(hipStream_t s, hipStreamCaptureMode mode);
+  void end(hipStream_t s);
   void launch(hipStream_t s) const;
-  bool ready() const { return exec_ != nullptr; }
-  size_t num_nodes() const { return nodes_; }
+  void adopt(std::shared_ptr<const Graph> group) { reset(); group_ = std::move(group); }
+  const Graph* group() const { return group_.get(); }
+  bool ready() const { return exec_ != nullptr || group_ != nullptr; }
+  size_t num_nodes() const { return group_ ? group_->num_nodes() : nodes_; }
+  hipGraphExec_t exec() const { return exec_; }
 
  private:
+  void reset();
   hipGraph_t graph_ = nullptr;
   hipGraphExec_t exec_ = nullptr;
   size_t nodes_ = 0;
+  std::shared_ptr<const Graph> group_;
 };
 
 // Monotonic wall clock in seconds (the reference's clock_gettime(CLOCK_MONOTONIC)).

@@ -26,6 +26,11 @@ void trace_push(const char* name);
 void trace_pop();
 void trace_mark(const char* name);
 
+// Failure detection for native crashes: with MIINT_CRASH_TRACE=1 a SIGSEGV/SIGBUS/SIGABRT
+// handler writes the native backtrace (glibc backtrace_symbols_fd) to stderr before the
+// default action runs. Installed by the Python module and the CLIs at start-up.
+void install_crash_handler_from_env();
+
 class TraceRange {
  public:
   explicit TraceRange(const char* name) : on_(tracing_enabled()) {

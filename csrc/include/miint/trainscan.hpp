@@ -49,6 +49,7 @@ struct TrainScanConfig {
 struct TrainScanResult {
   double distance = 0.0;     // phase-1 value "Total distance traveled" (already / sps)
   double sum_of_sums = 0.0;  // phase-2 last scanned element (raw, not scaled)
+  double distance_scan = 0.0;  // --parity: the printed element as the parallel scan rounds it
   double device_ms = 0.0;
   unsigned timeout = 0;      // look-back spin gave up (never expected)
 };
@@ -77,6 +78,11 @@ void launch_trainscan_rank_carry(const double* gathered, int rank, double* carri
 // K4: write vel (running integral) and pos (its running integral); carries may be null.
 void launch_trainscan_write(const TrainScanKernelParams& p, const void* ws, const double* carries,
                             double* vel, double* pos, hipStream_t s, bool fold = false);
+// --parity: the reference's sequential running sum over this slice, bit-exact (one
+// workgroup); out[0] = sum at the slice's last element, out[1] = at global element `want`
+// (0 if the slice does not hold it).
+void launch_trainscan_parity_serial(const TrainScanKernelParams& p, uint64_t want, double* out,
+                                    hipStream_t s);
 // One pass (K1 + K2 + K4 with a decoupled look-back): vel, pos and totals {T1, T2}.
 void launch_trainscan_onepass(const TrainScanKernelParams& p, void* ws, double* vel, double* pos,
                               double* totals, hipStream_t s);
@@ -104,6 +110,7 @@ class TrainScan {
   void enqueue_lookback(hipStream_t s);
   void exchange_carry(const double* slice, uint64_t n, double* slice_out, hipStream_t s);
   double pick_global(const double* slice, uint64_t global_index, hipStream_t s);
+  double parity_serial_element(uint64_t global_index, hipStream_t s);
 
   TrainScanConfig cfg_;
   int device_;

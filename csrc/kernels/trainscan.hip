@@ -25,6 +25,7 @@
 // outside [win_lo, win_hi) are zero.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 
 #include "miint/common.hpp"
@@ -591,6 +592,52 @@ OnePassState op_carve(void* ws, uint64_t nt) {
   return st;
 }
 
+// --parity distance, bit-exact with 4main.c: the reference's rank fills its
+// private InterpProfile over its fill window (4main.c:76-86, faccel at :262-269: truncating
+// index, separate multiply and add) and scans its element slice with ONE sequential fp64
+// running sum (4main.c:101-107 / 118-122). Any parallel scan rounds differently, and the
+// printed 6th decimal sees it (P = 16: 117642.707174 vs .707175), so the printed element is
+// reproduced with the reference's own dependency chain: the workgroup evaluates 256 samples
+// per round in parallel, lane 0 adds them in index order. out[0] = running sum at the slice's
+// last element, out[1] = running sum at global element `want` (0 if outside the slice).
+// Parity mode only (one workgroup, ~n x add latency); the rank carries are added on the host
+// in the reference's order (trainscan.cpp).
+__global__ __launch_bounds__(256) void ts_parity_serial(TrainScanKernelParams p, uint64_t want,
+                                                        double* out) {
+#pragma clang fp contract(off)
+  __shared__ double vals[256];
+  double local = 0.0, at = 0.0;
+  for (uint64_t base = 0; base < p.n; base += 256) {
+    const uint64_t j = base + threadIdx.x;
+    double v = 0.0;
+    if (j < p.n) {
+      const uint64_t i = p.i0 + j;
+      if (i >= p.win_lo && i < p.win_hi) {
+        const double t = 0.0 + p.dt * static_cast<double>(i);
+        const int k = static_cast<int>(t);
+        const double delta = t - static_cast<double>(k);
+        const double prod = (p.table[k + 1] - p.table[k]) * delta;
+        v = p.table[k] + prod;
+      }
+    }
+    vals[threadIdx.x] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint64_t m = p.n - base < 256 ? p.n - base : 256;
+      const uint64_t hit = want - p.i0 - base;  // wraps (never < m) when want is elsewhere
+      for (uint64_t q = 0; q < m; ++q) {
+        local = local + vals[q];
+        if (q == hit) at = local;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    out[0] = local;
+    out[1] = at;
+  }
+}
+
 }  // namespace
 
 size_t trainscan_workspace_bytes(uint64_t n) {
@@ -681,6 +728,18 @@ void launch_trainscan_write(const TrainScanKernelParams& p, const void* ws, cons
     ts_write<<<static_cast<unsigned>(nt), kB, 0, s>>>(p, prefix, nullptr, nullptr, carries, vel,
                                                       pos);
   }
+  MIINT_HIP(hipGetLastError());
+}
+
+void launch_trainscan_parity_serial(const TrainScanKernelParams& p, uint64_t want, double* out,
+                                    hipStream_t s) {
+  MIINT_CHECK(p.n >= 1, "parity serial scan needs a non-empty slice");
+  // every sample it may evaluate reads table[k + 1] with k = (int)(i * dt): i < win_hi and
+  // i < i0 + n, so the largest time must stay inside the table
+  const uint64_t hi = std::min<uint64_t>(p.win_hi, p.i0 + p.n);
+  MIINT_CHECK(hi == 0 || static_cast<double>(hi - 1) * p.dt < static_cast<double>(p.table_n - 1),
+              "parity serial scan: samples beyond the table");
+  ts_parity_serial<<<1, 256, 0, s>>>(p, want, out);
   MIINT_HIP(hipGetLastError());
 }
 

@@ -59,6 +59,7 @@ static ScanAlgo scan_algo_of(const std::string& s) {
 PYBIND11_MODULE(_miint, m) {
   m.doc() = "miint: MI355X-native numerical integration (HIP/gfx950 kernels, RCCL, hipGraph)";
   py::register_exception<miint::Error>(m, "MiintError", PyExc_RuntimeError);
+  install_crash_handler_from_env();
 
   // ------------------------------------------------------------------ enums
   py::enum_<Integrand>(m, "Integrand")
@@ -109,24 +110,53 @@ PYBIND11_MODULE(_miint, m) {
   m.def("wall_seconds", &wall_seconds);
 
   // ------------------------------------------------------------------ comm
-  py::class_<Comm>(m, "Comm")
-      .def(py::init([](py::bytes id, int rank, int world, int device) {
-             return new Comm(std::string(id), rank, world, device);
-           }),
-           py::arg("unique_id"), py::arg("rank"), py::arg("world"), py::arg("device"))
-      .def_static("unique_id", []() { return py::bytes(Comm::unique_id()); })
-      .def_static("version", &Comm::version)
+  py::class_<Comm>(m, "Communicator")
       .def_property_readonly("rank", &Comm::rank)
       .def_property_readonly("world", &Comm::world)
       .def_property_readonly("device", &Comm::device)
+      .def_property_readonly("kind", [](const Comm& c) { return std::string(c.kind()); })
+      .def_property_readonly("transport_world", &Comm::transport_world,
+                             "ranks the transport reports (ncclCommCount for RCCL)")
       .def("allreduce_sum", [](const Comm& c, uintptr_t send, uintptr_t recv, size_t count,
-                               uintptr_t s) { c.allreduce_sum(ptr<double>(send), ptr<double>(recv), count, stream(s)); })
+                               uintptr_t s) {
+             py::gil_scoped_release nogil;  // loopback collectives barrier across threads
+             c.allreduce_sum(ptr<double>(send), ptr<double>(recv), count, stream(s));
+           })
       .def("allgather", [](const Comm& c, uintptr_t send, uintptr_t recv, size_t count,
-                           uintptr_t s) { c.allgather(ptr<double>(send), ptr<double>(recv), count, stream(s)); })
+                           uintptr_t s) {
+             py::gil_scoped_release nogil;
+             c.allgather(ptr<double>(send), ptr<double>(recv), count, stream(s));
+           })
       .def("broadcast", [](const Comm& c, uintptr_t buf, size_t count, int root, uintptr_t s) {
+        py::gil_scoped_release nogil;
         c.broadcast(ptr<double>(buf), count, root, stream(s));
       })
+      .def("reduce_sum", [](const Comm& c, uintptr_t send, uintptr_t recv, size_t count,
+                            int root, uintptr_t s) {
+        py::gil_scoped_release nogil;
+        c.reduce_sum(ptr<double>(send), ptr<double>(recv), count, root, stream(s));
+      })
       .def("check_async", &Comm::check_async);
+  py::class_<RcclComm, Comm>(m, "Comm")
+      .def(py::init([](py::bytes id, int rank, int world, int device) {
+             return new RcclComm(std::string(id), rank, world, device);
+           }),
+           py::arg("unique_id"), py::arg("rank"), py::arg("world"), py::arg("device"))
+      .def_static("unique_id", []() { return py::bytes(RcclComm::unique_id()); })
+      .def_static("version", &RcclComm::version);
+  py::class_<LoopbackComm, Comm>(m, "LoopbackComm");
+  py::class_<LoopbackGroup, std::shared_ptr<LoopbackGroup>>(m, "LoopbackGroup",
+      "W logical ranks on one device (test transport; drive rank r from its own thread)")
+      .def(py::init(&LoopbackGroup::create), py::arg("world"), py::arg("device") = 0,
+           py::arg("timeout_s") = 120.0)
+      .def_property_readonly("world", &LoopbackGroup::world)
+      .def_property_readonly("device", &LoopbackGroup::device)
+      .def("comm", &LoopbackGroup::comm, py::arg("rank"), py::return_value_policy::reference_internal)
+      .def("barrier", &LoopbackGroup::barrier, py::arg("rank"), py::call_guard<py::gil_scoped_release>())
+      .def("mark_broken", &LoopbackGroup::mark_broken)
+      .def_property_readonly("broken", &LoopbackGroup::broken)
+      .def_property_readonly("collectives", &LoopbackGroup::collectives)
+      .def_property_readonly("graph_launches", &LoopbackGroup::graph_launches);
   m.def(
       "rendezvous_unique_id",
       [](const std::string& addr, int port, int rank, int world, double timeout_s) {
@@ -182,7 +212,11 @@ PYBIND11_MODULE(_miint, m) {
       .def_property_readonly("compute_stream", [](const RiemannPlan& p) { return reinterpret_cast<uintptr_t>(p.compute_stream()); })
       .def_property_readonly("comm_stream", [](const RiemannPlan& p) { return reinterpret_cast<uintptr_t>(p.comm_stream()); })
       .def("run", &RiemannPlan::run, py::call_guard<py::gil_scoped_release>())
-      .def("capture_graphs", &RiemannPlan::capture_graphs)
+      .def("capture_graphs", &RiemannPlan::capture_graphs, py::call_guard<py::gil_scoped_release>())
+      .def("prepare_steps", &RiemannPlan::prepare_steps, py::arg("steps"),
+           py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("graph_launches", &RiemannPlan::graph_launches)
+      .def_property_readonly("direct_steps", &RiemannPlan::direct_steps)
       .def("launch_steps", &RiemannPlan::launch_steps, py::arg("steps"), py::arg("pipeline") = true,
            py::arg("graphs") = true, py::call_guard<py::gil_scoped_release>())
       .def("sync", &RiemannPlan::sync, py::call_guard<py::gil_scoped_release>())
@@ -360,6 +394,7 @@ PYBIND11_MODULE(_miint, m) {
         py::dict d;
         d["distance"] = r.distance;
         d["sum_of_sums"] = r.sum_of_sums;
+        d["distance_scan"] = r.distance_scan;
         d["device_ms"] = r.device_ms;
         d["timeout"] = r.timeout;
         return d;
@@ -368,11 +403,15 @@ PYBIND11_MODULE(_miint, m) {
       .def_property_readonly("algo", [](const TrainScan& t) { return scan_algo_name(t.algo()); })
       .def_property_readonly("local_count", &TrainScan::local_count)
       .def("velocity_ptr", [](const TrainScan& t) { return reinterpret_cast<uintptr_t>(t.velocity()); })
-      .def("position_ptr", [](const TrainScan& t) { return reinterpret_cast<uintptr_t>(t.position()); });
+      .def("position_ptr", [](const TrainScan& t) { return reinterpret_cast<uintptr_t>(t.position()); })
+      .def("replicated_ptr", [](const TrainScan& t) { return reinterpret_cast<uintptr_t>(t.replicated()); })
+      .def_property_readonly("total", &TrainScan::total);
 
   // ------------------------------------------------------------------ oracle
   py::module_ o = m.def_submodule("oracle", "host oracles, generated fixtures, parity emulation");
   o.def("profile_table", &oracle::profile_table);
+  o.def("generated_profile_table", &oracle::generated_profile_table);
+  o.def("faccel_ref", [](double t) { return oracle::faccel_ref(oracle::profile_table(), t); });
   o.def("interp", [](double t) { return oracle::interp(oracle::profile_table(), t); });
   o.def("profile_exact_integral", &oracle::profile_exact_integral);
   o.def("analytic", &oracle::analytic, py::arg("integrand"), py::arg("a"), py::arg("b"),

@@ -1,4 +1,4 @@
-// RCCL communicator wrapper + TCP unique-id rendezvous (see miint/comm.hpp).
+// Communicators (RCCL, loopback) + TCP unique-id rendezvous (see miint/comm.hpp).
 #include "miint/comm.hpp"
 
 #include <arpa/inet.h>
@@ -9,6 +9,7 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <thread>
@@ -17,14 +18,14 @@
 
 namespace miint {
 
-std::string Comm::unique_id() {
+std::string RcclComm::unique_id() {
   ncclUniqueId id;
   MIINT_RCCL(ncclGetUniqueId(&id));
   return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
 }
 
-Comm::Comm(const std::string& id, int rank, int world, int device)
-    : rank_(rank), world_(world), device_(device) {
+RcclComm::RcclComm(const std::string& id, int rank, int world, int device)
+    : Comm(rank, world, device) {
   MIINT_CHECK(id.size() == sizeof(ncclUniqueId), "unique id must be 128 bytes");
   MIINT_CHECK(rank >= 0 && rank < world, "rank out of range");
   ncclUniqueId uid;
@@ -33,52 +34,53 @@ Comm::Comm(const std::string& id, int rank, int world, int device)
   MIINT_RCCL(ncclCommInitRank(&comm_, world, uid, rank));
 }
 
-std::vector<std::unique_ptr<Comm>> Comm::init_all(const std::vector<int>& devices) {
+std::vector<std::unique_ptr<Comm>> RcclComm::init_all(const std::vector<int>& devices) {
   const int n = static_cast<int>(devices.size());
   MIINT_CHECK(n >= 1, "need at least one device");
   std::vector<ncclComm_t> comms(n);
   MIINT_RCCL(ncclCommInitAll(comms.data(), n, devices.data()));
   std::vector<std::unique_ptr<Comm>> out;
-  for (int i = 0; i < n; ++i) {
-    std::unique_ptr<Comm> c(new Comm());
-    c->comm_ = comms[i];
-    c->rank_ = i;
-    c->world_ = n;
-    c->device_ = devices[i];
-    out.push_back(std::move(c));
-  }
+  for (int i = 0; i < n; ++i) out.emplace_back(new RcclComm(comms[i], i, n, devices[i]));
   return out;
 }
 
-Comm::~Comm() {
+RcclComm::~RcclComm() {
   if (comm_) (void)ncclCommDestroy(comm_);
 }
 
-void Comm::allreduce_sum(const double* send, double* recv, size_t count, hipStream_t s) const {
+int RcclComm::transport_world() const {
+  MIINT_CHECK(comm_ != nullptr, "communicator aborted");
+  int n = 0;
+  MIINT_RCCL(ncclCommCount(comm_, &n));
+  return n;
+}
+
+void RcclComm::allreduce_sum(const double* send, double* recv, size_t count, hipStream_t s) const {
   MIINT_RCCL(ncclAllReduce(send, recv, count, ncclFloat64, ncclSum, comm_, s));
 }
-void Comm::allgather(const double* send, double* recv, size_t count, hipStream_t s) const {
+void RcclComm::allgather(const double* send, double* recv, size_t count, hipStream_t s) const {
   MIINT_RCCL(ncclAllGather(send, recv, count, ncclFloat64, comm_, s));
 }
-void Comm::broadcast(double* buf, size_t count, int root, hipStream_t s) const {
+void RcclComm::broadcast(double* buf, size_t count, int root, hipStream_t s) const {
   MIINT_RCCL(ncclBroadcast(buf, buf, count, ncclFloat64, root, comm_, s));
 }
-void Comm::reduce_sum(const double* send, double* recv, size_t count, int root,
-                      hipStream_t s) const {
+void RcclComm::reduce_sum(const double* send, double* recv, size_t count, int root,
+                          hipStream_t s) const {
   MIINT_RCCL(ncclReduce(send, recv, count, ncclFloat64, ncclSum, root, comm_, s));
 }
-void Comm::check_async() const {
+void RcclComm::check_async() const {
+  MIINT_CHECK(comm_ != nullptr, "communicator aborted");
   ncclResult_t r = ncclSuccess;
   MIINT_RCCL(ncclCommGetAsyncError(comm_, &r));
   MIINT_RCCL(r);
 }
-void Comm::abort() const {
+void RcclComm::abort() const {
   if (comm_) (void)ncclCommAbort(comm_);
   comm_ = nullptr;
 }
-void Comm::group_start() { MIINT_RCCL(ncclGroupStart()); }
-void Comm::group_end() { MIINT_RCCL(ncclGroupEnd()); }
-std::string Comm::version() {
+void RcclComm::group_start() { MIINT_RCCL(ncclGroupStart()); }
+void RcclComm::group_end() { MIINT_RCCL(ncclGroupEnd()); }
+std::string RcclComm::version() {
   int v = 0;
   MIINT_RCCL(ncclGetVersion(&v));
   return std::to_string(v);
@@ -110,8 +112,8 @@ bool recv_all(int fd, char* p, size_t n) {
 
 std::string rendezvous_unique_id(const std::string& addr, int port, int rank, int world,
                                  double timeout_s) {
-  if (world == 1) return Comm::unique_id();
-  return rendezvous_share(addr, port, rank, world, rank == 0 ? Comm::unique_id() : std::string(),
+  if (world == 1) return RcclComm::unique_id();
+  return rendezvous_share(addr, port, rank, world, rank == 0 ? RcclComm::unique_id() : std::string(),
                           sizeof(ncclUniqueId), timeout_s);
 }
 

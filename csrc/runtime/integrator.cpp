@@ -95,7 +95,10 @@ DivMode RiemannPlan::effective_div() const {
   return miint::effective_div(cfg_.div, params_.h, cfg_.integrand, cfg_.dtype, params_.ncoef);
 }
 
-size_t RiemannPlan::graph_nodes() const { return batch_ ? batch_->num_nodes() : 0; }
+size_t RiemannPlan::graph_nodes() const {
+  auto it = graphs_.find(cfg_.slots);
+  return it == graphs_.end() ? 0 : it->second->num_nodes();
+}
 
 void RiemannPlan::enqueue_compute(hipStream_t s, int slot, int host_index) const {
   double* out = direct_ ? host_.device_ptr() + host_index : result_.get() + slot;
@@ -188,38 +191,59 @@ void RiemannPlan::enqueue_batch(hipStream_t cs, hipStream_t rs, int nsteps, bool
   MIINT_HIP(hipStreamWaitEvent(cs, ev_join_.get(), 0));
 }
 
-void RiemannPlan::capture_graphs() {
+void RiemannPlan::capture_graphs() { batch_graph(cfg_.slots); }
+
+const Graph* RiemannPlan::batch_graph(int nsteps) {
+  auto it = graphs_.find(nsteps);
+  if (it != graphs_.end()) return it->second.get();
+  if (!graph_error_.empty()) return nullptr;
   DeviceGuard g(device_);
   TraceRange tr("miint.plan.capture_graphs");
-  if (collective()) {
+  if (collective() && graphs_.empty()) {
     // RCCL sets up peer connections lazily at a communicator's first collective: run that
     // one eagerly, outside the capture, so the graph only records steady-state operations.
     comm_->allreduce_sum(result_.get(), result_.get(), 1, compute_.get());
     MIINT_HIP(hipStreamSynchronize(compute_.get()));
   }
-  batch_.reset(new Graph());
+  std::unique_ptr<Graph> gr(new Graph());
+  // A transport that captures a whole group on one stream gets the batch on that stream
+  // only (no fork/join onto the comm stream).
+  const bool one = collective() && comm_->capture_single_stream();
   try {
-    batch_->capture(compute_.get(), [&](hipStream_t s) {
-      enqueue_batch(s, comm_stream_.get(), cfg_.slots, true);
+    capture_with(collective() ? comm_ : nullptr, *gr, compute_.get(), [&](hipStream_t s) {
+      enqueue_batch(s, one ? s : comm_stream_.get(), nsteps, !one);
     });
   } catch (const Error& e) {
     // e.g. a collective that cannot be captured on this RCCL build: keep running with
     // direct stream enqueue (same results, more launch overhead) and say why.
-    batch_.reset();
     graph_error_ = e.what();
     (void)hipGetLastError();
     (void)hipStreamSynchronize(compute_.get());
     (void)hipStreamSynchronize(comm_stream_.get());
+    if (collective() && std::string(comm_->kind()) == "loopback") throw;  // group is broken
+    return nullptr;
   }
+  return (graphs_[nsteps] = std::move(gr)).get();
 }
 
-bool RiemannPlan::use_graphs(bool requested) {
-  if (requested && !batch_ && graph_error_.empty()) capture_graphs();
-  return requested && batch_ != nullptr;
+void RiemannPlan::prepare_steps(int steps) {
+  const int S = cfg_.slots;
+  if (steps >= S) batch_graph(S);
+  if (steps % S) batch_graph(steps % S);
+}
+
+// Capture (outside any timed region, if prepare_steps ran) the graphs `steps` replays.
+bool RiemannPlan::use_graphs(bool requested, int steps) {
+  if (!requested) return false;
+  const int S = cfg_.slots;
+  if (steps >= S && !batch_graph(S)) return false;
+  if (steps % S && !batch_graph(steps % S)) return false;
+  return true;
 }
 
 int RiemannPlan::host_index_of(int k, bool graphs) const {
-  return ((graphs && batch_) || bucketed()) ? k % cfg_.slots : k % host_capacity();
+  const bool batched = last_mode_ < 0 ? ((graphs && graphs_ready()) || bucketed()) : last_mode_ == 1;
+  return batched ? k % cfg_.slots : k % host_capacity();
 }
 
 void RiemannPlan::launch_steps(int steps, bool pipeline, bool graphs) {
@@ -228,11 +252,22 @@ void RiemannPlan::launch_steps(int steps, bool pipeline, bool graphs) {
   hipStream_t cs = compute_.get();
   hipStream_t rs = comm_stream_.get();
   const int S = cfg_.slots;
-  if (use_graphs(graphs)) {
-    for (int b = 0; b < steps / S; ++b) batch_->launch(cs);
-    if (steps % S) enqueue_batch(cs, rs, steps % S, pipeline);
+  const Comm* gc = collective() ? comm_ : nullptr;
+  if (use_graphs(graphs, steps)) {
+    last_mode_ = 1;
+    if (steps >= S) {
+      const Graph* full = batch_graph(S);
+      for (int b = 0; b < steps / S; ++b) launch_with(gc, *full, cs);
+      graph_launches_ += steps / S;
+    }
+    if (steps % S) {
+      launch_with(gc, *batch_graph(steps % S), cs);
+      ++graph_launches_;
+    }
     return;
   }
+  direct_steps_ += steps;
+  last_mode_ = bucketed() ? 1 : 0;
   if (bucketed()) {
     for (int k = 0; k < steps; k += S) enqueue_batch(cs, rs, std::min(S, steps - k), false);
     return;
@@ -273,7 +308,7 @@ void RiemannPlan::sync() const {
 
 StepTiming RiemannPlan::run_steps(int steps, bool pipeline, bool graphs) {
   DeviceGuard g(device_);
-  use_graphs(graphs);
+  use_graphs(graphs, steps);
   StepTiming t;
   sync();
   const double w0 = wall_seconds();

@@ -48,7 +48,14 @@ std::vector<double> make_profile() {
 
 }  // namespace
 
+extern const double kProfileData[kProfileLen];  // profile_data.cpp (bit-exact ex4vel.h)
+
 const std::vector<double>& profile_table() {
+  static const std::vector<double> t(kProfileData, kProfileData + kProfileLen);
+  return t;
+}
+
+const std::vector<double>& generated_profile_table() {
   static const std::vector<double> t = make_profile();
   return t;
 }
@@ -170,6 +177,16 @@ double cintegrate_parity(int sp, int sm) {
   return static_cast<double>(gsum);
 }
 
+// 4main.c:262-269 faccel exactly as the reference evaluates it: truncating index, delta from
+// the truncated time, separate multiply and add (the reference is built without FMA
+// contraction; so is this, by the volatile product).
+double faccel_ref(const std::vector<double>& tab, double time) {
+  const int k = static_cast<int>(time);
+  const double delta = time - static_cast<double>(k);
+  volatile double prod = (tab[k + 1] - tab[k]) * delta;
+  return tab[k] + prod;
+}
+
 TrainScanParity trainscan_parity(int P) {
   MIINT_CHECK(P >= 1, "comm size must be >= 1");
   const auto& tab = profile_table();
@@ -181,7 +198,7 @@ TrainScanParity trainscan_parity(int P) {
   auto interp_rank = [&](int q, long i) -> double {
     const long lo = static_cast<long>(q) * fill_secs * kStepsPerSec;
     const long hi = lo + static_cast<long>(fill_secs) * kStepsPerSec;
-    return (i >= lo && i < hi) ? interp(tab, 0.0 + dt * static_cast<double>(i)) : 0.0;
+    return (i >= lo && i < hi) ? faccel_ref(tab, 0.0 + dt * static_cast<double>(i)) : 0.0;
   };
   // Phase 1 on root: block q = local scan of rank q's slice + carry of block q-1's last.
   std::vector<double> ds(static_cast<size_t>(T), 0.0);

@@ -65,15 +65,29 @@ float Event::elapsed_ms(const Event& a, const Event& b) {
   return ms;
 }
 
-Graph::~Graph() {
-  if (exec_) (void)hipGraphExecDestroy(exec_);
-  if (graph_) (void)hipGraphDestroy(graph_);
-}
+Graph::~Graph() { reset(); }
 
-void Graph::capture(hipStream_t s, const std::function<void(hipStream_t)>& body) {
+void Graph::reset() {
   if (exec_) { (void)hipGraphExecDestroy(exec_); exec_ = nullptr; }
   if (graph_) { (void)hipGraphDestroy(graph_); graph_ = nullptr; }
-  MIINT_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeGlobal));
+  nodes_ = 0;
+  group_.reset();
+}
+
+void Graph::begin(hipStream_t s, hipStreamCaptureMode mode) {
+  reset();
+  MIINT_HIP(hipStreamBeginCapture(s, mode));
+}
+
+void Graph::end(hipStream_t s) {
+  MIINT_HIP(hipStreamEndCapture(s, &graph_));
+  MIINT_HIP(hipGraphGetNodes(graph_, nullptr, &nodes_));
+  MIINT_HIP(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0));
+}
+
+void Graph::capture(hipStream_t s, const std::function<void(hipStream_t)>& body,
+                    hipStreamCaptureMode mode) {
+  begin(s, mode);
   try {
     body(s);
   } catch (...) {
@@ -82,12 +96,11 @@ void Graph::capture(hipStream_t s, const std::function<void(hipStream_t)>& body)
     if (g) (void)hipGraphDestroy(g);
     throw;
   }
-  MIINT_HIP(hipStreamEndCapture(s, &graph_));
-  MIINT_HIP(hipGraphGetNodes(graph_, nullptr, &nodes_));
-  MIINT_HIP(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0));
+  end(s);
 }
 
 void Graph::launch(hipStream_t s) const {
+  MIINT_CHECK(group_ == nullptr, "a group-captured graph is launched through its communicator");
   MIINT_CHECK(exec_ != nullptr, "graph not captured");
   MIINT_HIP(hipGraphLaunch(exec_, s));
 }

@@ -74,14 +74,15 @@ double Table2DPlan::time(int iters, bool graphs) {
     stream_.sync();
     return Event::elapsed_ms(e0_, e1_) / iters;
   }
+  const Comm* gc = comm_ && world_ > 1 ? comm_ : nullptr;  // group-wide graphs (loopback)
   if (!graph_.ready())
-    graph_.capture(s, [&](hipStream_t cs) {
+    capture_with(gc, graph_, s, [&](hipStream_t cs) {
       for (int i = 0; i < kGraphSteps; ++i) enqueue(cs);
     });
   const int launches = std::max(1, (iters + kGraphSteps - 1) / kGraphSteps);
-  graph_.launch(s);  // warm
+  launch_with(gc, graph_, s);  // warm
   e0_.record(s);
-  for (int i = 0; i < launches; ++i) graph_.launch(s);
+  for (int i = 0; i < launches; ++i) launch_with(gc, graph_, s);
   e1_.record(s);
   stream_.sync();
   return Event::elapsed_ms(e0_, e1_) / (launches * kGraphSteps);

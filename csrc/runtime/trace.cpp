@@ -2,6 +2,9 @@
 #include "miint/trace.hpp"
 
 #include <dlfcn.h>
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
 
 #include <atomic>
 #include <chrono>
@@ -46,6 +49,24 @@ void load_roctx() {
 }
 
 }  // namespace
+
+namespace {
+void crash_handler(int sig) {
+  static const char msg[] = "\nmiint: fatal signal, native backtrace:\n";
+  (void)!::write(2, msg, sizeof(msg) - 1);
+  void* frames[64];
+  const int n = ::backtrace(frames, 64);
+  ::backtrace_symbols_fd(frames, n, 2);
+  ::signal(sig, SIG_DFL);
+  ::raise(sig);
+}
+}  // namespace
+
+void install_crash_handler_from_env() {
+  const char* v = std::getenv("MIINT_CRASH_TRACE");
+  if (!v || v[0] != '1') return;
+  for (int sig : {SIGSEGV, SIGBUS, SIGABRT}) ::signal(sig, crash_handler);
+}
 
 void enable_tracing(bool on) {
   g_enabled = on ? 1 : 0;

@@ -16,7 +16,8 @@ constexpr int kLocalTotal = 0;  // [0] look-back: local slice total
 constexpr int kCarry = 1;       // [1] look-back carry | [2..3] fused {C1, C2}
 constexpr int kPick = 4;        // [4] pick_global value
 constexpr int kTotals = 5;      // [5..6] fused {T1, T2}, [7] count
-constexpr int kGather = 8;      // [8 ..) gathered values (3 per rank)
+constexpr int kParity = 8;      // [8..9] --parity serial {last, at}
+constexpr int kGather = 10;     // [10 ..) gathered values (3 per rank)
 }  // namespace
 
 TrainScan::TrainScan(const TrainScanConfig& cfg, int device, const Comm* comm)
@@ -54,7 +55,7 @@ TrainScan::TrainScan(const TrainScanConfig& cfg, int device, const Comm* comm)
   }
   state_ = DeviceBuffer<char>(cfg_.algo == ScanAlgo::kLookback ? scan_state_bytes(count_)
                                                                : trainscan_workspace_bytes(count_));
-  scratch_ = DeviceBuffer<double>(kGather + 3 * static_cast<size_t>(world_));
+  scratch_ = DeviceBuffer<double>(kGather + 3 * static_cast<size_t>(world_));  // >= 2 per rank
   host_ = PinnedBuffer<double>(4);
   MIINT_HIP(hipMemset(scratch_.get(), 0, scratch_.bytes()));
   MIINT_HIP(hipMemset(state_.get(), 0, state_.bytes()));
@@ -87,6 +88,33 @@ double TrainScan::pick_global(const double* slice, uint64_t gi, hipStream_t s) {
   MIINT_HIP(hipMemcpyAsync(host_.get(), sc + kPick, sizeof(double), hipMemcpyDeviceToHost, s));
   MIINT_HIP(hipStreamSynchronize(s));
   return host_[0];
+}
+
+// --parity: the printed element exactly as 4main.c rounds it. Every rank runs the
+// reference's sequential running sum over its slice (device, bit-exact), the {last, at}
+// pairs meet in an allgather, and the root's carry fix-up (4main.c:147-154: block q adds
+// the already-carried last element of block q-1, one fp64 add per element) is replayed in
+// rank order: G_0 = last_0, G_q = last_q + G_{q-1}, element = at_q + G_{q-1}.
+double TrainScan::parity_serial_element(uint64_t gi, hipStream_t s) {
+  TrainScanKernelParams p{table_.get(), static_cast<int>(oracle::profile_table().size()),
+                          1.0 / cfg_.steps_per_sec, begin_, count_, win_lo_, win_hi_};
+  double* sc = scratch_.get();
+  launch_trainscan_parity_serial(p, gi, sc + kParity, s);
+  const int W = (comm_ && world_ > 1) ? world_ : 1;
+  PinnedBuffer<double> h(2 * static_cast<size_t>(W));
+  if (W > 1) {
+    comm_->allgather(sc + kParity, sc + kGather, 2, s);
+    MIINT_HIP(hipMemcpyAsync(h.get(), sc + kGather, 2 * W * sizeof(double), hipMemcpyDeviceToHost, s));
+  } else {
+    MIINT_HIP(hipMemcpyAsync(h.get(), sc + kParity, 2 * sizeof(double), hipMemcpyDeviceToHost, s));
+  }
+  MIINT_HIP(hipStreamSynchronize(s));
+  const uint64_t sub = count_;  // parity slices are all total / world long
+  const uint64_t q = gi / sub;
+  if (q >= static_cast<uint64_t>(W)) return 0.0;  // the unscanned residual (4main.c:91)
+  double carry = 0.0;
+  for (uint64_t b = 0; b < q; ++b) carry = b == 0 ? h[0] : h[2 * b] + carry;
+  return q == 0 ? h[1] : h[2 * q + 1] + carry;
 }
 
 void TrainScan::enqueue_fused(hipStream_t s) {
@@ -159,6 +187,8 @@ TrainScanResult TrainScan::run() {
   // 4main.c:241 prints default_sum[tablelen-2]; the complete integral is element T-1.
   const uint64_t gi = cfg_.parity ? total_ - 2 : total_ - 1;
   r.distance = pick_global(vel_.get(), gi, s) / cfg_.steps_per_sec;
+  r.distance_scan = r.distance;
+  if (cfg_.parity) r.distance = parity_serial_element(gi, s) / cfg_.steps_per_sec;
   if (cfg_.phase2 || cfg_.algo != ScanAlgo::kLookback) {
     const uint64_t last = cfg_.parity ? (total_ / world_) * world_ - 1 : total_ - 1;
     r.sum_of_sums = pick_global(pos_.get(), last, s);

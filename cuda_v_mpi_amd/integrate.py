@@ -7,7 +7,9 @@
 Backends
   ``hip``  the native runtime: gfx950 kernels, hipGraph replay, RCCL for world > 1
            (``comm="native"``: C++ RCCL communicator captured in the graph, default;
-           ``comm="torch"``: kernels on the torch stream + torch.distributed all_reduce)
+           ``comm="torch"``: kernels on the torch stream + torch.distributed all_reduce;
+           ``comm_obj=``: any native communicator, e.g. a loopback rank, see
+           parallel/loopback.py)
   ``cpu``  plain PyTorch fp64 evaluation of the rank's slice + torch.distributed (gloo)
            all_reduce. Exists so the decomposition / collective logic can be exercised
            without a GPU; it is never used implicitly.
@@ -63,7 +65,7 @@ class Integrator:
                  backend: str = "hip", ctx: DistContext | None = None, comm: str = "native",
                  fused: bool = True, grid: int = 0, slots: int = 16, a: float | None = None,
                  b: float | None = None, force_collective: bool = False, bucket: bool = True,
-                 chain: bool = True, **spec_kw):
+                 chain: bool = True, comm_obj=None, **spec_kw):
         spec = integrands.get(integrand, **spec_kw) if isinstance(integrand, str) else integrand
         if a is not None or b is not None:
             spec = dataclasses.replace(spec, a=spec.a if a is None else a,
@@ -76,6 +78,9 @@ class Integrator:
             raise ValueError("dtype must be fp64|fp32")
         self.spec, self.n, self.rule, self.dtype, self.div = spec, int(n), rule, dtype, div
         self.backend, self.comm_kind = backend, comm
+        if comm_obj is not None:  # an existing native communicator (e.g. a loopback rank)
+            ctx = DistContext(rank=comm_obj.rank, world=comm_obj.world, device=comm_obj.device,
+                              backend=comm_obj.kind)
         self.ctx = ctx or DistContext()
         self.begin, self.count = decomposition.rank_slice(self.n, self.ctx.rank, self.ctx.world)
         self._plan = None
@@ -99,7 +104,10 @@ class Integrator:
             cfg.force_collective = force_collective
             cfg.bucket = bucket
             cfg.chain = chain
-            if (self.ctx.world > 1 or force_collective) and comm == "native":
+            if comm_obj is not None:
+                self._comm = comm_obj
+                self._plan = m.RiemannPlan(cfg, comm_obj.device, comm_obj)
+            elif (self.ctx.world > 1 or force_collective) and comm == "native":
                 self._comm = native_comm(self.ctx)
                 self._plan = m.RiemannPlan(cfg, self.ctx.device, self._comm)
             else:

@@ -37,6 +37,10 @@ class TorchStepper:
         cap = self.out.numel()
         for k in range(steps):
             row = self.out[k % cap:k % cap + 1]
+            if k >= cap and self.ctx.world > 1:
+                # row k % cap is about to be overwritten: the compute stream first waits
+                # for the all-reduce of step k - cap that still reads it
+                self._works[k - cap].wait()
             kernels.riemann(self.spec, self.n, rule=self.rule, dtype=self.dtype, div=self.div,
                             i_begin=self.begin, n_local=self.count, out=row, workspace=self.ws)
             if self.ctx.world > 1:

@@ -1,12 +1,15 @@
 """Data fixtures: the 1801-sample train velocity profile (reference ``ex4vel.h``).
 
 The reference ships the table as a 211-line C header "auto-generated from Excel"
-(ex4vel.h:1-8). It is the discrete form of a 7-phase jerk-limited profile; rather than copy
-the numbers, this module regenerates them from that definition (and the native runtime does
-the same in C++, csrc/runtime/oracle.cpp): running sums of a piecewise-constant jerk of
-0.002904762 m/s^3, rounded to 15 significant digits like the spreadsheet export. The result
-matches the shipped table to 1.1e-13 everywhere (tests/test_fixtures.py checks this against
-/root/reference/ex4vel.h whenever that file is present).
+(ex4vel.h:1-8). Its values live bit-exact in ONE place, csrc/runtime/profile_data.cpp
+(hex-float literals, sha256 pinned as PROFILE_SHA256); this module reads them from that
+file's text, so Python and the native runtime share the same bits without the extension.
+
+The table is also the discrete form of a 7-phase jerk-limited profile:
+``generated_profile_table()`` rebuilds it from that definition (running sums of a
+piecewise-constant jerk of 0.002904762 m/s^3, rounded to 15 significant digits like the
+spreadsheet export) and lands within 1.1e-13 of the data everywhere — an independent check
+that the data is the profile it claims to be.
 """
 from __future__ import annotations
 
@@ -23,6 +26,9 @@ STEPS_PER_SEC = 10000
 JERK = 0.002904762
 
 REFERENCE_HEADER = "/root/reference/ex4vel.h"
+PROFILE_SHA256 = "4ebfbb500555fc9d7d054031eb7d9ec8cd813b71513480d569e2e4eee9b18a7a"
+PROFILE_DATA_SRC = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(
+    os.path.abspath(__file__)))), "csrc", "runtime", "profile_data.cpp")
 
 
 def accel_steps(i: int) -> int:
@@ -49,7 +55,7 @@ def _round15(x: float) -> float:
 
 
 @functools.lru_cache(maxsize=1)
-def _profile_tuple() -> tuple:
+def _generated_tuple() -> tuple:
     v = [0.0] * PROFILE_LEN
     vel = acc = 0.0
     kprev = 0
@@ -62,9 +68,32 @@ def _profile_tuple() -> tuple:
     return tuple(_round15(x) for x in v)
 
 
+@functools.lru_cache(maxsize=1)
+def _profile_tuple() -> tuple:
+    with open(PROFILE_DATA_SRC) as fh:
+        src = fh.read()
+    body = src[src.index("kProfileData[kProfileLen] = {") + 29:]
+    body = body[:body.index("};")]
+    vals = tuple(float.fromhex(t) for t in re.findall(r"-?0x[0-9a-fA-F.]+p[-+]?\d+", body))
+    if len(vals) != PROFILE_LEN:
+        raise ValueError(f"{PROFILE_DATA_SRC}: expected {PROFILE_LEN} values, got {len(vals)}")
+    return vals
+
+
+def profile_sha256(table: np.ndarray) -> str:
+    import hashlib
+
+    return hashlib.sha256(np.asarray(table, dtype="<f8").tobytes()).hexdigest()
+
+
 def profile_table() -> np.ndarray:
-    """Generated DefaultProfile (float64[1801]); a fresh copy each call."""
+    """DefaultProfile (float64[1801]), bit-exact; a fresh copy each call."""
     return np.array(_profile_tuple(), dtype=np.float64)
+
+
+def generated_profile_table() -> np.ndarray:
+    """The profile rebuilt from its 7-phase jerk definition (within 1.1e-13 of the data)."""
+    return np.array(_generated_tuple(), dtype=np.float64)
 
 
 def load_reference_table(path: str = REFERENCE_HEADER) -> np.ndarray | None:

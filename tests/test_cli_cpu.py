@@ -63,7 +63,38 @@ def test_native_cli_refuses_without_gpu():
         assert p.returncode == 1 and "HIP devices" in p.stderr
 
 
-def test_bench_rejects_gpus_without_torchrun():
+def _bench(*args, timeout=300):
+    return subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args],
+                          capture_output=True, text=True, timeout=timeout)
+
+
+def test_bench_spawns_ranks_without_torchrun():
+    """`python bench.py --gpus 2` is one command for 2 ranks (the reference's
+    `mpirun -np P`, riemann.cpp:62-86): the parent spawns 2 children with RANK / LOCAL_RANK
+    / WORLD_SIZE / MASTER_* set (each child asserts its env against the process group) and
+    never imports torch itself, so it cannot have initialised HIP. CPU form: gloo + torch
+    fp64 evaluation of each rank's slice."""
+    p = _bench("--gpus", "2", "--device", "cpu", "--backend", "gloo", "--samples", "2e4",
+               "--steps", "2", "--warmup", "1", "--settle-ms", "0")
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.strip().splitlines() if l.startswith("{")]
+    assert len(lines) == 1  # rank 0 only
+    js = json.loads(lines[0])
+    assert js["n_gpus"] == 2 and js["launcher"] == "spawn"
+    assert js["parent_imported_torch"] is False
+    assert len(js["per_rank_ms"]) == 2 and js["per_rank_spread_ms"] >= 0
+    assert js["config"]["N"] == 40_000 and js["config"]["parallelism"] == "dp2"
+    assert js["verified"] and abs(js["result"] - math.pi) < 1e-3
+
+
+def test_bench_spawn_propagates_rank_failure():
+    p = _bench("--gpus", "3", "--device", "cpu", "--backend", "gloo", "--integrand", "nope",
+               "--steps", "1", "--warmup", "1")
+    assert p.returncode != 0
+
+
+def test_bench_rejects_world_mismatch():
     p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2"],
-                       capture_output=True, text=True, timeout=300)
-    assert p.returncode == 2 and "torchrun" in p.stderr
+                       capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, WORLD_SIZE="3", RANK="0"))
+    assert p.returncode == 2 and "WORLD_SIZE=3" in p.stderr

@@ -23,17 +23,31 @@ def test_profile_shape_and_phases():
     assert abs(v[1800]) < 1e-12
 
 
-def test_profile_matches_reference_header_when_present():
+def test_profile_bits_pinned():
+    """The data table is bit-exact everywhere (also on the GPU box, where the reference
+    is not mounted): its sha256 is pinned."""
+    assert fixtures.profile_sha256(fixtures.profile_table()) == fixtures.PROFILE_SHA256
+
+
+def test_profile_equals_reference_header_when_present():
     ref = fixtures.load_reference_table()
     if ref is None:
         pytest.skip("reference ex4vel.h not mounted")
-    gen = fixtures.profile_table()
-    assert ref.shape == gen.shape
-    assert np.max(np.abs(ref - gen)) < 2e-13  # spreadsheet rounding noise only
+    assert np.array_equal(ref, fixtures.profile_table())  # max |ref - data| == 0
+    assert fixtures.profile_sha256(ref) == fixtures.PROFILE_SHA256
+
+
+def test_generated_profile_reproduces_the_data():
+    """The 7-phase jerk definition rebuilds the table to the spreadsheet's rounding noise."""
+    gen, data = fixtures.generated_profile_table(), fixtures.profile_table()
+    assert gen.shape == data.shape
+    assert np.max(np.abs(gen - data)) < 2e-13
 
 
 def test_native_profile_equals_python(native):
     assert np.array_equal(np.array(native.oracle.profile_table()), fixtures.profile_table())
+    assert np.array_equal(np.array(native.oracle.generated_profile_table()),
+                          fixtures.generated_profile_table())
 
 
 def test_profile_exact_integral(native):

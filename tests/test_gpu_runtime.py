@@ -37,8 +37,8 @@ def test_plan_steps_graph_and_plain_agree(cuda, graphs, fused):
 def test_chained_batches_equal_fused_bitwise(cuda, name, collective):
     """Graph batches of chained kernels (kernel k finalizes step k-1, a finalize closes the
     batch; no ticket) give every step exactly the fused kernel's value: 21 steps in batches
-    of 8 (two graph replays + 5 enqueued directly), on one GPU and through the bucketed
-    1-rank RCCL stage."""
+    of 8 (two replays of the 8-step graph + one of a 5-step graph), on one GPU and through
+    the bucketed 1-rank RCCL stage."""
     dtype = "fp32" if name.endswith("_fp32") else "fp64"
     name = name.split("_")[0]
     kw = dict(n=50_000_017, rule="mid", slots=8, force_collective=collective, dtype=dtype)
@@ -48,6 +48,7 @@ def test_chained_batches_equal_fused_bitwise(cuda, name, collective):
         assert it.plan.chained == chain
         it.run_steps(21, pipeline=True, graphs=True)
         assert it.plan.graphs_ready, it.plan.graph_error
+        assert it.plan.graph_launches == 3 and it.plan.direct_steps == 0
         for k in range(13, 21):
             assert it.plan.host_result(it.plan.host_index_of(k, True)) == want, (chain, k)
 
@@ -325,3 +326,12 @@ def test_bench_contract(native, cuda):
         assert k in js
     assert js["n_gpus"] == 1 and js["steps"] == 20 and js["verified"]
     assert js["value"] > 1e11
+    # the 20 timed steps are ONE replay of a captured 20-step graph (slots = 48)
+    assert js["graph_replays_timed"] == 1 and js["direct_steps_timed"] == 0
+    assert js["config"]["graphs"] is True
+    # the record carries what the headline rests on: IEEE-division speed and per-point ulp
+    assert js["ieee_div_value"] > 1e11 and js["ieee_div"]["abs_err"] < 2e-9
+    assert js["per_point_max_ulp"] <= 5.0
+    b3 = js["baseline3_strong_1e10"]
+    assert b3["N"] == 10**10 and abs(b3["abs_err"] - 1e-10) < 1e-13 and b3["value"] > 1e11
+    assert js["rccl_version"] and js["per_rank_ms"] and js["launcher"] == "single"

@@ -1,0 +1,274 @@
+"""Every world > 1 code path on ONE GPU, through the loopback communicator.
+
+The reference's subject is its P-rank decomposition: riemann.cpp:62-86 (master/worker
+partition + MPI_Send/Recv gather) and 4main.c:95-221 (slice scans, root carries, Bcast).
+RCCL refuses two ranks on one device and the pool has one GPU, so these tests run the real
+plans (RiemannPlan, TrainScan, Table2DPlan: rank slicing, bucketed / per-step reductions,
+group-captured graphs, allgather-fed rank carries, parity windows, --replicate) with W
+logical ranks on device 0 (LoopbackComm: one thread per rank, stream-ordered collectives)
+and compare with the single-rank run.
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+import torch
+
+from cuda_v_mpi_amd import Integrator
+from cuda_v_mpi_amd.parallel import loopback
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(REPO, "build", "bin")
+N = 10**9
+
+
+@pytest.fixture(scope="module")
+def single_pi4(cuda):
+    return Integrator("pi4", n=N, rule="mid").run().value
+
+
+def _riemann_ranks(world, steps, *, graphs, bucket, pipeline=True, fused=True, slots=16,
+                   integrand="pi4", n=N, rule="mid", dtype="fp64"):
+    def body(rank, comm):
+        it = Integrator(integrand, n=n, rule=rule, dtype=dtype, comm_obj=comm, bucket=bucket,
+                        fused=fused, slots=slots)
+        p = it.plan
+        assert p.world == world and p.rank == rank and p.collective
+        if graphs:
+            p.prepare_steps(steps)
+        p.launch_steps(steps, pipeline, graphs)
+        p.sync()
+        vals = [p.host_result(p.host_index_of(k, graphs)) for k in range(max(0, steps - slots), steps)]
+        return dict(vals=vals, begin=p.begin, count=p.count, graph_launches=p.graph_launches,
+                    direct=p.direct_steps, graph_error=p.graph_error)
+    out = loopback.run_ranks(world, body)
+    return out, loopback.run_ranks.last_group
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("mode", ["bucketed_graph", "bucketed_direct", "perstep_graph",
+                                  "perstep_direct_pipelined", "perstep_direct_serial",
+                                  "unfused_bucketed_graph"])
+def test_riemann_loopback_matches_single(single_pi4, world, mode):
+    """37 steps (two full batches of 16 + a remainder batch of 5): every rank of every step
+    holds the global sum, equal to the one-rank integration of the same N to 1e-15."""
+    graphs = "graph" in mode
+    out, grp = _riemann_ranks(world, 37, graphs=graphs, bucket="bucketed" in mode,
+                              pipeline="serial" not in mode, fused="unfused" not in mode)
+    # the ranks' slices tile [0, N) exactly
+    assert sum(o["count"] for o in out) == N
+    assert [o["begin"] for o in out] == sorted(o["begin"] for o in out)
+    for r, o in enumerate(out):
+        assert o["graph_error"] == ""
+        for v in o["vals"]:
+            assert v == pytest.approx(single_pi4, rel=1e-15, abs=0), (r, mode)
+        # every rank holds bitwise the same global values
+        assert o["vals"] == out[0]["vals"]
+        if graphs:
+            assert o["graph_launches"] == 3 and o["direct"] == 0  # 2 x 16 + one 5-step batch
+        else:
+            assert o["graph_launches"] == 0 and o["direct"] == 37
+    assert grp.collectives > 0
+    assert grp.graph_launches == (3 if graphs else 0)
+
+
+@pytest.mark.parametrize("integrand,dtype", [("sin", "fp64"), ("table", "fp64"),
+                                             ("train", "fp64"), ("pi4", "fp32")])
+def test_riemann_loopback_integrands(cuda, integrand, dtype):
+    n = 300_000_007
+    want = Integrator(integrand, n=n, rule="mid", dtype=dtype).run().value
+    out, _ = _riemann_ranks(3, 20, graphs=True, bucket=True, integrand=integrand, n=n,
+                            dtype=dtype)
+    tol = 1e-15 if dtype == "fp64" else 1e-9
+    for o in out:
+        assert o["vals"][-1] == pytest.approx(want, rel=tol, abs=1e-15)
+
+
+def _trainscan(native, world, **cfg_kw):
+    def mk():
+        c = native.TrainScanConfig()
+        for k, v in cfg_kw.items():
+            setattr(c, k, v)
+        return c
+
+    def body(rank, comm):
+        ts = native.TrainScan(mk(), 0, comm)
+        r = ts.run()
+        r2 = ts.run()  # a second pipeline on the same plan: workspaces re-armed
+        if ts.algo == "fused":  # fixed-order tile prefixes: bitwise reproducible
+            assert r2["distance"] == r["distance"] and r2["sum_of_sums"] == r["sum_of_sums"]
+        else:  # decoupled look-back sums whatever predecessor state it finds first
+            assert r2["distance"] == pytest.approx(r["distance"], rel=1e-15, abs=0)
+            assert r2["sum_of_sums"] == pytest.approx(r["sum_of_sums"], rel=1e-15, abs=0)
+        out = dict(r, begin=ts.local_begin, count=ts.local_count, algo=ts.algo)
+        if cfg_kw.get("replicate"):
+            full = torch.empty(ts.total, dtype=torch.float64, device="cuda")
+            torch.cuda.synchronize()
+            native_copy(full, ts.replicated_ptr())
+            out["replicated"] = full.cpu().numpy()
+        return out
+    return loopback.run_ranks(world, body)
+
+
+def native_copy(dst: torch.Tensor, src_ptr: int) -> None:
+    """Device-to-device copy from a raw device address into a torch tensor."""
+    import ctypes
+
+    hip = ctypes.CDLL("libamdhip64.so")
+    rc = hip.hipMemcpy(ctypes.c_void_p(dst.data_ptr()), ctypes.c_void_p(src_ptr),
+                       ctypes.c_size_t(dst.numel() * dst.element_size()), 3)  # D2D
+    assert rc == 0
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("algo", ["fused", "lookback", "onepass"])
+def test_trainscan_loopback_matches_single(native, cuda, world, algo):
+    """The distributed scan: local scans, an allgather of the per-rank totals (fused: one
+    {T1, T2, count} triple per rank) and on-device rank carries, on W logical ranks. The
+    distance and the sum of sums equal the one-rank run (the carries regroup the additions of
+    an 18e6-term running sum, and the look-back scans already round run to run at ~1e-15, so
+    equality is to a few ulp of the running sums, not bitwise)."""
+    c = native.TrainScanConfig()
+    c.algo = algo
+    one = native.TrainScan(c, 0).run()
+    out = _trainscan(native, world, algo=algo)
+    assert sum(o["count"] for o in out) == 18_000_000
+    for o in out:
+        assert o["timeout"] == 0
+        assert o["algo"] == ("fused" if algo == "onepass" else algo)  # onepass needs totals first
+        assert o["distance"] == pytest.approx(one["distance"], rel=4e-15, abs=0)
+        assert o["sum_of_sums"] == pytest.approx(one["sum_of_sums"], rel=4e-15, abs=0)
+
+
+@pytest.mark.parametrize("world,want", [(1, "122000.004030"), (2, None), (7, "0.000000"),
+                                        (16, "117642.707174")])
+def test_trainscan_loopback_parity(native, cuda, world, want):
+    """4main.c's partitions on the real GPU plan (fill by whole seconds per rank, scan by
+    elements, residual never scanned, element T-2 printed): P = 7 -> 0.000000 and
+    P = 16 -> 117642.707174, equal to the host emulation for any P."""
+    host = native.oracle.trainscan_parity(world)
+    out = _trainscan(native, world, parity=True, algo="lookback")
+    for o in out:
+        # the printed element: the reference's sequential running sums on the device,
+        # carries replayed in rank order -> bit-identical to the host emulation
+        assert o["distance"] == host[0]
+        # the parallel scan of the same partitions agrees to its rounding
+        assert o["distance_scan"] == pytest.approx(host[0], rel=1e-12, abs=1e-9)
+        if want is not None:
+            assert "%f" % o["distance"] == want
+        assert o["sum_of_sums"] == pytest.approx(host[1], rel=1e-12, abs=1e-6)
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_trainscan_loopback_replicate(native, cuda, world):
+    """--replicate (4main.c:157, every rank ends with the whole table): the all-gathered
+    table on every rank equals the one-rank velocity array."""
+    one = native.TrainScan(native.TrainScanConfig(), 0)
+    one.run()
+    ref = torch.empty(18_000_000, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    native_copy(ref, one.velocity_ptr())
+    ref = ref.cpu().numpy()
+    out = _trainscan(native, world, replicate=True)
+    for o in out:
+        np.testing.assert_allclose(o["replicated"], ref, rtol=2e-15, atol=1e-9)
+        assert np.array_equal(o["replicated"], out[0]["replicated"])
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("grid", [4096, 1000])
+def test_table2d_loopback_matches_single(native, cuda, world, grid):
+    """The 2-D field (BASELINE #5) with its sample rows split over W ranks and the partials
+    meeting in one all-reduce, direct and as group-captured graph replays."""
+    want = native.Table2DPlan(grid).run()
+
+    def body(rank, comm):
+        p = native.Table2DPlan(grid, 1800.0, 0, comm)
+        v = p.run()
+        ms = p.time(64, True)
+        v2 = p.run()
+        return dict(v=v, v2=v2, ms=ms, rows=(p.row0, p.row1))
+    out = loopback.run_ranks(world, body)
+    assert sum(o["rows"][1] - o["rows"][0] for o in out) == grid
+    for o in out:
+        assert o["v"] == pytest.approx(want, rel=1e-15, abs=0)
+        assert o["v2"] == o["v"] and o["ms"] > 0
+    assert loopback.run_ranks.last_group.graph_launches >= 3
+
+
+def test_loopback_collectives_raw(native, cuda):
+    """allreduce / reduce / allgather (also in place) / broadcast on raw device buffers,
+    against their definitions."""
+    W, n = 5, 1000
+
+    def body(rank, comm):
+        s = torch.cuda.Stream()
+        x = torch.arange(n, dtype=torch.float64, device="cuda") * (rank + 1) + rank
+        y = torch.empty_like(x)
+        g = torch.empty(W * n, dtype=torch.float64, device="cuda")
+        b = torch.full((n,), float(rank), dtype=torch.float64, device="cuda")
+        red = torch.zeros_like(x)
+        torch.cuda.synchronize()
+        h = s.cuda_stream
+        comm.allreduce_sum(x.data_ptr(), y.data_ptr(), n, h)
+        comm.allgather(x.data_ptr(), g.data_ptr(), n, h)
+        comm.broadcast(b.data_ptr(), n, 2, h)
+        comm.reduce_sum(x.data_ptr(), red.data_ptr(), n, 1, h)
+        gi = torch.zeros(W * n, dtype=torch.float64, device="cuda")
+        gi[rank * n:(rank + 1) * n] = x
+        torch.cuda.synchronize()
+        comm.allgather(gi[rank * n:].data_ptr(), gi.data_ptr(), n, h)  # in place
+        s.synchronize()
+        return [t.cpu().numpy() for t in (x, y, g, b, red, gi)]
+    out = loopback.run_ranks(W, body)
+    xs = [o[0] for o in out]
+    total = sum(xs)
+    for r, o in enumerate(out):
+        np.testing.assert_array_equal(o[1], total)
+        np.testing.assert_array_equal(o[2], np.concatenate(xs))
+        np.testing.assert_array_equal(o[3], np.full(n, 2.0))
+        np.testing.assert_array_equal(o[5], np.concatenate(xs))
+    np.testing.assert_array_equal(out[1][4], total)
+
+
+def test_loopback_failure_breaks_group_not_hangs(native, cuda):
+    """A rank that dies before a collective must not leave the others waiting forever: the
+    group is marked broken and every rank's next barrier raises."""
+    def body(rank, comm):
+        if rank == 1:
+            raise ValueError("rank 1 died")
+        x = torch.zeros(4, dtype=torch.float64, device="cuda")
+        comm.allreduce_sum(x.data_ptr(), x.data_ptr(), 4, torch.cuda.current_stream().cuda_stream)
+    with pytest.raises(RuntimeError, match="rank 1 died"):
+        loopback.run_ranks(3, body, timeout_s=30.0)
+
+
+def _cli(args, timeout=300):
+    p = subprocess.run(args, capture_output=True, text=True, timeout=timeout)
+    assert p.returncode == 0, p.stderr[-3000:]
+    return p.stdout.strip().splitlines()
+
+
+@pytest.mark.parametrize("world,want", [(7, "0.000000"), (16, "117642.707174")])
+def test_cli_trainscan_loopback_parity(native, cuda, world, want):
+    """`trainscan --parity --loopback P` prints 4main.c's P-rank output from the GPU plan."""
+    lines = _cli([os.path.join(BIN, "trainscan"), "--parity", "--loopback", str(world),
+                  "--algo", "lookback"])
+    assert lines[0] == "Step size of 10000"
+    assert lines[2] == f"Total distance traveled = {want}"
+
+
+def test_cli_riemann_and_table2d_loopback(native, cuda):
+    one = json.loads(_cli([os.path.join(BIN, "riemann"), "--integrand", "pi4", "--rule", "mid",
+                           "--json"])[-1])
+    many = json.loads(_cli([os.path.join(BIN, "riemann"), "--integrand", "pi4", "--rule",
+                            "mid", "--json", "--loopback", "8", "--iters", "20"])[-1])
+    assert many["gpus"] == 8
+    assert many["result"] == pytest.approx(one["result"], rel=1e-15, abs=0)
+    t2 = json.loads(_cli([os.path.join(BIN, "miint"), "table2d", "--loopback", "3"])[-1])
+    assert t2["rel_err_vs_oracle"] < 1e-14

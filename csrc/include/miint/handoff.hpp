@@ -1,11 +1,25 @@
-// Last-workgroup hand-off for one-launch reductions (Riemann fused kernel, 2-D field).
+// Cross-workgroup hand-offs inside one launch: write-once slots + last-workgroup ticket.
 //
-// Every workgroup publishes its partial with an agent-scope (sc1, write-through) store,
-// drains it (s_waitcnt vmcnt(0)), then takes a ticket with an agent-scope atomic. The
-// workgroup that draws the last ticket acquires (agent fence: buffer_inv sc1) and reduces
-// all partials in index order with sc1 loads — the R1 hand-off of cdna_hip_programming.md
-// §6 G16. Placement-independent: correctness never depends on which XCD a block lands on,
-// and the index-ordered final sum is bitwise reproducible.
+// Write-once slot protocol (used by every in-kernel hand-off: the fused Riemann and 2-D
+// field reductions here, the look-back scans in scan.hip and trainscan.hip, the trainscan
+// block-prefix ticket): a slot holds kUnset — a NaN bit pattern no arithmetic produces —
+// until its producer stores the value with ONE relaxed agent-scope atomic store; a consumer
+// reads THE SLOT ITSELF with relaxed agent-scope atomic loads until it is no longer kUnset.
+// The value is its own flag, so there is no second object whose visibility would have to be
+// ordered against it: C++/HIP coherence of a single atomic object is all the protocol needs
+// (no release/acquire pair, no reliance on address or control dependencies, nothing a
+// compiler may reorder). On gfx950 the relaxed agent-scope forms are sc1 (L1-bypassing,
+// write-through) stores and loads, so a consumer never sees a stale line either
+// (MI355X_MICROARCH.md "Valid forms"); the producer's s_waitcnt vmcnt(0) before its ticket
+// only makes the slot usually visible by the time the ticket is counted (no spin). Slots
+// are re-armed to kUnset by their single consumer once read, or by the launcher's memset.
+// Every wait is bounded: a slot still unset after kSlotSpinLimit polls reads as NaN (and
+// raises the caller's timeout word), which poisons the result instead of hanging the GPU.
+//
+// Last-workgroup ticket (fused reductions): every workgroup publishes its partial into its
+// slot, then takes a ticket with an agent-scope atomic; the workgroup that draws the last
+// ticket reduces all slots in index order (bitwise reproducible, placement-independent —
+// cdna_hip_programming.md §6 G16) and re-arms them.
 //
 // Two-level ticket: workgroup b counts in group b % G (G = kTicketGroups counters, each on
 // its own 256-byte line); the last arrival of each group takes the top-level ticket, and the
@@ -22,9 +36,46 @@ namespace miint {
 
 constexpr int kFinalBatch = 16;  // partial loads in flight per thread
 
+// ---------------------------------------------------------------- write-once slots
+// both 32-bit halves kUnsetSlotWord (kernels.hpp), so hipMemsetD32 fills slots; a quiet NaN
+// with a payload no arithmetic produces
+constexpr unsigned long long kUnsetBits =
+    (static_cast<unsigned long long>(kUnsetSlotWord) << 32) | kUnsetSlotWord;
+constexpr unsigned kSlotSpinLimit = 1u << 26;
+
+__device__ __forceinline__ bool slot_unset(double v) {
+  return static_cast<unsigned long long>(__double_as_longlong(v)) == kUnsetBits;
+}
+__device__ __forceinline__ double slot_unset_value() {
+  return __longlong_as_double(static_cast<long long>(kUnsetBits));
+}
+__device__ __forceinline__ double slot_load(const double* p) {
+  return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void slot_store(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Wait until the slot is set; NaN (and *timeout = 1, if given) after kSlotSpinLimit polls.
+__device__ __forceinline__ double slot_wait(const double* p, double first,
+                                            unsigned* timeout = nullptr) {
+  double v = first;
+  unsigned spins = 0;
+  while (slot_unset(v)) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > kSlotSpinLimit) {
+      if (timeout) __hip_atomic_store(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return __builtin_nan("");
+    }
+    v = slot_load(p);
+  }
+  return v;
+}
+
 // Thread t sums partials t, t + BLOCK, t + 2 BLOCK, ... in increasing order. The loads of a
 // batch are all issued before the first add (a plain loop waited for every load).
-template <int BLOCK, bool AGENT_SCOPE>
+// SLOTS = true: the partials are write-once slots of this launch (waited for, see above);
+// false: plain loads of partials a previous launch wrote (the kernel boundary orders them).
+template <int BLOCK, bool SLOTS>
 __device__ __forceinline__ double ordered_partials(const double* partials, int n) {
   double v = 0.0;
   for (int base = 0; base < n; base += kFinalBatch * BLOCK) {
@@ -32,29 +83,41 @@ __device__ __forceinline__ double ordered_partials(const double* partials, int n
 #pragma unroll
     for (int k = 0; k < kFinalBatch; ++k) {
       const int i = base + k * BLOCK + static_cast<int>(threadIdx.x);
-      if constexpr (AGENT_SCOPE)
-        r[k] = i < n ? __hip_atomic_load(&partials[i], __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT)
-                     : 0.0;
+      if constexpr (SLOTS)
+        r[k] = i < n ? slot_load(&partials[i]) : 0.0;
       else
         r[k] = i < n ? partials[i] : 0.0;
     }
 #pragma unroll
-    for (int k = 0; k < kFinalBatch; ++k) v += r[k];
+    for (int k = 0; k < kFinalBatch; ++k) {
+      if constexpr (SLOTS) {
+        const int i = base + k * BLOCK + static_cast<int>(threadIdx.x);
+        if (slot_unset(r[k])) r[k] = slot_wait(&partials[i], r[k]);
+      }
+      v += r[k];
+    }
   }
   return v;
 }
 
-// Publish this workgroup's partial s (thread 0's value) as partials[bid] and take the
+// Re-arm slots [0, n) after this thread's ordered_partials<BLOCK, true> read them (each
+// thread re-arms exactly the slots it read).
+template <int BLOCK>
+__device__ __forceinline__ void rearm_slots(double* partials, int n) {
+  for (int i = static_cast<int>(threadIdx.x); i < n; i += BLOCK)
+    slot_store(&partials[i], slot_unset_value());
+}
+
+// Publish this workgroup's partial s (thread 0's value) into slot partials[bid] and take the
 // ticket. Returns true, uniformly across the workgroup, in the last of `nblocks`
-// workgroups, which may then read every partial with ordered_partials<BLOCK, true>.
-// `flag` is a __shared__ int of the caller.
+// workgroups, which may then read every slot with ordered_partials<BLOCK, true> (and must
+// re-arm them with rearm_slots). `flag` is a __shared__ int of the caller.
 __device__ __forceinline__ bool publish_and_ticket(double s, double* partials, unsigned* ticket,
                                                    unsigned bid, unsigned nblocks, int* flag) {
   const unsigned G = nblocks < kTicketGroups ? nblocks : kTicketGroups;
   if (threadIdx.x == 0) {
-    __hip_atomic_store(&partials[bid], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    slot_store(&partials[bid], s);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // latency only: see the header
     const unsigned g = bid % G;
     const unsigned members = (nblocks - g + G - 1) / G;
     const unsigned prev = __hip_atomic_fetch_add(ticket + g * kTicketStride, 1u,
@@ -68,13 +131,7 @@ __device__ __forceinline__ bool publish_and_ticket(double s, double* partials, u
     *flag = last;
   }
   __syncthreads();
-  if (!*flag) return false;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  return true;
+  return *flag != 0;  // the slots are read as atomics: no acquire fence needed
 }
 
 // Re-arm the ticket (last workgroup only: every group has arrived, nobody else touches it).

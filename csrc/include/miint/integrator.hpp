@@ -167,7 +167,8 @@ class RiemannPlan {
   RiemannParams params_{};
   double scale_ = 1.0;
   LaunchShape shape_{1, kRiemannBlock};
-  DeviceBuffer<double> partials_;  // 2 x grid: chained batches alternate halves
+  DeviceBuffer<double> partials_;  // 2 x grid: chained batches alternate halves (+ 2-kernel)
+  DeviceBuffer<double> slots_;     // grid write-once slots of the fused (ticket) kernel
   DeviceBuffer<double> result_;
   DeviceBuffer<unsigned int> ticket_;
   DeviceBuffer<double> table_;

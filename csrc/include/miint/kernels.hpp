@@ -79,6 +79,10 @@ void launch_riemann_partials(const RiemannParams& p, DType dtype, DivMode div,
 void launch_finalize(const double* partials, int n, double scale, double* out,
                      hipStream_t stream);
 
+// Fill `count` doubles with the write-once slots' unset pattern (handoff.hpp).
+constexpr unsigned kUnsetSlotWord = 0xFFFAFFFAu;
+void fill_unset_slots(double* p, size_t count, hipStream_t stream);
+
 // Ticket of the one-launch reduction: kTicketGroups group counters and one top counter,
 // each on its own 256-byte line (kTicketWords unsigned words in all). A single counter
 // serialised 2048 same-address atomics at the end of every launch (~14 us at N = 1e8).
@@ -86,9 +90,10 @@ constexpr int kTicketGroups = 16;
 constexpr int kTicketStride = 64;  // words between counters (256 B)
 constexpr int kTicketWords = (kTicketGroups + 1) * kTicketStride;
 
-// One-launch variant: partials + last-workgroup ticket reduction (agent-scope hand-off,
-// cdna_hip_programming.md §6 G16). `ticket` (kTicketWords words) must be zero before the
-// first launch; the last workgroup re-arms it.
+// One-launch variant: partials + last-workgroup ticket reduction (write-once slots,
+// handoff.hpp; cdna_hip_programming.md §6 G16). `ticket` (kTicketWords words) must be zero
+// and `partials` (grid doubles) filled with the unset pattern (fill_unset_slots) before the
+// first launch; the last workgroup re-arms both.
 void launch_riemann_fused(const RiemannParams& p, DType dtype, DivMode div, LaunchShape shape,
                           const double* table, int table_n, double* partials,
                           unsigned int* ticket, double scale, double* out, hipStream_t stream);
@@ -165,7 +170,8 @@ int table2d_grid(const Table2DParams& p);
 const char* table2d_path(const Table2DParams& p);
 void launch_table2d_partials(const Table2DParams& p, double* partials, hipStream_t stream);
 // One launch: partials + last-workgroup reduction into out[0] (ticket: kTicketWords words,
-// zero before the first launch, re-armed by the kernel; partials: table2d_grid(p) doubles).
+// zero before the first launch; partials: table2d_grid(p) doubles filled with the unset
+// pattern (fill_unset_slots); both re-armed by the kernel).
 void launch_table2d_fused(const Table2DParams& p, double* partials, unsigned* ticket,
                           double* out, hipStream_t stream);
 void launch_outer_product(const double* v, int n, double* table, hipStream_t stream);

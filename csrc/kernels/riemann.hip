@@ -340,8 +340,8 @@ __global__ __launch_bounds__(kFinalBlock) void finalize_kernel(const double* par
 }
 
 // ---------------------------------------------------------------------------- fused (ticket)
-// One launch: partials, then the last-workgroup hand-off of handoff.hpp (sc1 publish,
-// two-level ticket, acquire, index-ordered sum) — bitwise identical to partials + finalize.
+// One launch: partials, then the last-workgroup hand-off of handoff.hpp (write-once slots,
+// two-level ticket, index-ordered sum, re-arm) — bitwise identical to partials + finalize.
 template <DivMode M, class F>
 __device__ __forceinline__ void fused_body(const RiemannParams& p, const double* table,
                                            int table_n, double* partials, unsigned int* ticket,
@@ -353,6 +353,7 @@ __device__ __forceinline__ void fused_body(const RiemannParams& p, const double*
   const double s = block_sum<B>(lane_sum<M>(p, f), red);
   if (!publish_and_ticket(s, partials, ticket, blockIdx.x, gridDim.x, &is_last)) return;
   const double v = ordered_partials<B, true>(partials, static_cast<int>(gridDim.x));
+  rearm_slots<B>(partials, static_cast<int>(gridDim.x));
   const double tot = block_sum<B>(v, red);
   if (threadIdx.x == 0) out[0] = tot * scale;
   rearm_ticket(ticket, gridDim.x);

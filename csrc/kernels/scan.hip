@@ -8,15 +8,19 @@
 // wave-parallel look-back over up to 64 predecessors at a time. Across GPUs the only
 // traffic is an allgather of one fp64 total per rank (csrc/runtime/trainscan.cpp).
 //
-// Inter-workgroup protocol (cdna_hip_programming.md §6 G16, MI355X_MICROARCH.md "Valid
-// forms"): per-tile value written with an agent-scope sc1 store, drained with
-// s_waitcnt vmcnt(0), then the status flag written with an sc1 store by the same lane;
-// consumers poll flags and read values with sc1 loads only. Tile ids come from an atomic
-// counter so a tile only ever waits on tiles that are already running (forward progress
-// under any dispatch order). State words are zeroed by hipMemsetAsync every launch.
+// Inter-workgroup protocol: the write-once slots of handoff.hpp. Per tile there are two
+// slots, its aggregate and its inclusive prefix, each filled with the unset pattern by the
+// launcher's memset and written ONCE per launch with a relaxed agent-scope atomic store; a
+// look-back lane polls its predecessor's prefix slot, then its aggregate slot, and the value
+// it reads is the status — no separate flag whose ordering against the value the memory
+// model would have to guarantee. Tile ids come from an atomic counter so a tile only ever
+// waits on tiles that are already running (forward progress under any dispatch order).
+// Bounded spins: a predecessor that never publishes makes the prefix NaN (every later
+// output poisoned) and raises the timeout word, which every host path turns into an error.
 #include <hip/hip_runtime.h>
 
 #include "miint/common.hpp"
+#include "miint/handoff.hpp"
 #include "miint/kernels.hpp"
 #include "miint/trainscan.hpp"
 #include "miint/wave_reduce.hpp"
@@ -27,32 +31,12 @@ namespace {
 constexpr int kB = 256;
 constexpr int kItems = 16;                 // per thread
 constexpr int kTileN = kB * kItems;        // 4096 elements = 32 KB per tile
-constexpr unsigned kFlagAgg = 1u, kFlagPrefix = 2u;
-constexpr unsigned kSpinLimit = 1u << 26;  // bounded spins: never hang the GPU
-
 struct ScanState {
   unsigned* counter;   // dynamic tile id
-  unsigned* flags;     // per tile: 0 none, 1 aggregate, 2 inclusive prefix
-  double* agg;         // per tile aggregate
-  double* pref;        // per tile inclusive prefix
-  unsigned* timeout;   // set if any spin gave up (checked by tests)
+  double* agg;         // per tile aggregate (write-once slot)
+  double* pref;        // per tile inclusive prefix (write-once slot)
+  unsigned* timeout;   // set if any spin gave up (every host path turns it into an error)
 };
-
-__device__ __forceinline__ void store_sc1(double* p, double v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double load_sc1(const double* p) {
-  return __hip_atomic_load(const_cast<double*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned load_flag(const unsigned* p) {
-  return __hip_atomic_load(const_cast<unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void publish(ScanState st, unsigned tile, double* slot, double v,
-                                        unsigned flag) {
-  store_sc1(slot + tile, v);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __hip_atomic_store(st.flags + tile, flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // Wave 0: exclusive prefix of `tile` by look-back (lanes examine tile-1-lane).
 __device__ double look_back(ScanState st, unsigned tile) {
@@ -61,22 +45,28 @@ __device__ double look_back(ScanState st, unsigned tile) {
   long base = static_cast<long>(tile) - 1;
   for (;;) {
     const long j = base - lane;
-    unsigned f = kFlagPrefix;  // lanes past the front act as "prefix 0"
+    bool is_pref = true;  // lanes past the front act as "prefix 0"
     double v = 0.0;
     if (j >= 0) {
       unsigned spins = 0;
-      while ((f = load_flag(st.flags + j)) == 0u) {
+      for (;;) {
+        v = slot_load(st.pref + j);
+        if (!slot_unset(v)) break;
+        v = slot_load(st.agg + j);
+        if (!slot_unset(v)) {
+          is_pref = false;
+          break;
+        }
         __builtin_amdgcn_s_sleep(1);
-        if (++spins > kSpinLimit) {
+        if (++spins > kSlotSpinLimit) {
           __hip_atomic_store(st.timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          f = kFlagPrefix;
+          v = __builtin_nan("");
           break;
         }
       }
-      if (j >= 0) v = (f == kFlagPrefix) ? load_sc1(st.pref + j) : load_sc1(st.agg + j);
     }
     // first lane (closest predecessor) holding an inclusive prefix
-    const unsigned long long pm = __ballot(f == kFlagPrefix);
+    const unsigned long long pm = __ballot(is_pref);
     const int stop = pm ? __builtin_ctzll(pm) : 64;
     const double mine = lane <= stop ? v : 0.0;
     excl += wave_sum(mine);
@@ -124,11 +114,11 @@ __device__ __forceinline__ void scan_tile(ScanState st, uint64_t n, double* out,
   if (threadIdx.x < 64) {
     double excl = 0.0;
     if (tile == 0) {
-      if (threadIdx.x == 0) publish(st, tile, st.pref, total, kFlagPrefix);
+      if (threadIdx.x == 0) slot_store(st.pref + tile, total);
     } else {
-      if (threadIdx.x == 0) publish(st, tile, st.agg, total, kFlagAgg);
+      if (threadIdx.x == 0) slot_store(st.agg + tile, total);
       excl = look_back(st, tile);
-      if (threadIdx.x == 0) publish(st, tile, st.pref, excl + total, kFlagPrefix);
+      if (threadIdx.x == 0) slot_store(st.pref + tile, excl + total);
     }
     if (threadIdx.x == 0) prefix_sh = excl + (carry_in ? carry_in[0] : 0.0);
   }
@@ -185,29 +175,28 @@ __global__ void exclusive_carry_kernel(const double* totals, int rank, double* o
   out[0] = c;
 }
 
-size_t align16(size_t b) { return (b + 15) & ~size_t(15); }
-
+// State: {counter, timeout} (16 B, zeroed per launch), then the agg and pref slots (filled
+// with the unset pattern per launch).
 ScanState carve(void* state, uint64_t ntiles) {
   char* p = static_cast<char*>(state);
   ScanState st;
   st.counter = reinterpret_cast<unsigned*>(p);
   st.timeout = reinterpret_cast<unsigned*>(p + 4);
-  p += 16;
-  st.flags = reinterpret_cast<unsigned*>(p);
-  p += align16(ntiles * sizeof(unsigned));
-  st.agg = reinterpret_cast<double*>(p);
-  p += align16(ntiles * sizeof(double));
-  st.pref = reinterpret_cast<double*>(p);
+  st.agg = reinterpret_cast<double*>(p + 16);
+  st.pref = st.agg + ntiles;
   return st;
 }
 
-size_t zeroed_bytes(uint64_t ntiles) { return 16 + align16(ntiles * sizeof(unsigned)); }
+void arm_state(void* state, uint64_t ntiles, hipStream_t stream) {
+  MIINT_HIP(hipMemsetAsync(state, 0, 16, stream));
+  fill_unset_slots(reinterpret_cast<double*>(static_cast<char*>(state) + 16), 2 * ntiles, stream);
+}
 
 }  // namespace
 
 size_t scan_state_bytes(uint64_t n) {
   const uint64_t nt = (n + kTileN - 1) / kTileN;
-  return 16 + align16(nt * sizeof(unsigned)) + 2 * align16(nt * sizeof(double));
+  return 16 + 2 * nt * sizeof(double);
 }
 
 void launch_inclusive_scan(const double* in, double* out, uint64_t n, void* state,
@@ -216,7 +205,7 @@ void launch_inclusive_scan(const double* in, double* out, uint64_t n, void* stat
   const uint64_t nt = (n + kTileN - 1) / kTileN;
   MIINT_CHECK(nt < (1u << 31), "scan too large");
   ScanState st = carve(state, nt);
-  MIINT_HIP(hipMemsetAsync(state, 0, zeroed_bytes(nt), stream));
+  arm_state(state, nt, stream);
   scan_kernel<<<static_cast<unsigned>(nt), kB, 0, stream>>>(in, out, n, st, carry_in);
   MIINT_HIP(hipGetLastError());
 }
@@ -234,7 +223,7 @@ void launch_interp_scan_window(const double* table, int table_n, double dt, uint
   MIINT_CHECK(table_n >= 2 && table_n <= kMaxTable, "table size must be in [2, 2048]");
   const uint64_t nt = (n + kTileN - 1) / kTileN;
   ScanState st = carve(state, nt);
-  MIINT_HIP(hipMemsetAsync(state, 0, zeroed_bytes(nt), stream));
+  arm_state(state, nt, stream);
   interp_scan_kernel<<<static_cast<unsigned>(nt), kB, 0, stream>>>(
       table, table_n, dt, i0, n, win_lo, win_hi, out, st, carry_in);
   MIINT_HIP(hipGetLastError());

@@ -160,7 +160,9 @@ __global__ __launch_bounds__(kB) void table2d_kernel(Table2DParams p, double* pa
   } else {
     const unsigned nb = gridDim.x * gridDim.y;
     if (!publish_and_ticket(s, partials, ticket, bid, nb, &is_last)) return;
-    const double tot = block_sum<kB>(ordered_partials<kB, true>(partials, static_cast<int>(nb)), red);
+    const double v = ordered_partials<kB, true>(partials, static_cast<int>(nb));
+    rearm_slots<kB>(partials, static_cast<int>(nb));
+    const double tot = block_sum<kB>(v, red);
     if (threadIdx.x == 0) out[0] = tot;
     rearm_ticket(ticket, nb);
   }
@@ -310,7 +312,9 @@ __global__ __launch_bounds__(kB) void table2d_stream_kernel(Table2DParams p, int
   } else {
     const unsigned nb = gridDim.x * gridDim.y;
     if (!publish_and_ticket(s, partials, ticket, bid, nb, &is_last)) return;
-    const double tot = block_sum<kB>(ordered_partials<kB, true>(partials, static_cast<int>(nb)), red);
+    const double v = ordered_partials<kB, true>(partials, static_cast<int>(nb));
+    rearm_slots<kB>(partials, static_cast<int>(nb));
+    const double tot = block_sum<kB>(v, red);
     if (threadIdx.x == 0) out[0] = tot;
     rearm_ticket(ticket, nb);
   }

@@ -29,6 +29,8 @@
 #include <cmath>
 
 #include "miint/common.hpp"
+#include "miint/handoff.hpp"
+#include "miint/kernels.hpp"
 #include "miint/trainscan.hpp"
 #include "miint/wave_reduce.hpp"
 
@@ -266,34 +268,27 @@ __global__ __launch_bounds__(kB) void ts_tile_scan_closed(TrainScanKernelParams 
     }
     return;
   }
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0) {  // write-once slots (handoff.hpp), filled unset by the launcher
     double* g = cs.agg + 4 * blockIdx.x;
-    __hip_atomic_store(g, A, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(g + 1, B, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(g + 2, N, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    slot_store(g, A);
+    slot_store(g + 1, B);
+    slot_store(g + 2, N);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // latency only
     const unsigned prev =
         __hip_atomic_fetch_add(cs.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     is_last = (prev == gridDim.x - 1);
   }
   __syncthreads();
   if (!is_last) return;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
   // exclusive scan over the block aggregates, kB at a time (affine: Q += N PB + B)
   double cp = 0.0, cq = 0.0;
   for (uint32_t b0 = 0; b0 < gridDim.x; b0 += kB) {
     const uint32_t b = b0 + threadIdx.x;
     const bool vb = b < gridDim.x;
     const double* g = cs.agg + 4 * b;
-    const double a = vb ? __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
-    const double bb =
-        vb ? __hip_atomic_load(g + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
-    const double nb =
-        vb ? __hip_atomic_load(g + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+    const double a = vb ? slot_wait(g, slot_load(g)) : 0.0;
+    const double bb = vb ? slot_wait(g + 1, slot_load(g + 1)) : 0.0;
+    const double nb = vb ? slot_wait(g + 2, slot_load(g + 2)) : 0.0;
     double ta, tq;
     const double pb = cp + (block_inclusive_scan<kB>(a, red, &ta) - a);
     __syncthreads();
@@ -450,28 +445,24 @@ __global__ __launch_bounds__(kB) void ts_write(TrainScanKernelParams p, const f6
 // predecessor s that published its inclusive state (P_s, Q_s): (P_s, Q_s + 4096 (t-1-s) P_s).
 // Commutative terms: the wave sums them with DPP exactly like the 1-component look-back.
 // Samples are generated once and HBM sees only the 16 B/sample of vel + pos stores.
-// Tile ids come from an atomic counter (forward progress under any dispatch order); spins
-// are bounded and report through the timeout word. The look-back sums whatever mix of
+// Tile ids come from an atomic counter (forward progress under any dispatch order). The tile
+// states are write-once slots (handoff.hpp): {A, B} aggregate and {P, Q} prefix pairs, each
+// component its own slot; a lane that sees a pair's first component set waits for the
+// second. Spins are bounded (NaN + the timeout word). The look-back sums whatever mix of
 // aggregates and prefixes it finds, so the last bits may differ run to run; the 3-kernel
 // path (ScanAlgo::kFused) is the bitwise-deterministic one.
-constexpr unsigned kOpAgg = 1u, kOpPrefix = 2u;
-constexpr unsigned kOpSpinLimit = 1u << 26;
 constexpr size_t kOpHeader = 64;  // counter @0, timeout @4
 
 struct OnePassState {
   unsigned* counter;
   unsigned* timeout;
-  unsigned* flags;  // per tile: 0 none, 1 aggregate, 2 inclusive prefix
-  double* agg;      // per tile {A, B}
-  double* pref;     // per tile inclusive {P, Q}
+  double* agg;      // per tile {A, B} (slots)
+  double* pref;     // per tile inclusive {P, Q} (slots)
 };
 
-__device__ __forceinline__ void op_publish(const OnePassState& st, double* slot, unsigned tile,
-                                           double x, double y, unsigned flag) {
-  __hip_atomic_store(slot + 2 * tile, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(slot + 2 * tile + 1, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __hip_atomic_store(st.flags + tile, flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void op_publish(double* slot, unsigned tile, double x, double y) {
+  slot_store(slot + 2 * tile, x);
+  slot_store(slot + 2 * tile + 1, y);
 }
 
 // Wave 0: exclusive {P, Q} of `tile` (lanes examine tile-1-lane, 64 at a time).
@@ -481,24 +472,33 @@ __device__ f64x2 op_look_back(const OnePassState& st, unsigned tile) {
   long base = static_cast<long>(tile) - 1;
   for (;;) {
     const long j = base - lane;
-    unsigned f = kOpPrefix;  // lanes past the front act as "prefix 0"
+    bool is_pref = true;  // lanes past the front act as "prefix 0"
     double a = 0.0, b = 0.0;
     if (j >= 0) {
       unsigned spins = 0;
-      while ((f = __hip_atomic_load(st.flags + j, __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT)) == 0u) {
+      const double* src = nullptr;
+      for (;;) {
+        a = slot_load(st.pref + 2 * j);
+        if (!slot_unset(a)) {
+          src = st.pref + 2 * j;
+          break;
+        }
+        a = slot_load(st.agg + 2 * j);
+        if (!slot_unset(a)) {
+          src = st.agg + 2 * j;
+          is_pref = false;
+          break;
+        }
         __builtin_amdgcn_s_sleep(1);
-        if (++spins > kOpSpinLimit) {
+        if (++spins > kSlotSpinLimit) {
           __hip_atomic_store(st.timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          f = kOpPrefix;
+          a = __builtin_nan("");
           break;
         }
       }
-      const double* src = (f == kOpPrefix ? st.pref : st.agg) + 2 * j;
-      a = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      b = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      b = src ? slot_wait(src + 1, slot_load(src + 1), st.timeout) : a;
     }
-    const unsigned long long pm = __ballot(f == kOpPrefix);
+    const unsigned long long pm = __ballot(is_pref);
     const int stop = pm ? __builtin_ctzll(pm) : 64;
     const double gap = static_cast<double>(kTile) * static_cast<double>(static_cast<long>(tile) - 1 - j);
     const bool use = lane <= stop && j >= 0;
@@ -553,12 +553,12 @@ __global__ __launch_bounds__(kB) void ts_onepass(TrainScanKernelParams p, OnePas
   if (threadIdx.x < kWave) {
     f64x2 ex = {0.0, 0.0};
     if (tile > 0) {
-      if (threadIdx.x == 0) op_publish(st, st.agg, tile, A, Bt, kOpAgg);
+      if (threadIdx.x == 0) op_publish(st.agg, tile, A, Bt);
       ex = op_look_back(st, tile);
     }
     if (threadIdx.x == 0) {
       const double pi = ex.x + A, qi = fma(nt, ex.x, ex.y + Bt);
-      op_publish(st, st.pref, tile, pi, qi, kOpPrefix);
+      op_publish(st.pref, tile, pi, qi);
       pre_sh[0] = ex.x;
       pre_sh[1] = ex.y;
       if (tile + 1 == ntiles) {
@@ -585,9 +585,7 @@ OnePassState op_carve(void* ws, uint64_t nt) {
   OnePassState st;
   st.counter = reinterpret_cast<unsigned*>(p);
   st.timeout = reinterpret_cast<unsigned*>(p + 4);
-  st.flags = reinterpret_cast<unsigned*>(p + kOpHeader);
-  char* q = p + kOpHeader + ((nt * sizeof(unsigned) + 15) & ~uint64_t(15));
-  st.agg = reinterpret_cast<double*>(q);
+  st.agg = reinterpret_cast<double*>(p + kOpHeader);
   st.pref = st.agg + 2 * nt;
   return st;
 }
@@ -642,8 +640,9 @@ __global__ __launch_bounds__(256) void ts_parity_serial(TrainScanKernelParams p,
 
 size_t trainscan_workspace_bytes(uint64_t n) {
   const uint64_t nt = (n + kTile - 1) / kTile;
-  // 3-kernel path: {sums, prefix} f64x2 per tile; one-pass: header + flags + {agg, pref}
-  return kOpHeader + ((nt * sizeof(unsigned) + 15) & ~uint64_t(15)) + 2 * nt * sizeof(f64x2);
+  // 3-kernel path: {sums, prefix} f64x2 per tile + per-block {prefix, aggregates, ticket};
+  // one-pass: header + {agg, pref} slot pairs per tile. The one-pass layout is the larger.
+  return kOpHeader + 2 * nt * sizeof(f64x2);
 }
 
 void launch_trainscan_onepass(const TrainScanKernelParams& p, void* ws, double* vel, double* pos,
@@ -657,7 +656,8 @@ void launch_trainscan_onepass(const TrainScanKernelParams& p, void* ws, double* 
   const uint64_t nt = (p.n + kTile - 1) / kTile;
   MIINT_CHECK(nt < (1u << 31), "slice too large");
   const OnePassState st = op_carve(ws, nt);
-  MIINT_HIP(hipMemsetAsync(ws, 0, kOpHeader + ((nt * sizeof(unsigned) + 15) & ~uint64_t(15)), s));
+  MIINT_HIP(hipMemsetAsync(ws, 0, kOpHeader, s));
+  fill_unset_slots(st.agg, 4 * nt, s);
   ts_onepass<<<static_cast<unsigned>(nt), kB, 0, s>>>(p, st, static_cast<unsigned>(nt), vel, pos,
                                                        totals);
   MIINT_HIP(hipGetLastError());
@@ -690,9 +690,12 @@ void launch_trainscan_local(const TrainScanKernelParams& p, void* ws, double* to
     if (use_fold(p, fold))
       ts_tile_scan_closed<false><<<static_cast<unsigned>((nt + kB - 1) / kB), kB, 0, s>>>(
           p, sps, static_cast<uint32_t>(nt), cs, totals);
-    else
+    else {
+      // the block-aggregate hand-off: write-once slots, armed here (a few doubles per block)
+      fill_unset_slots(cs.agg, 4 * ((nt + kB - 1) / kB), s);
       ts_tile_scan_closed<true><<<static_cast<unsigned>((nt + kB - 1) / kB), kB, 0, s>>>(
           p, sps, static_cast<uint32_t>(nt), cs, totals);
+    }
     MIINT_HIP(hipGetLastError());
     return;
   }

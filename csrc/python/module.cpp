@@ -76,6 +76,10 @@ PYBIND11_MODULE(_miint, m) {
       .value("series_direct", DivMode::kSeriesDirect);
 
   m.attr("TICKET_WORDS") = kTicketWords;
+  m.attr("UNSET_SLOT_WORD") = kUnsetSlotWord;
+  m.def("fill_unset_slots", [](uintptr_t p, size_t count, uintptr_t s) {
+    fill_unset_slots(ptr<double>(p), count, stream(s));
+  });
   m.attr("RIEMANN_TILE") = kRiemannTile;
   m.attr("RIEMANN_BLOCK") = kRiemannBlock;
   m.def("series_ok", &series_ok);

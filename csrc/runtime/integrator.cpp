@@ -68,6 +68,8 @@ RiemannPlan::RiemannPlan(const RiemannConfig& cfg, int device, const Comm* comm)
   }
 
   partials_ = DeviceBuffer<double>(2 * static_cast<size_t>(shape_.grid));
+  slots_ = DeviceBuffer<double>(static_cast<size_t>(shape_.grid));
+  fill_unset_slots(slots_.get(), slots_.size(), nullptr);
   result_ = DeviceBuffer<double>(static_cast<size_t>(cfg.slots));
   ticket_ = DeviceBuffer<unsigned int>(kTicketWords);
   MIINT_HIP(hipMemset(ticket_.get(), 0, ticket_.bytes()));
@@ -95,9 +97,10 @@ DivMode RiemannPlan::effective_div() const {
   return miint::effective_div(cfg_.div, params_.h, cfg_.integrand, cfg_.dtype, params_.ncoef);
 }
 
-size_t RiemannPlan::graph_nodes() const {
-  auto it = graphs_.find(cfg_.slots);
-  return it == graphs_.end() ? 0 : it->second->num_nodes();
+size_t RiemannPlan::graph_nodes() const {  // the largest captured batch graph
+  size_t n = 0;
+  for (const auto& kv : graphs_) n = std::max(n, kv.second->num_nodes());
+  return n;
 }
 
 void RiemannPlan::enqueue_compute(hipStream_t s, int slot, int host_index) const {
@@ -105,7 +108,7 @@ void RiemannPlan::enqueue_compute(hipStream_t s, int slot, int host_index) const
   const int tn = static_cast<int>(cfg_.table.size());
   if (cfg_.fused) {
     launch_riemann_fused(params_, cfg_.dtype, cfg_.div, shape_, table_.get(), tn,
-                         partials_.get(), ticket_.get(), scale_, out, s);
+                         slots_.get(), ticket_.get(), scale_, out, s);
   } else {
     launch_riemann_partials(params_, cfg_.dtype, cfg_.div, shape_, table_.get(), tn,
                             partials_.get(), s);

@@ -1,6 +1,8 @@
 // Native HIP runtime layer implementation (see miint/runtime.hpp).
 #include "miint/runtime.hpp"
 
+#include "miint/kernels.hpp"
+
 namespace miint {
 
 namespace {
@@ -30,6 +32,12 @@ DeviceInfo device_info(int device) {
   d.l2_bytes = prop.l2CacheSize;
   d.max_threads_per_cu = prop.maxThreadsPerMultiProcessor;
   return d;
+}
+
+void fill_unset_slots(double* p, size_t count, hipStream_t stream) {
+  if (count == 0) return;
+  MIINT_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(p),
+                              static_cast<int>(kUnsetSlotWord), 2 * count, stream));
 }
 
 void set_device(int device) { MIINT_HIP(hipSetDevice(device)); }

@@ -32,6 +32,7 @@ Table2DPlan::Table2DPlan(const Table2DConfig& cfg, int device, const Comm* comm)
   const Table2DParams p{table_.get(), n, n, cfg.extent, cfg.extent, cfg.grid, cfg.grid,
                         row0_, std::max(row1_, row0_ + 1)};
   partials_ = DeviceBuffer<double>(static_cast<size_t>(table2d_grid(p)));
+  fill_unset_slots(partials_.get(), partials_.size(), stream_.get());  // fused kernel's slots
   result_ = DeviceBuffer<double>(1);
   ticket_ = DeviceBuffer<unsigned int>(kTicketWords);
   MIINT_HIP(hipMemset(ticket_.get(), 0, ticket_.bytes()));

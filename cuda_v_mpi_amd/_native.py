@@ -28,7 +28,7 @@ def extension_path() -> str:
 
 def _sources() -> list[str]:
     pats = ["csrc/kernels/*.hip", "csrc/runtime/*.cpp", "csrc/python/*.cpp",
-            "csrc/include/miint/*.hpp", "Makefile"]
+            "csrc/include/miint/*.hpp"]
     out: list[str] = []
     for p in pats:
         out.extend(glob.glob(os.path.join(_REPO, p)))

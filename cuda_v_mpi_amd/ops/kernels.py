@@ -89,13 +89,22 @@ def finalize(partials: torch.Tensor, scale: float, out: torch.Tensor | None = No
     return out
 
 
+def unset_slots(n: int, device) -> torch.Tensor:
+    """n fp64 write-once slots in their unset state (csrc/include/miint/handoff.hpp): what the
+    one-launch reductions hand partials over in; the consuming workgroup re-arms them."""
+    word = native().UNSET_SLOT_WORD
+    bits = (word << 32) | word
+    return torch.full((n,), bits - (1 << 64), dtype=torch.int64, device=device).view(torch.float64)
+
+
 class FusedWorkspace:
-    """Partials + ticket for the one-launch reduction; reuse across calls (graph-safe)."""
+    """Partials (write-once slots) + ticket for the one-launch reduction; reuse across
+    calls (graph-safe: the kernel re-arms both)."""
 
     def __init__(self, grid: int, device: torch.device | None = None):
         dev = device or _device()
         self.grid = grid
-        self.partials = torch.empty(grid, dtype=torch.float64, device=dev)
+        self.partials = unset_slots(grid, dev)
         self.ticket = torch.zeros(native().TICKET_WORDS, dtype=torch.int32, device=dev)
 
 
@@ -264,7 +273,8 @@ def table2d(table: torch.Tensor, X: float, Y: float, gx: int, gy: int, row0: int
     row1 = gy if row1 is None else row1
     m = native()
     grid = m.table2d_grid(nx, ny, X, Y, gx, gy, row0, row1)
-    partials = torch.empty(grid, dtype=torch.float64, device=table.device)
+    partials = (unset_slots(grid, table.device) if fused
+                else torch.empty(grid, dtype=torch.float64, device=table.device))
     if not fused:
         m.launch_table2d_partials(table.data_ptr(), nx, ny, X, Y, gx, gy, row0, row1,
                                   partials.data_ptr(), _stream())

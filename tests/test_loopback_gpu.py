@@ -157,11 +157,12 @@ def test_trainscan_loopback_parity(native, cuda, world, want):
         # the printed element: the reference's sequential running sums on the device,
         # carries replayed in rank order -> bit-identical to the host emulation
         assert o["distance"] == host[0]
-        # the parallel scan of the same partitions agrees to its rounding
-        assert o["distance_scan"] == pytest.approx(host[0], rel=1e-12, abs=1e-9)
+        # the parallel scan of the same partitions agrees up to the sequential sum's drift
+        # (P = 1: the reference's 18e6-term running sum prints ...004030, exact ...004000)
+        assert o["distance_scan"] == pytest.approx(host[0], rel=5e-10, abs=1e-9)
         if want is not None:
             assert "%f" % o["distance"] == want
-        assert o["sum_of_sums"] == pytest.approx(host[1], rel=1e-12, abs=1e-6)
+        assert o["sum_of_sums"] == pytest.approx(host[1], rel=5e-10, abs=1e-6)
 
 
 @pytest.mark.parametrize("world", [2, 3, 8])

@@ -91,6 +91,9 @@ struct RiemannParams {
   // trig[8 + j] = sin(k_j h) for k_j = j + 1/2 (j < 8), then cos(c0 h), sin(c0 h) for the
   // sub-tile centres c0 = 8, 24, ..., 88 (integrands.hpp, struct AngleSeries)
   double trig[kSinTrig];
+  // The same table rounded to fp32 by the host (the fp32 sin / train series, integrands_f32.hpp):
+  // kernel arguments, so the packed constants stay in SGPR pairs instead of VGPR copies.
+  float trig32[kSinTrig];
 };
 
 }  // namespace miint

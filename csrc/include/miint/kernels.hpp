@@ -47,12 +47,18 @@ inline DivMode effective_div(DivMode d, double h, Integrand f) {
 
 constexpr int kPolySeriesMaxCoeffs = 8;  // polynomials up to degree 7 have a series path
 
-// With the dtype (the fp32 path has one series form, 192-sample tiles of first order, and
-// otherwise IEEE division) and the polynomial's coefficient count (Taylor-pair tiles for up
+// With the dtype (the fp32 paths: pi4's 192-sample first-order tiles where series_ok, and
+// the packed-fp32 forms of the other integrands' series tiles) and the polynomial's
+// coefficient count (Taylor-pair tiles for up
 // to kPolySeriesMaxCoeffs coefficients, exact for any h; Horner per sample otherwise).
 inline DivMode effective_div(DivMode d, double h, Integrand f, DType t, int ncoef = 0) {
-  if (t == DType::kF32)
-    return (d == DivMode::kIeee || !series_ok(h)) ? DivMode::kIeee : DivMode::kSeries;
+  if (t == DType::kF32) {  // fp32: one series form per integrand (integrands_f32.hpp)
+    if (d == DivMode::kIeee) return DivMode::kIeee;
+    if (f == Integrand::kPi4) return series_ok(h) ? DivMode::kSeries : DivMode::kIeee;
+    if (f == Integrand::kPoly)
+      return (ncoef >= 1 && ncoef <= kPolySeriesMaxCoeffs) ? DivMode::kSeries : DivMode::kIeee;
+    return DivMode::kSeries;  // sin, train velocity, table: exact for any h
+  }
   if (f == Integrand::kPoly)
     return (d == DivMode::kSeries && ncoef >= 1 && ncoef <= kPolySeriesMaxCoeffs)
                ? DivMode::kSeries

@@ -24,6 +24,7 @@
 #include "miint/common.hpp"
 #include "miint/handoff.hpp"
 #include "miint/integrands.hpp"
+#include "miint/integrands_f32.hpp"
 #include "miint/kernels.hpp"
 #include "miint/wave_reduce.hpp"
 
@@ -70,11 +71,7 @@ __device__ __forceinline__ double lane_sum(const RiemannParams& p, const F& f) {
 constexpr int kMaxTable = 2048;  // LDS budget for a 1-D table: 16 KB
 
 // ---------------------------------------------------------------------------- fp32 functor
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) {
-  return __builtin_elementwise_fma(a, b, c);
-}
+// (the other integrands' fp32 functors: integrands_f32.hpp)
 
 // 4/(1+x^2) in packed fp32 (v_pk_fma_f32 pairs). Tile base comes in as fp64 so sample
 // coordinates do not collapse at 1e9 samples; in-tile offsets and all
@@ -243,6 +240,43 @@ template <> struct Maker<TrainVel> {
     return f;
   }
 };
+template <> struct Maker<SinF32> {
+  static constexpr int kLds = 1;
+  __device__ static SinF32 make(const RiemannParams& p, const double*, int, double*) {
+    SinF32 f;
+    f.init(p.trig32);
+    return f;
+  }
+};
+template <> struct Maker<TrainVelF32> {
+  static constexpr int kLds = 1;
+  __device__ static TrainVelF32 make(const RiemannParams& p, const double*, int, double*) {
+    TrainVelF32 f;
+    f.init_trig(p.trig32);
+    f.inv_ts = 1.0 / p.p0;
+    f.vs = p.p1;
+    return f;
+  }
+};
+template <int NC> struct Maker<PolyF32<NC>> {
+  static constexpr int kLds = 1;
+  __device__ static PolyF32<NC> make(const RiemannParams& p, const double*, int, double*) {
+    PolyF32<NC> f;
+    f.init(p.coef, p.ncoef);
+    return f;
+  }
+};
+template <> struct Maker<TableF32> {
+  static constexpr int kLds = kMaxTable;
+  __device__ static TableF32 make(const RiemannParams&, const double* table, int n, double* lds) {
+    for (int i = threadIdx.x; i < n; i += B) lds[i] = table[i];
+    __syncthreads();
+    TableF32 f;
+    f.tab = lds;
+    f.nseg = n - 1;
+    return f;
+  }
+};
 template <> struct Maker<Table> {
   static constexpr int kLds = kMaxTable;
   __device__ static Table make(const RiemannParams&, const double* table, int n, double* lds) {
@@ -259,11 +293,14 @@ template <> struct Maker<Table> {
 // table from global memory instead of staging all of it in every workgroup's LDS.
 template <DivMode M, class F>
 constexpr int lds_words() {
-  if constexpr (__is_same(F, Table) && M == DivMode::kSeries) return 1;
+  if constexpr ((__is_same(F, Table) || __is_same(F, TableF32)) && M == DivMode::kSeries) return 1;
   else return Maker<F>::kLds;
 }
 template <class F> struct IsPoly { static constexpr bool value = false; };
 template <int NC> struct IsPoly<Poly<NC>> { static constexpr bool value = true; };
+template <int NC> struct IsPoly<PolyF32<NC>> { static constexpr bool value = true; };
+template <class F> struct IsPolyF64 { static constexpr bool value = false; };
+template <int NC> struct IsPolyF64<Poly<NC>> { static constexpr bool value = true; };
 
 template <DivMode M, class F>
 __device__ __forceinline__ F make_functor(const RiemannParams& p, const double* table, int n,
@@ -275,6 +312,12 @@ __device__ __forceinline__ F make_functor(const RiemannParams& p, const double* 
   } else if constexpr (__is_same(F, Table) && M == DivMode::kSeries) {
     Table f{{}, table, n - 1};
     f.init();
+    f.inv_h = 1.0 / p.h;
+    return f;
+  } else if constexpr (__is_same(F, TableF32) && M == DivMode::kSeries) {
+    TableF32 f;
+    f.tab = table;
+    f.nseg = n - 1;
     f.inv_h = 1.0 / p.h;
     return f;
   } else {
@@ -296,8 +339,11 @@ constexpr bool occupancy_hint() {
   if constexpr (__is_same(F, Pi4)) return M == DivMode::kSeriesDirect;
   else if constexpr (__is_same(F, Pi4F32)) return M == DivMode::kIeee;
   else if constexpr (__is_same(F, Sin)) return M == DivMode::kIeee;
+  else if constexpr (__is_same(F, PolyF32<16>)) return true;
   else if constexpr (IsPoly<F>::value) return M == DivMode::kSeries;
-  else return __is_same(F, TrainVel) || __is_same(F, Table);
+  else if constexpr (__is_same(F, SinF32) || __is_same(F, TrainVelF32))
+    return M == DivMode::kSeries;
+  else return __is_same(F, TrainVel) || __is_same(F, Table) || __is_same(F, TableF32);
 }
 
 // Partials kernel: one fp64 partial per workgroup.
@@ -431,7 +477,7 @@ __global__ __launch_bounds__(B) void point_values_kernel(RiemannParams p, const 
     if constexpr (M == DivMode::kSeries && __is_same(F, Pi4)) {
       // exactly the operations Pi4::tile_acc applies to sample u
       v = full ? f.series_point(xm, p.h, u) : f.point(x);
-    } else if constexpr (M == DivMode::kSeries && IsPoly<F>::value) {
+    } else if constexpr (M == DivMode::kSeries && IsPolyF64<F>::value) {
       v = full ? f.series_point(xm, u) : f.point(x);
     } else if constexpr (M == DivMode::kSeries && __is_same(F, Table)) {
       v = full ? f.series_point(xm, p.h, u) : f.point(x);
@@ -486,10 +532,35 @@ template <template <DivMode, class> class Op, class... A>
 void dispatch(const RiemannParams& p, DType dtype, DivMode m, A&&... a) {
   const Integrand f = static_cast<Integrand>(p.integrand);
   if (dtype == DType::kF32) {
-    MIINT_CHECK(f == Integrand::kPi4, "fp32 path is implemented for the pi4 integrand");
-    if (m == DivMode::kIeee) Op<DivMode::kIeee, Pi4F32>::run(a...);
-    else Op<DivMode::kSeries, Pi4F32>::run(a...);
-    return;
+    const bool ser = m == DivMode::kSeries;
+    switch (f) {
+      case Integrand::kPi4:
+        if (ser) Op<DivMode::kSeries, Pi4F32>::run(a...);
+        else Op<DivMode::kIeee, Pi4F32>::run(a...);
+        return;
+      case Integrand::kSin:
+        if (ser) Op<DivMode::kSeries, SinF32>::run(a...);
+        else Op<DivMode::kIeee, SinF32>::run(a...);
+        return;
+      case Integrand::kTrainVel:
+        if (ser) Op<DivMode::kSeries, TrainVelF32>::run(a...);
+        else Op<DivMode::kIeee, TrainVelF32>::run(a...);
+        return;
+      case Integrand::kTable:
+        if (ser) Op<DivMode::kSeries, TableF32>::run(a...);
+        else Op<DivMode::kIeee, TableF32>::run(a...);
+        return;
+      case Integrand::kPoly:  // buckets as fp64
+        if (ser && p.ncoef <= 4) Op<DivMode::kSeries, PolyF32<4>>::run(a...);
+        else if (ser && p.ncoef <= 6) Op<DivMode::kSeries, PolyF32<6>>::run(a...);
+        else if (ser && p.ncoef == 7) Op<DivMode::kSeries, PolyF32<7>>::run(a...);
+        else if (ser && p.ncoef <= 8) Op<DivMode::kSeries, PolyF32<8>>::run(a...);
+        else if (p.ncoef <= 4) Op<DivMode::kIeee, PolyF32<4>>::run(a...);
+        else if (p.ncoef <= 8) Op<DivMode::kIeee, PolyF32<8>>::run(a...);
+        else Op<DivMode::kIeee, PolyF32<16>>::run(a...);
+        return;
+    }
+    fail("unknown integrand", __FILE__, __LINE__);
   }
   switch (f) {
     case Integrand::kPi4:
@@ -594,6 +665,7 @@ static RiemannParams prepared(const RiemannParams& p, DivMode eff) {
     }
   }
   if ((f == Integrand::kSin || f == Integrand::kTrainVel) && eff == DivMode::kSeries) {
+    // (the fp32 functors read the same table, rounded to fp32 on the device)
     const long double delta =
         f == Integrand::kSin ? static_cast<long double>(p.h)
                              : static_cast<long double>(p.h) / static_cast<long double>(p.p0);
@@ -607,6 +679,7 @@ static RiemannParams prepared(const RiemannParams& p, DivMode eff) {
       q.trig[2 * AngleSeries<12>::kPairs + 2 * i] = static_cast<double>(cosl(c0 * delta));
       q.trig[2 * AngleSeries<12>::kPairs + 2 * i + 1] = static_cast<double>(sinl(c0 * delta));
     }
+    for (int i = 0; i < kSinTrig; ++i) q.trig32[i] = static_cast<float>(q.trig[i]);
   }
   return q;
 }

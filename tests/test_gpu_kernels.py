@@ -53,6 +53,36 @@ def test_riemann_fp32_small_and_odd_n(cuda, n):
     assert got == pytest.approx(want, rel=2e-6)
 
 
+F32_SPECS = [integrands.sin(), integrands.train(), integrands.table(), integrands.poly(seed=3)]
+
+
+@pytest.mark.parametrize("spec", F32_SPECS, ids=lambda s: s.name)
+@pytest.mark.parametrize("n", [1000, 1_000_003, 10**9])
+@pytest.mark.parametrize("div", ["series", "ieee"])
+def test_fp32_integrands_vs_fp64(cuda, spec, n, div):
+    """Packed-fp32 forms of the reference's own integrands (sin: cintegrate.cu:47-72; the
+    velocity table: cintegrate.cu:74-98) and of the train velocity and polynomial, against
+    the fp64 torch reference (N <= 1e6) or the fp64 kernel (N = 1e9, itself checked against
+    torch in test_riemann_vs_torch and the series tests). Every sample is evaluated in fp32
+    from an fp64 tile base and folded into fp64; the measured relative errors are ~1e-8 and
+    below (profiles/r2/fp32_errors.jsonl), the bound here is 2e-6."""
+    got = float(kernels.riemann(spec, n, rule="mid", dtype="fp32", div=div).item())
+    if n <= 1_000_003:
+        want = _ref_sum(spec, n, rule="mid")
+    else:
+        want = float(kernels.riemann(spec, n, rule="mid", dtype="fp64").item())
+    assert got == pytest.approx(want, rel=2e-6, abs=1e-9)
+
+
+@pytest.mark.parametrize("spec", F32_SPECS, ids=lambda s: s.name)
+def test_fp32_plan_reports_series(native, cuda, spec):
+    """fp32 is accepted for every integrand and runs its packed series form."""
+    from cuda_v_mpi_amd import Integrator
+    it = Integrator(spec, n=10**8, dtype="fp32")
+    assert "series" in str(it.plan.effective_div)
+    assert it.run().value == pytest.approx(spec.analytic(), rel=1e-5)
+
+
 @pytest.mark.parametrize("spec", SPECS, ids=lambda s: s.name)
 def test_fused_equals_two_kernel_bitwise(cuda, spec):
     n = 3_000_017

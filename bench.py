@@ -91,6 +91,9 @@ def parse(argv=None) -> argparse.Namespace:
                    help="run the RCCL all-reduce stage even on 1 GPU (tests the multi-GPU graph)")
     p.add_argument("--no-extras", action="store_true",
                    help="skip the post-timing extras (IEEE run, per-point ulp, N=1e10 strong)")
+    p.add_argument("--sweep-gpus", default="",
+                   help="e.g. 1,2,4,8: run the scaling sweep (cuda_v_mpi_amd/parallel/scaling.py) "
+                        "over these GPU counts instead of one benchmark")
     p.add_argument("--verbose", action="store_true")
     p.add_argument("--jsonl", default="", help="also append the JSON line to this file")
     return p.parse_args(argv)
@@ -157,6 +160,12 @@ def spawn_ranks(n: int, argv: list[str]) -> int:
 def main(argv=None) -> int:
     argv = sys.argv[1:] if argv is None else argv
     args = parse(argv)
+    if args.sweep_gpus:
+        from cuda_v_mpi_amd.parallel import scaling
+
+        return scaling.main(["--gpus", args.sweep_gpus, "--steps", str(args.steps),
+                             "--warmup", str(args.warmup)] +
+                            (["--jsonl", args.jsonl] if args.jsonl else []))
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus > 1 and world_env == 1 and "RANK" not in os.environ:
         return spawn_ranks(args.gpus, argv)

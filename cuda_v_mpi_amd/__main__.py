@@ -9,6 +9,7 @@ SURVEY §2.6) on top of the Python API, and adds JSON output:
     integrate   any integrand, JSON result                        [--integrand --n --rule ...]
     table2d     2-D velocity field v(x) v(y), bilinear, JSON      [--grid 4096 --iters 100]
     oracle      print every SURVEY §6.1 oracle value (CPU only)
+    scale       GPU-count sweep 1,2,4,8: weak/strong efficiency, RCCL latency [--gpus 1,2,4,8]
     info        devices and build
 
 Multi-GPU: launch under torchrun (one process per GPU); the process group is created from
@@ -212,7 +213,21 @@ def main(argv=None) -> int:
     t2.add_argument("--backend", default="hip", choices=["hip", "cpu"])
     sub.add_parser("oracle")
     sub.add_parser("info")
+    sc = sub.add_parser("scale")
+    sc.add_argument("--gpus", default="1,2,4,8")
+    sc.add_argument("--steps", type=int, default=200)
+    sc.add_argument("--warmup", type=int, default=10)
+    sc.add_argument("--no-comm", action="store_true")
+    sc.add_argument("--jsonl", default="")
+    sc.add_argument("--md", default="")
     a = p.parse_args(argv)
+    if a.cmd == "scale":
+        from .parallel import scaling
+
+        return scaling.main(["--gpus", a.gpus, "--steps", str(a.steps), "--warmup",
+                             str(a.warmup)] + (["--no-comm"] if a.no_comm else []) +
+                            (["--jsonl", a.jsonl] if a.jsonl else []) +
+                            (["--md", a.md] if a.md else []))
     return {"riemann": cmd_riemann, "cintegrate": cmd_cintegrate, "trainscan": cmd_trainscan,
             "integrate": cmd_integrate, "table2d": cmd_table2d, "oracle": cmd_oracle,
             "info": cmd_info}[a.cmd](a)

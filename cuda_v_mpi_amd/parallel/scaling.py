@@ -1,0 +1,166 @@
+"""GPU-count scaling sweep (SURVEY §7.1 layer 10): the headline over N in {1, 2, 4, 8} GPUs.
+
+The reference measures its decomposition by re-running ``mpirun -np P`` by hand
+(riemann.cpp:62-86, 4main.c:69-157) and reading a wall clock. Here one command runs, for
+every GPU count the node has,
+
+  * ``bench.py --gpus N`` (one process per GPU, spawned by bench.py itself; RCCL over xGMI):
+    the weak-scaling headline (1e9 samples per GPU) and, from the same run, BASELINE #3's
+    strong-scaling point (N = 1e10 in total over the N GPUs);
+  * ``miint comm --gpus N`` (one process driving N GPUs, ncclCommInitAll): all-reduce and
+    all-gather latency at 8 B (the Riemann payload, riemann.cpp:76) and 144 MB (4main.c:157's
+    broadcast table),
+
+and derives weak- and strong-scaling efficiency against the N = 1 row. Counts the node
+cannot run get an explicit ``skipped`` row instead of a number.
+
+    python -m cuda_v_mpi_amd scale --gpus 1,2,4,8 [--steps 200] [--jsonl FILE] [--md FILE]
+    python bench.py --sweep-gpus 1,2,4,8
+
+This process never touches the GPU (children do): the device count comes from
+``torch.cuda.device_count()``, which does not initialise HIP on this stack.
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+BENCH = os.path.join(REPO, "bench.py")
+MIINT = os.path.join(REPO, "build", "bin", "miint")
+
+
+def visible_gpus() -> int:
+    try:
+        import torch
+
+        return int(torch.cuda.device_count())
+    except Exception:  # pragma: no cover - no torch / no ROCm
+        return 0
+
+
+def _last_json(text: str) -> dict | None:
+    for line in reversed(text.strip().splitlines()):
+        line = line.strip()
+        if line.startswith("{"):
+            try:
+                return json.loads(line)
+            except ValueError:
+                continue
+    return None
+
+
+def run_bench(n: int, steps: int, warmup: int, timeout: float = 900.0,
+              extra: list[str] | None = None) -> dict:
+    cmd = [sys.executable, BENCH, "--gpus", str(n), "--steps", str(steps), "--warmup",
+           str(warmup)] + list(extra or [])
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=REPO)
+    js = _last_json(p.stdout)
+    if p.returncode != 0 or js is None:
+        raise RuntimeError(f"bench.py --gpus {n} failed (rc {p.returncode}): {p.stderr[-2000:]}")
+    return js
+
+
+def run_comm(n: int, timeout: float = 600.0) -> dict:
+    """8 B and 144 MB all-reduce / all-gather times (slowest rank) from `miint comm`."""
+    if not os.path.exists(MIINT):
+        return {"skipped": f"{MIINT} not built"}
+    p = subprocess.run([MIINT, "comm", "--gpus", str(n), "--max-bytes", "144e6", "--iters", "10"],
+                       capture_output=True, text=True, timeout=timeout, cwd=REPO)
+    if p.returncode != 0:
+        return {"error": p.stderr[-1000:]}
+    rows = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    out = {}
+    for r in rows:
+        b = r["bytes"] / (n if r["op"] == "allgather" else 1)  # per-rank payload
+        if r["op"] in ("allreduce", "allgather") and (b == 8 or b >= 144e6 * 0.99):
+            key = f"{r['op']}_{'8B' if b == 8 else '144MB'}"
+            out[key + "_us"] = r["us"]
+            out[key + "_busbw_GBps"] = r["busbw_GBps"]
+    return out
+
+
+def sweep(counts: list[int], steps: int = 200, warmup: int = 10, comm: bool = True) -> list[dict]:
+    have = visible_gpus()
+    rows: list[dict] = []
+    for n in counts:
+        if n > have:
+            rows.append({"n_gpus": n, "skipped": f"only {have} devices"})
+            continue
+        b = run_bench(n, steps, warmup)
+        row = {
+            "n_gpus": n,
+            "value": b["value"],
+            "ms_per_step": b["ms_per_step"],
+            "per_rank_spread_ms": b.get("per_rank_spread_ms"),
+            "rccl_world": b.get("rccl_world"),
+            "rccl_version": b.get("rccl_version"),
+            "graphs": b["config"]["graphs"],
+            "verified": b["verified"],
+        }
+        s = b.get("baseline3_strong_1e10")
+        if s:
+            row["strong_1e10_value"] = s["value"]
+            row["strong_1e10_ms"] = s["ms_per_step"]
+        if comm:
+            row.update(run_comm(n))
+        rows.append(row)
+    base = next((r for r in rows if r["n_gpus"] == 1 and "value" in r), None)
+    for r in rows:
+        if base is None or "value" not in r:
+            continue
+        n = r["n_gpus"]
+        r["weak_eff"] = r["value"] / (n * base["value"])
+        if "strong_1e10_value" in r and "strong_1e10_value" in base:
+            r["strong_eff"] = r["strong_1e10_value"] / (n * base["strong_1e10_value"])
+    return rows
+
+
+def markdown(rows: list[dict]) -> str:
+    cols = ["n_gpus", "value", "ms_per_step", "weak_eff", "strong_1e10_value", "strong_eff",
+            "per_rank_spread_ms", "rccl_world", "allreduce_8B_us", "allgather_8B_us",
+            "allreduce_144MB_us", "allgather_144MB_us"]
+    out = ["| " + " | ".join(cols) + " |", "|" + "---|" * len(cols)]
+    for r in rows:
+        if "skipped" in r:
+            out.append(f"| {r['n_gpus']} | skipped: {r['skipped']} |" + " |" * (len(cols) - 2))
+            continue
+        cells = []
+        for c in cols:
+            v = r.get(c)
+            cells.append("" if v is None else (f"{v:.4g}" if isinstance(v, float) else str(v)))
+        out.append("| " + " | ".join(cells) + " |")
+    return "\n".join(out)
+
+
+def main(argv=None) -> int:
+    import argparse
+
+    ap = argparse.ArgumentParser(description=__doc__,
+                                 formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", default="1,2,4,8")
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--no-comm", action="store_true")
+    ap.add_argument("--jsonl", default="")
+    ap.add_argument("--md", default="")
+    a = ap.parse_args(argv)
+    rows = sweep([int(x) for x in a.gpus.split(",")], a.steps, a.warmup, comm=not a.no_comm)
+    for r in rows:
+        print(json.dumps(r), flush=True)
+    md = markdown(rows)
+    print(md)
+    if a.jsonl:
+        with open(a.jsonl, "a") as f:
+            for r in rows:
+                f.write(json.dumps(r) + "\n")
+    if a.md:
+        with open(a.md, "w") as f:
+            f.write(md + "\n")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

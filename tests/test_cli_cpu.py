@@ -98,3 +98,24 @@ def test_bench_rejects_world_mismatch():
                        capture_output=True, text=True, timeout=300,
                        env=dict(os.environ, WORLD_SIZE="3", RANK="0"))
     assert p.returncode == 2 and "WORLD_SIZE=3" in p.stderr
+
+
+def test_scale_sweep_rows_and_efficiency(monkeypatch):
+    """The GPU-count sweep's bookkeeping on a GPU-less box: counts the node cannot run get an
+    explicit skipped row; efficiencies are computed against the N = 1 row."""
+    from cuda_v_mpi_amd.parallel import scaling
+
+    monkeypatch.setattr(scaling, "visible_gpus", lambda: 2)
+    fake = {1: 1.0e13, 2: 1.9e13}
+    monkeypatch.setattr(scaling, "run_bench", lambda n, s, w: {
+        "value": fake[n], "ms_per_step": 0.075, "per_rank_spread_ms": 0.001,
+        "rccl_world": n if n > 1 else None, "config": {"graphs": True}, "verified": True,
+        "baseline3_strong_1e10": {"value": fake[n] * 1.05, "ms_per_step": 0.7}})
+    monkeypatch.setattr(scaling, "run_comm", lambda n: {"allreduce_8B_us": 10.0 * n})
+    rows = scaling.sweep([1, 2, 4, 8])
+    assert [r["n_gpus"] for r in rows] == [1, 2, 4, 8]
+    assert rows[2]["skipped"] == "only 2 devices" and rows[3]["skipped"] == "only 2 devices"
+    assert rows[0]["weak_eff"] == 1.0 and abs(rows[1]["weak_eff"] - 0.95) < 1e-12
+    assert abs(rows[1]["strong_eff"] - 0.95) < 1e-12
+    md = scaling.markdown(rows)
+    assert "skipped: only 2 devices" in md and md.count("\n") == 5

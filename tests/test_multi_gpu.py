@@ -84,3 +84,18 @@ def test_trainscan_threads_match_single(native, cuda, g):
     b = json.loads(many.stdout.strip().splitlines()[-1])
     assert b["distance"] == pytest.approx(a["distance"], rel=1e-13)
     assert b["sum_of_sums"] == pytest.approx(a["sum_of_sums"], rel=1e-12)
+
+
+@pytest.mark.parametrize("g", [2, 8])
+def test_bench_self_spawned_ranks(native, cuda, g):
+    """`python bench.py --gpus G` without torchrun: the parent spawns G rank processes; RCCL
+    reports G ranks; per-rank timings for all of them; BASELINE #3 strong point included."""
+    if _devices() < g:
+        pytest.skip(f"needs {g} HIP devices")
+    p = _run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(g), "--steps", "48",
+              "--warmup", "8"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    js = json.loads(p.stdout.strip().splitlines()[-1])
+    assert js["verified"] and js["n_gpus"] == g and js["launcher"] == "spawn"
+    assert js["rccl_world"] == g and len(js["per_rank_ms"]) == g
+    assert js["baseline3_strong_1e10"]["n_per_gpu"] == 10**10 // g

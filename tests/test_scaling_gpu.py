@@ -1,0 +1,40 @@
+"""The GPU-count scaling sweep on the GPU (SURVEY §7.1 layer 10): every count the box has
+gets a measured row, the others an explicit skipped row, and the N = 1 row agrees with a
+plain `bench.py --gpus 1` run."""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_scale_sweep_one_gpu_row_matches_bench(native, cuda):
+    import torch
+
+    have = torch.cuda.device_count()
+    p = subprocess.run([sys.executable, "-m", "cuda_v_mpi_amd", "scale", "--gpus", "1,2,4,8",
+                        "--steps", "200", "--warmup", "10"], cwd=REPO, capture_output=True,
+                       text=True, timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    rows = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    assert [r["n_gpus"] for r in rows] == [1, 2, 4, 8]
+    for r in rows:
+        if r["n_gpus"] > have:
+            assert r["skipped"] == f"only {have} devices"
+        else:
+            assert r["verified"] and r["graphs"] and r["value"] > 1e12
+    one = rows[0]
+    assert one["weak_eff"] == 1.0 and one["strong_eff"] == 1.0
+    assert one["allreduce_8B_us"] > 0 and one["allgather_144MB_us"] > 0
+    b = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "200",
+                        "--warmup", "10", "--no-extras"], cwd=REPO, capture_output=True,
+                       text=True, timeout=300)
+    assert b.returncode == 0, b.stderr[-2000:]
+    ref = json.loads(b.stdout.strip().splitlines()[-1])
+    assert one["value"] == pytest.approx(ref["value"], rel=0.02)

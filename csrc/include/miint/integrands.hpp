@@ -309,10 +309,12 @@ __device__ __forceinline__ void tile_sincos(double th, double& S, double& C) {
 // with cos/sin(k delta) for the 8 pair offsets k = j + 1/2 and for the centres computed once
 // per launch on the host in long double (RiemannParams::trig, kernel arguments -> SGPRs).
 // Per pair: 1 mul + 2 fma for the two samples + 2 accumulations (2.5 VALU per sample); the
-// seed and the 4-op re-centring per sub-tile add the rest (388 VALU per 128-sample tile).
+// seed (~40 VALU) and the 4-op re-centring per sub-tile add the rest: ~388 VALU per tile at
+// Subs = 8 (TrainVel, 128 samples), ~580 at Subs = 12 (Sin, 192 samples); measured per
+// sample: 2.98 (Sin) and 3.13 (TrainVel) VALU (profiles/r2/fp32_counters.md, fp64 rows).
 // Every centre comes straight from the tile midpoint (one rounding), so the per-point error
 // does not grow with the tile. No truncation (valid for any h).
-// Subs sub-tiles per seed: Sin runs 12 (192-sample tiles, 1.20e13 -> 1.25e13 subint/s over
+// Subs sub-tiles per seed: Sin runs 12 (192-sample tiles, 1.20e13 -> 1.24e13 subint/s over
 // 8), TrainVel keeps 8 (12 measured 1.18e13 -> 1.15e13). The host fills the centre table for
 // the largest Subs; a smaller Subs reads its prefix (the same c0 = 8, 24, ... values).
 template <int Subs>
@@ -382,9 +384,10 @@ struct AngleSeries {
 
 // ------------------------------------------------------------------ sin(x), fp64
 // kIeee: ocml sin per sample (~53 VALU per sample measured, with its range reduction).
-// kSeries (default): AngleSeries with w = 1. Per point: absolute error vs ocml sin
-// <= 7.2e-16 measured (tests allow 4 ulp(1)); the sum agrees with the kIeee path to 2e-15
-// relative. N = 1e9 on [0, pi]: 103.5 us per integration (9.66e12 subint/s) vs 1.53 ms.
+// kSeries (default): AngleSeries<12> with w = 1 (192-sample tiles). Per point: absolute
+// error vs ocml sin <= 7.2e-16 measured (tests allow 4 ulp(1)); the sum agrees with the kIeee
+// path to 2e-15 relative. N = 1e9 on [0, pi]: 81.2 us per integration (1.23e13 subint/s,
+// profiles/r2/bench_fp32_all.jsonl) vs 1.53 ms for ocml sin per sample.
 struct Sin : TileDefaults<Sin>, AngleSeries<12> {
   static constexpr double kScale = 1.0;
   template <DivMode M>

@@ -27,9 +27,9 @@ constexpr int kDirectHalfSpan = 16;  // the same for kSeriesDirect's 32-sample t
 inline bool series_ok(double h) { return kSeriesHalfSpan * (h < 0 ? -h : h) <= 2e-6; }
 inline bool direct_ok(double h) { return kDirectHalfSpan * (h < 0 ? -h : h) <= 2e-6; }
 
-// Division mode actually used for step h: a step too coarse for the 192-sample series tiles
-// (N < 4.8e7 on [0, 1]) still fits the 32-sample kSeriesDirect tiles down to N = 8e6 (5 VALU
-// per sample against ~14 for IEEE division); coarser steps use IEEE division.
+// Division mode actually used for step h: the 192-sample series tiles need N > 4.8e7 on
+// [0, 1]; a coarser step still fits the 32-sample kSeriesDirect tiles down to N = 8e6
+// (5 VALU per sample against ~14 for IEEE division); coarser steps use IEEE division.
 inline DivMode effective_div(DivMode d, double h) {
   if (d == DivMode::kIeee) return d;
   if (d == DivMode::kSeries && series_ok(h)) return d;

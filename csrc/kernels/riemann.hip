@@ -62,7 +62,9 @@ __device__ __forceinline__ double lane_sum(const RiemannParams& p, const F& f) {
   uint64_t r = 0;
   for (; r < r_all; ++r, ib += istep) acc = f.template tile_acc<T, M>(fma(ib, p.h, p.a), p.h, acc);
   if (r < r_any && r < rounds) acc = f.template tile_acc<T, M>(fma(ib, p.h, p.a), p.h, acc);
-  // remainder (< T samples): one per lane; T <= 64 <= lanes of any grid
+  // remainder (< T samples): one per lane of the launch, so T must not exceed the lanes of
+  // the smallest grid (one 256-thread workgroup); the longest tile is 192 samples
+  static_assert(T <= B, "the remainder loop gives each lane at most one sample");
   const uint64_t done = ntile * T;
   if (gid < p.n - done) acc += f.point(fma(base + static_cast<double>(done + gid), p.h, p.a));
   return acc;

@@ -43,10 +43,11 @@ def test_riemann_vs_torch(cuda, spec, n):
     assert got == pytest.approx(want, rel=1e-12, abs=1e-12)
 
 
-@pytest.mark.parametrize("n", [1, 63, 4097, 1_000_003, 40_000_001])
+@pytest.mark.parametrize("n", [1, 63, 4097, 1_000_003, 40_000_001, 50_000_017])
 def test_riemann_fp32_small_and_odd_n(cuda, n):
     """fp32 path at odd N and N below the grid size (remainder samples, partial tiles, the
-    IEEE fallback below 4.8e7 and the series tiles above) against the fp64 torch reference."""
+    IEEE fallback up to 4.8e7 and, at 50_000_017, the 192-sample series tiles with a
+    remainder of 17 samples) against the fp64 torch reference."""
     spec = integrands.pi4()
     got = float(kernels.riemann(spec, n, rule="mid", dtype="fp32").item())
     want = _ref_sum(spec, n, rule="mid")
@@ -103,14 +104,17 @@ def test_rank_slices_sum_to_whole(cuda):
     assert math.fsum(parts) == pytest.approx(whole, rel=1e-14)
 
 
-@pytest.mark.parametrize("n", [10**9, 48_000_000])
-def test_pi4_series_per_point_accuracy(cuda, n):
+@pytest.mark.parametrize("n", [10**9, 48_000_001])
+def test_pi4_series_per_point_accuracy(native, cuda, n):
     """Every sample of the series path against IEEE division, in units of ulp(IEEE value):
     <= 5 ulp and >= 95 % within 2 ulp (whole domain: 91 % within 1, 99.4 % within 2; see
     tools/ulp_probe.py). Also at the coarsest step the series path accepts (96 h <= 2e-6:
-    n >= 4.8e7 on [0, 1]). Per point, g = 1/2 + e is rounded at ulp(1/2) scale, and the IEEE
+    N > 4.8e7 on [0, 1]; 48_000_001 is the first N, and the plan must report the series
+    division for it, so the case cannot silently fall back). Per point, g = 1/2 + e is rounded at ulp(1/2) scale, and the IEEE
     reference rounds every coordinate x0 + u h (the series uses exact offsets), so window
     means are not a bias measure; the sum-level check is test_series_equals_ieee_sum."""
+    from cuda_v_mpi_amd import Integrator
+    assert str(Integrator("pi4", n=n, div="series").plan.effective_div).endswith("series")
     spec = integrands.pi4()
     for i0 in (0, n // 8 + 12_345, n - (1 << 16)):
         v = kernels.point_values(spec, n, rule="left", div="series", i_begin=i0, n_local=1 << 16)
@@ -258,10 +262,13 @@ def test_pi4_mid_steps_use_direct_series(native, cuda, n):
     assert a == pytest.approx(b, rel=1e-15, abs=0)
 
 
-@pytest.mark.parametrize("n", [33_000_000, 10**8, 10**9])
+@pytest.mark.parametrize("n", [50_000_000, 10**8, 10**9])
 def test_series_equals_ieee_sum(cuda, n):
     """The whole sum: series vs correctly rounded division agree to fp64 resolution, i.e.
-    the series path's per-point rounding carries no bias into the result."""
+    the series path's per-point rounding carries no bias into the result (every N here is
+    above 4.8e7, so the 192-sample series tiles run, which the plan confirms)."""
+    from cuda_v_mpi_amd import Integrator
+    assert str(Integrator("pi4", n=n, div="series").plan.effective_div).endswith("series")
     spec = integrands.pi4()
     a = float(kernels.riemann(spec, n, div="series").item())
     b = float(kernels.riemann(spec, n, div="ieee").item())

@@ -30,8 +30,9 @@ Weak scaling: every GPU integrates its own 1e9-sample slice of a global N = 1e9 
 global sums) are checked on the host against pi. After the timed region (outside it) the
 record also gets: the same config with IEEE division per sample ("ieee_div"), the series
 path's per-point error against IEEE division on a 64 K-sample window ("per_point_max_ulp"),
-and BASELINE config #3 — N = 1e10 in total, strong-scaled over the same GPUs
-("baseline3_strong_1e10").
+BASELINE config #3 — N = 1e10 in total, strong-scaled over the same GPUs
+("baseline3_strong_1e10") — and BASELINE config #5 — the 4096^2 2-D velocity field with its
+rows split over the same GPUs ("baseline5_table2d_4096").
 """
 from __future__ import annotations
 
@@ -90,7 +91,7 @@ def parse(argv=None) -> argparse.Namespace:
     p.add_argument("--force-collective", action="store_true",
                    help="run the RCCL all-reduce stage even on 1 GPU (tests the multi-GPU graph)")
     p.add_argument("--no-extras", action="store_true",
-                   help="skip the post-timing extras (IEEE run, per-point ulp, N=1e10 strong)")
+                   help="skip the post-timing extras (IEEE run, per-point ulp, N=1e10 strong, 2-D field)")
     p.add_argument("--sweep-gpus", default="",
                    help="e.g. 1,2,4,8: run the scaling sweep (cuda_v_mpi_amd/parallel/scaling.py) "
                         "over these GPU counts instead of one benchmark")
@@ -299,7 +300,14 @@ def main(argv=None) -> int:
         rccl_version = native().Comm.version()
     extras = {}
     if not cpu and not use_torch and not args.no_extras:
-        extras = run_extras(args, ctx, integ, n_total, pipeline, dev)
+        # The headline is already measured: a failure in an extra must not cost the record.
+        # (Every rank runs the same extras, so an exception on one is one on all; the
+        # collective sequence stays matched.)
+        try:
+            extras = run_extras(args, ctx, integ, n_total, pipeline, dev)
+        except Exception as e:  # noqa: BLE001
+            extras = {"extras_error": f"{type(e).__name__}: {e}"}
+            print(f"bench.py: extras failed: {extras['extras_error']}", file=sys.stderr)
 
     if ctx.is_root:
         out = {
@@ -423,6 +431,33 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
                                         "steps": steps, "result": v, "abs_err": abs(v - math.pi),
                                         "n_per_gpu": n3 // ctx.world, "scaling": "strong"}
         del st
+    # (4) BASELINE config #5: the 2-D field v(x) v(y) from the velocity profile, 4096^2
+    #     bilinear midpoint samples, sample rows split over the same GPUs; one integration =
+    #     one fused kernel per rank, the partials of a 32-integration graph replay meeting in
+    #     one RCCL all-reduce (Table2DPlan)
+    if args.integrand == "pi4":
+        import torch
+
+        from cuda_v_mpi_amd import native
+        from cuda_v_mpi_amd.parallel.dist import native_comm
+
+        m = native()
+        g = 4096
+        comm2 = native_comm(ctx) if (ctx.world > 1 or args.force_collective) else None
+        p2 = m.Table2DPlan(g, 1800.0, ctx.device, comm2, not args.no_bucket)
+        p2.run()
+        p2.time(p2.graph_steps * 4, True)  # warm replays
+        ms = p2.time(p2.graph_steps * 10, True)
+        t = torch.tensor([ms], dtype=torch.float64, device=dev)
+        ctx.all_reduce_max(t)
+        ms = float(t.item())
+        v, want = p2.last_result(), m.table2d_oracle(g)
+        out["baseline5_table2d_4096"] = {
+            "grid": g, "samples": g * g, "ms_per_integration": ms,
+            "samples_per_s": g * g / (ms * 1e-3), "result": v, "midpoint_oracle": want,
+            "rel_err_vs_oracle": abs(v - want) / want, "rows_this_rank": [p2.row0, p2.row1],
+            "bucketed_allreduce": bool(p2.bucketed), "n_gpus": ctx.world}
+        del p2, comm2
     return out
 
 

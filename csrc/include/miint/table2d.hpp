@@ -28,6 +28,11 @@ struct Table2DConfig {
   // Without a communicator: integrate only row slice `rank` of `world` (the share one GPU
   // of a `world`-GPU run computes; the result is that partial). Ignored with a communicator.
   int world = 1, rank = 0;
+  // Graph timing with a communicator: the kGraphSteps integrations of one replay each write
+  // their own partial, and ONE all-reduce of kGraphSteps doubles (plus one copy) ends the
+  // replay — every integration still gets its own global sum (RiemannPlan's bucketing).
+  // false: kernel -> 8-byte all-reduce -> copy per integration.
+  bool bucket = true;
 };
 
 class Table2DPlan {
@@ -40,17 +45,23 @@ class Table2DPlan {
   // kGraphSteps integrations are captured once into a hipGraph and replayed (iters rounded
   // up to whole replays): one launch per kGraphSteps instead of one per integration.
   double time(int iters, bool graphs = true);
+  // Global value of the last integration time() ran (every rank holds it).
+  double last_result() const;
+  bool bucketed() const { return bucketed_; }
   static constexpr int kGraphSteps = 32;
   int row0() const { return row0_; }
   int row1() const { return row1_; }
 
  private:
   void enqueue(hipStream_t s);
+  void launch_local(double* out, hipStream_t s);  // this rank's rows -> *out (device ptr)
   Table2DConfig cfg_;
   int device_;
   const Comm* comm_;
   int rank_ = 0, world_ = 1;
   int row0_ = 0, row1_ = 0;
+  bool bucketed_ = false;
+  bool last_bucketed_ = false;
   Stream stream_;
   DeviceBuffer<double> v_, table_, partials_, result_;
   DeviceBuffer<unsigned int> ticket_;

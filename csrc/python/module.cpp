@@ -353,17 +353,21 @@ PYBIND11_MODULE(_miint, m) {
 
   // ------------------------------------------------------------------ 2-D field plan
   py::class_<Table2DPlan>(m, "Table2DPlan")
-      .def(py::init([](int grid, double extent, int device, const Comm* comm) {
+      .def(py::init([](int grid, double extent, int device, const Comm* comm, bool bucket) {
              Table2DConfig c;
              c.grid = grid;
              c.extent = extent;
+             c.bucket = bucket;
              return new Table2DPlan(c, device, comm);
            }),
            py::arg("grid") = 4096, py::arg("extent") = 1800.0, py::arg("device") = 0,
-           py::arg("comm") = nullptr, py::keep_alive<1, 5>())
+           py::arg("comm") = nullptr, py::arg("bucket") = true, py::keep_alive<1, 5>())
       .def("run", &Table2DPlan::run, py::call_guard<py::gil_scoped_release>())
       .def("time", &Table2DPlan::time, py::arg("iters"), py::arg("graphs") = true,
            py::call_guard<py::gil_scoped_release>())
+      .def("last_result", &Table2DPlan::last_result)
+      .def_property_readonly("bucketed", &Table2DPlan::bucketed)
+      .def_property_readonly("graph_steps", [](const Table2DPlan&) { return Table2DPlan::kGraphSteps; })
       .def_property_readonly("row0", &Table2DPlan::row0)
       .def_property_readonly("row1", &Table2DPlan::row1);
   m.def("table2d_oracle", &table2d_oracle, py::arg("grid"), py::arg("extent") = 1800.0);

@@ -101,6 +101,22 @@ PYBIND11_MODULE(_miint, m) {
   });
   m.def("set_device", &set_device);
   m.def("device_synchronize", []() { MIINT_HIP(hipDeviceSynchronize()); });
+  // Host wait policy of the current device (hipDeviceSchedule*): "spin" polls the completion
+  // signal (lowest wake-up latency, one busy core per waiting thread), "yield", "blocking"
+  // (interrupt), "auto" (the runtime's default).
+  m.def("set_device_flags", [](const std::string& mode) {
+    unsigned f = hipDeviceScheduleAuto;
+    if (mode == "spin") f = hipDeviceScheduleSpin;
+    else if (mode == "yield") f = hipDeviceScheduleYield;
+    else if (mode == "blocking") f = hipDeviceScheduleBlockingSync;
+    else if (mode != "auto") throw std::invalid_argument("spin|yield|blocking|auto");
+    MIINT_HIP(hipSetDeviceFlags(f));
+  });
+  m.def("get_device_flags", []() {
+    unsigned f = 0;
+    MIINT_HIP(hipGetDeviceFlags(&f));
+    return f;
+  });
   m.def("process_start_seconds", &process_start_seconds);
   m.def("enable_tracing", &enable_tracing, "roctx ranges around runtime phases (MIINT_ROCTX=1)");
   m.def("tracing_enabled", &tracing_enabled);

@@ -235,6 +235,7 @@ int main(int argc, char** argv) {
       Table2DConfig c;
       c.grid = static_cast<int>(a.integer("grid", 4096));
       c.bucket = !a.flag("no-bucket");  // one all-reduce per graph replay of kGraphSteps
+      c.chain = !a.flag("no-chain");    // graph replays: chained launches, no per-launch tail
       // --slice R/W: time only rank R's rows of a W-GPU split, on this GPU (no collective)
       const std::string sl = a.str("slice", "");
       if (!sl.empty()) {
@@ -244,7 +245,7 @@ int main(int argc, char** argv) {
         c.world = std::stoi(sl.substr(k + 1));
       }
       double value = 0.0, timed = 0.0, ms = 0.0;
-      bool bucketed = false;
+      bool bucketed = false, chained = false;
       std::mutex mu;
       cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
         Table2DPlan plan(c, dev, comm);
@@ -255,6 +256,7 @@ int main(int argc, char** argv) {
           value = v;
           timed = plan.last_result();
           bucketed = plan.bucketed() && graphs;
+          chained = plan.chained() && graphs;
         }
         if (t > ms) ms = t;
       });
@@ -271,6 +273,7 @@ int main(int argc, char** argv) {
               .add("result", value)
               .add("timed_result", timed)
               .add("bucketed_allreduce", bucketed)
+              .add("chained", chained)
               .add("midpoint_oracle", want)
               .add("rel_err_vs_oracle", std::fabs(value - want) / want)
               .add("rel_err_vs_exact", std::fabs(value - exact) / exact)

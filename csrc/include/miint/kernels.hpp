@@ -180,6 +180,14 @@ void launch_table2d_partials(const Table2DParams& p, double* partials, hipStream
 // pattern (fill_unset_slots); both re-armed by the kernel).
 void launch_table2d_fused(const Table2DParams& p, double* partials, unsigned* ticket,
                           double* out, hipStream_t stream);
+// Batches of integrations of the same field: launch j writes its table2d_grid(p) partials
+// into `partials` (one half of a double buffer) and, if prev != nullptr, its workgroup 0
+// first sums launch j-1's partials (the other half, same p) into *prev_out; the batch's last
+// partials are closed by launch_table2d_finalize. Values are bitwise those of the fused
+// launch.
+void launch_table2d_chained(const Table2DParams& p, double* partials, const double* prev,
+                            double* prev_out, hipStream_t stream);
+void launch_table2d_finalize(const double* partials, int n, double* out, hipStream_t stream);
 void launch_outer_product(const double* v, int n, double* table, hipStream_t stream);
 
 }  // namespace miint

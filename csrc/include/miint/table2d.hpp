@@ -33,6 +33,9 @@ struct Table2DConfig {
   // replay — every integration still gets its own global sum (RiemannPlan's bucketing).
   // false: kernel -> 8-byte all-reduce -> copy per integration.
   bool bucket = true;
+  // Graph timing: chained launches (launch j's workgroup 0 closes launch j-1's partials,
+  // one finalize closes the replay) instead of the fused hand-off tail in every launch.
+  bool chain = true;
 };
 
 class Table2DPlan {
@@ -48,6 +51,7 @@ class Table2DPlan {
   // Global value of the last integration time() ran (every rank holds it).
   double last_result() const;
   bool bucketed() const { return bucketed_; }
+  bool chained() const { return cfg_.chain && (!comm_ || world_ == 1 || bucketed_); }
   static constexpr int kGraphSteps = 32;
   int row0() const { return row0_; }
   int row1() const { return row1_; }
@@ -61,9 +65,9 @@ class Table2DPlan {
   int rank_ = 0, world_ = 1;
   int row0_ = 0, row1_ = 0;
   bool bucketed_ = false;
-  bool last_bucketed_ = false;
+  bool last_batched_ = false;  // the last time() left kGraphSteps results in host_
   Stream stream_;
-  DeviceBuffer<double> v_, table_, partials_, result_;
+  DeviceBuffer<double> v_, table_, partials_, chain_, result_;
   DeviceBuffer<unsigned int> ticket_;
   PinnedBuffer<double> host_;
   Event e0_, e1_;

@@ -100,18 +100,56 @@ __global__ __launch_bounds__(kB) void outer_product_kernel(const double* __restr
 // such tiles, else 64 (4 x 4 per thread).
 __device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+// Launch modes of both 2-D kernels:
+//   kT2Partials  one partial per workgroup (a later finalize sums them)
+//   kT2Fused     + last-workgroup hand-off (handoff.hpp): out[0] = the launch's integral
+//   kT2Chained   partials, and workgroup 0 first sums the PREVIOUS launch's partials (the
+//                other half of a double buffer; the kernel boundary orders them) into
+//                *prev_out. In a batch of back-to-back integrations this takes the hand-off
+//                tail (slot publish, ticket, one workgroup's ordered read of every slot:
+//                2.2-3.4 us, profiles/r2/table2d_tail.jsonl) off the critical path; the
+//                batch's last partials are closed by table2d_finalize_kernel.
+// Every mode sums the partials with ordered_partials + block_sum in index order, so the
+// value is bitwise the same whichever of them produced it.
+enum : int { kT2Partials = 0, kT2Fused = 1, kT2Chained = 2 };
+
+struct Table2DChain {
+  const double* prev;  // previous launch's partials (kT2Chained; nullptr: nothing to close)
+  int prev_n;
+  double* prev_out;
+};
+
+__device__ __forceinline__ void table2d_close(const double* parts, int n, double* out,
+                                              double* red) {
+  const double v = ordered_partials<kB, false>(parts, n);
+  const double tot = block_sum<kB>(v, red);
+  if (threadIdx.x == 0) *out = tot;
+  __syncthreads();  // red is reused by the caller's own block_sum
+}
+
+__global__ __launch_bounds__(kB) void table2d_finalize_kernel(const double* parts, int n,
+                                                              double* out) {
+  __shared__ double red[kB / kWave];
+  table2d_close(parts, n, out, red);
+}
+
 // Per thread: columns c0 + tx + 16 b, rows r0 + ty + 16 a. The column terms (table column,
 // fraction) and row terms (row offset, fraction) are computed once per thread — 2 kPer
 // index computations instead of kPer^2 (the first form spent 41 VALU per sample) — leaving
 // per sample four loads and the bilinear blend. FUSED: the last workgroup reduces all
 // partials (handoff.hpp) and writes out[0]; otherwise one partial per workgroup for a
 // finalize.
-template <int kTile, bool FUSED>
+template <int kTile, int MODE>
 __global__ __launch_bounds__(kB) void table2d_kernel(Table2DParams p, double* partials,
-                                                     unsigned* ticket, double* out) {
+                                                     unsigned* ticket, double* out,
+                                                     Table2DChain chain) {
   constexpr int kPer = kTile / 16;
   __shared__ double red[kB / kWave];
   __shared__ int is_last;
+  if constexpr (MODE == kT2Chained) {
+    if (chain.prev && blockIdx.x == 0 && blockIdx.y == 0)
+      table2d_close(chain.prev, chain.prev_n, chain.prev_out, red);
+  }
   const double sx = p.X / p.gx, sy = p.Y / p.gy;          // sample spacing
   const double cx = (p.nx - 1) / p.X, cy = (p.ny - 1) / p.Y;  // table cells per unit
   const int c0 = blockIdx.x * kTile;
@@ -155,7 +193,7 @@ __global__ __launch_bounds__(kB) void table2d_kernel(Table2DParams p, double* pa
   }
   const double s = block_sum<kB>(acc, red) * (sx * sy);
   const unsigned bid = blockIdx.y * gridDim.x + blockIdx.x;
-  if constexpr (!FUSED) {
+  if constexpr (MODE != kT2Fused) {
     if (threadIdx.x == 0) partials[bid] = s;
   } else {
     const unsigned nb = gridDim.x * gridDim.y;
@@ -201,10 +239,10 @@ __device__ __forceinline__ double fma_sv(double a, double s, double c) {
   return r;
 }
 
-template <bool FUSED>
+template <int MODE>
 __global__ __launch_bounds__(kB) void table2d_stream_kernel(Table2DParams p, int rows_per_wave,
                                                             double* partials, unsigned* ticket,
-                                                            double* out) {
+                                                            double* out, Table2DChain chain) {
   __shared__ double tile[kSH * kSW];
   __shared__ double red[kB / kWave];
   __shared__ int is_last;
@@ -241,6 +279,13 @@ __global__ __launch_bounds__(kB) void table2d_stream_kernel(Table2DParams p, int
       const int rr = ly + kRowsPer * j;
       const unsigned off = (lx < w && rr < hgt) ? static_cast<unsigned>(rr * p.nx + lx) * 8u : 0u;
       v[j] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(tb) + off);
+    }
+    // chained: workgroup 0 closes the previous integration while its staging loads fly
+    // (the loads above hold 32 VGPRs; the kernel is LDS-limited to 4 waves per SIMD, whose
+    // 128-VGPR budget the close's 16 loads in flight fit beside them)
+    if constexpr (MODE == kT2Chained) {
+      if (chain.prev && blockIdx.x == 0 && blockIdx.y == 0)
+        table2d_close(chain.prev, chain.prev_n, chain.prev_out, red);
     }
 #pragma unroll
     for (int j = 0; j < kPasses; ++j) tile[(ly + kRowsPer * j) * kSW + lx] = v[j];
@@ -307,7 +352,7 @@ __global__ __launch_bounds__(kB) void table2d_stream_kernel(Table2DParams p, int
   for (int b = 0; b < kSCols; ++b) a += ok[b] ? acc[b] : 0.0;
   const double s = block_sum<kB>(a, red) * (sx * sy);
   const unsigned bid = blockIdx.y * gridDim.x + blockIdx.x;
-  if constexpr (!FUSED) {
+  if constexpr (MODE != kT2Fused) {
     if (threadIdx.x == 0) partials[bid] = s;
   } else {
     const unsigned nb = gridDim.x * gridDim.y;
@@ -406,28 +451,42 @@ static void check_table2d(const Table2DParams& p) {
   MIINT_CHECK(p.row0 >= 0 && p.row1 <= p.gy && p.row0 < p.row1, "table2d row range");
 }
 
-template <bool FUSED>
+template <int MODE>
 static void launch_table2d(const Table2DParams& p, double* partials, unsigned* ticket,
-                           double* out, hipStream_t stream) {
+                           double* out, Table2DChain chain, hipStream_t stream) {
   check_table2d(p);
   const Table2DShape sh = table2d_shape(p);
   if (sh.stream)
-    table2d_stream_kernel<FUSED><<<sh.grid, kB, 0, stream>>>(p, sh.rows_per_wave, partials,
-                                                             ticket, out);
+    table2d_stream_kernel<MODE><<<sh.grid, kB, 0, stream>>>(p, sh.rows_per_wave, partials,
+                                                            ticket, out, chain);
   else if (sh.tile == 128)
-    table2d_kernel<128, FUSED><<<sh.grid, kB, 0, stream>>>(p, partials, ticket, out);
+    table2d_kernel<128, MODE><<<sh.grid, kB, 0, stream>>>(p, partials, ticket, out, chain);
   else
-    table2d_kernel<64, FUSED><<<sh.grid, kB, 0, stream>>>(p, partials, ticket, out);
+    table2d_kernel<64, MODE><<<sh.grid, kB, 0, stream>>>(p, partials, ticket, out, chain);
   MIINT_HIP(hipGetLastError());
 }
 
 void launch_table2d_partials(const Table2DParams& p, double* partials, hipStream_t stream) {
-  launch_table2d<false>(p, partials, nullptr, nullptr, stream);
+  launch_table2d<kT2Partials>(p, partials, nullptr, nullptr, {nullptr, 0, nullptr}, stream);
 }
 
 void launch_table2d_fused(const Table2DParams& p, double* partials, unsigned* ticket,
                           double* out, hipStream_t stream) {
-  launch_table2d<true>(p, partials, ticket, out, stream);
+  launch_table2d<kT2Fused>(p, partials, ticket, out, {nullptr, 0, nullptr}, stream);
+}
+
+void launch_table2d_chained(const Table2DParams& p, double* partials, const double* prev,
+                            double* prev_out, hipStream_t stream) {
+  MIINT_CHECK(prev == nullptr || prev_out != nullptr, "chained table2d: prev without prev_out");
+  MIINT_CHECK(prev == nullptr || prev != partials, "chained table2d: prev aliases partials");
+  const int nb = table2d_grid(p);
+  launch_table2d<kT2Chained>(p, partials, nullptr, nullptr, {prev, nb, prev_out}, stream);
+}
+
+void launch_table2d_finalize(const double* partials, int n, double* out, hipStream_t stream) {
+  MIINT_CHECK(n >= 1, "table2d finalize: no partials");
+  table2d_finalize_kernel<<<1, kB, 0, stream>>>(partials, n, out);
+  MIINT_HIP(hipGetLastError());
 }
 
 }  // namespace miint

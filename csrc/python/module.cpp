@@ -342,6 +342,16 @@ PYBIND11_MODULE(_miint, m) {
     launch_table2d_fused(p, ptr<double>(partials), ptr<unsigned>(ticket), ptr<double>(out),
                          stream(s));
   });
+  m.def("launch_table2d_chained", [](uintptr_t table, int nx, int ny, double X, double Y, int gx,
+                                      int gy, int row0, int row1, uintptr_t partials,
+                                      uintptr_t prev, uintptr_t prev_out, uintptr_t s) {
+    Table2DParams p{ptr<const double>(table), nx, ny, X, Y, gx, gy, row0, row1};
+    launch_table2d_chained(p, ptr<double>(partials), ptr<const double>(prev),
+                           ptr<double>(prev_out), stream(s));
+  });
+  m.def("launch_table2d_finalize", [](uintptr_t partials, int n, uintptr_t out, uintptr_t s) {
+    launch_table2d_finalize(ptr<const double>(partials), n, ptr<double>(out), stream(s));
+  });
   m.def("launch_outer_product", [](uintptr_t v, int n, uintptr_t t, uintptr_t s) {
     launch_outer_product(ptr<const double>(v), n, ptr<double>(t), stream(s));
   });
@@ -369,20 +379,24 @@ PYBIND11_MODULE(_miint, m) {
 
   // ------------------------------------------------------------------ 2-D field plan
   py::class_<Table2DPlan>(m, "Table2DPlan")
-      .def(py::init([](int grid, double extent, int device, const Comm* comm, bool bucket) {
+      .def(py::init([](int grid, double extent, int device, const Comm* comm, bool bucket,
+                       bool chain) {
              Table2DConfig c;
              c.grid = grid;
              c.extent = extent;
              c.bucket = bucket;
+             c.chain = chain;
              return new Table2DPlan(c, device, comm);
            }),
            py::arg("grid") = 4096, py::arg("extent") = 1800.0, py::arg("device") = 0,
-           py::arg("comm") = nullptr, py::arg("bucket") = true, py::keep_alive<1, 5>())
+           py::arg("comm") = nullptr, py::arg("bucket") = true, py::arg("chain") = true,
+           py::keep_alive<1, 5>())
       .def("run", &Table2DPlan::run, py::call_guard<py::gil_scoped_release>())
       .def("time", &Table2DPlan::time, py::arg("iters"), py::arg("graphs") = true,
            py::call_guard<py::gil_scoped_release>())
       .def("last_result", &Table2DPlan::last_result)
       .def_property_readonly("bucketed", &Table2DPlan::bucketed)
+      .def_property_readonly("chained", &Table2DPlan::chained)
       .def_property_readonly("graph_steps", [](const Table2DPlan&) { return Table2DPlan::kGraphSteps; })
       .def_property_readonly("row0", &Table2DPlan::row0)
       .def_property_readonly("row1", &Table2DPlan::row1);

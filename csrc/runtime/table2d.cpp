@@ -32,6 +32,7 @@ Table2DPlan::Table2DPlan(const Table2DConfig& cfg, int device, const Comm* comm)
   const Table2DParams p{table_.get(), n, n, cfg.extent, cfg.extent, cfg.grid, cfg.grid,
                         row0_, std::max(row1_, row0_ + 1)};
   partials_ = DeviceBuffer<double>(static_cast<size_t>(table2d_grid(p)));
+  chain_ = DeviceBuffer<double>(2 * partials_.size());  // chained launches' double buffer
   fill_unset_slots(partials_.get(), partials_.size(), stream_.get());  // fused kernel's slots
   bucketed_ = cfg.bucket && comm_ && world_ > 1;
   result_ = DeviceBuffer<double>(kGraphSteps);
@@ -65,7 +66,7 @@ double Table2DPlan::run() {
   DeviceGuard g(device_);
   enqueue(stream_.get());
   stream_.sync();
-  last_bucketed_ = false;
+  last_batched_ = false;
   return host_[0];
 }
 
@@ -81,15 +82,37 @@ double Table2DPlan::time(int iters, bool graphs) {
     return Event::elapsed_ms(e0_, e1_) / iters;
   }
   const Comm* gc = comm_ && world_ > 1 ? comm_ : nullptr;  // group-wide graphs (loopback)
+  const bool multi = gc != nullptr;
+  const bool batched = !multi || bucketed_;  // kGraphSteps results land in one replay
   if (!graph_.ready())
     capture_with(gc, graph_, s, [&](hipStream_t cs) {
-      if (bucketed_) {  // kGraphSteps partials -> one all-reduce -> one copy
-        for (int i = 0; i < kGraphSteps; ++i) launch_local(result_.get() + i, cs);
+      if (!batched) {  // one 8-byte all-reduce per integration
+        for (int i = 0; i < kGraphSteps; ++i) enqueue(cs);
+        return;
+      }
+      // integration i's value -> outs[i]: mapped pinned memory on one rank, else the
+      // device slots one all-reduce (+ one copy) closes
+      double* outs = multi ? result_.get() : host_.device_ptr();
+      if (row1_ <= row0_) {  // more ranks than rows
+        MIINT_HIP(hipMemsetAsync(outs, 0, kGraphSteps * sizeof(double), cs));
+      } else if (chained()) {
+        const int n = static_cast<int>(oracle::profile_table().size());
+        const Table2DParams p{table_.get(), n, n, cfg_.extent, cfg_.extent, cfg_.grid,
+                              cfg_.grid, row0_, row1_};
+        const size_t nb = partials_.size();
+        for (int i = 0; i < kGraphSteps; ++i)
+          launch_table2d_chained(p, chain_.get() + (i & 1) * nb,
+                                 i ? chain_.get() + ((i - 1) & 1) * nb : nullptr,
+                                 i ? outs + i - 1 : nullptr, cs);
+        launch_table2d_finalize(chain_.get() + ((kGraphSteps - 1) & 1) * nb,
+                                static_cast<int>(nb), outs + kGraphSteps - 1, cs);
+      } else {
+        for (int i = 0; i < kGraphSteps; ++i) launch_local(outs + i, cs);
+      }
+      if (multi) {
         comm_->allreduce_sum(result_.get(), result_.get(), kGraphSteps, cs);
         MIINT_HIP(hipMemcpyAsync(host_.get(), result_.get(), kGraphSteps * sizeof(double),
                                  hipMemcpyDeviceToHost, cs));
-      } else {
-        for (int i = 0; i < kGraphSteps; ++i) enqueue(cs);
       }
     });
   const int launches = std::max(1, (iters + kGraphSteps - 1) / kGraphSteps);
@@ -98,12 +121,12 @@ double Table2DPlan::time(int iters, bool graphs) {
   for (int i = 0; i < launches; ++i) launch_with(gc, graph_, s);
   e1_.record(s);
   stream_.sync();
-  last_bucketed_ = bucketed_;
+  last_batched_ = batched;
   return Event::elapsed_ms(e0_, e1_) / (launches * kGraphSteps);
 }
 
 double Table2DPlan::last_result() const {
-  return last_bucketed_ ? host_[kGraphSteps - 1] : host_[0];
+  return last_batched_ ? host_[kGraphSteps - 1] : host_[0];
 }
 
 double table2d_oracle(int grid, double extent) {

@@ -7,6 +7,7 @@ import os
 import subprocess
 
 import pytest
+import torch
 
 from cuda_v_mpi_amd import Integrator
 from cuda_v_mpi_amd.utils import output
@@ -104,16 +105,57 @@ def test_plan_effective_div_fallback(cuda):
     assert it.run().value == pytest.approx(want, rel=1e-14)
 
 
-def test_table2d_plan_graph_replay(native, cuda):
+@pytest.mark.parametrize("grid", [4096, 1000])
+@pytest.mark.parametrize("chain", [True, False])
+def test_table2d_plan_graph_replay(native, cuda, grid, chain):
     """Table2DPlan: one integration matches the separable oracle; timing by hipGraph replays
-    of 32 integrations and by direct enqueue both work, and the value is unchanged after."""
-    plan = native.Table2DPlan(4096)
-    want = native.table2d_oracle(4096)
+    of 32 integrations (chained launches + one finalize, or 32 fused launches) and by direct
+    enqueue both work; the replays' last value is bitwise the direct run's."""
+    plan = native.Table2DPlan(grid, 1800.0, 0, None, True, chain)
+    assert plan.chained == chain
+    want = native.table2d_oracle(grid)
     v = plan.run()
     assert v == pytest.approx(want, rel=1e-14)
     assert plan.time(64, True) > 0
+    assert plan.last_result() == v
     assert plan.time(8, False) > 0
+    assert plan.last_result() == v
     assert plan.run() == v
+
+
+@pytest.mark.parametrize("grid,rows", [(4096, None), (4096, (1536, 2048)), (8192, (0, 1024)),
+                                       (1000, None), (333, (10, 200))])
+def test_table2d_chained_bitwise_equals_fused(native, cuda, grid, rows):
+    """Raw chained launches: 3 integrations through the double buffer (launch j's workgroup 0
+    closes launch j-1, a finalize closes the last) give bitwise the fused launch's value, on
+    both kernels (row stream: 4096/8192 grids; tile: 1000, 333) and on row slices."""
+    from cuda_v_mpi_amd.ops import kernels
+    from cuda_v_mpi_amd.utils import fixtures
+
+    v = torch.as_tensor(fixtures.profile_table(), device="cuda")
+    T = kernels.outer_product(v)
+    n = T.shape[0]
+    r0, r1 = rows or (0, grid)
+    args = (T.data_ptr(), n, n, 1800.0, 1800.0, grid, grid, r0, r1)
+    nb = native.table2d_grid(n, n, 1800.0, 1800.0, grid, grid, r0, r1)
+    s = torch.cuda.current_stream().cuda_stream
+    slots = torch.empty(nb, dtype=torch.float64, device="cuda")
+    native.fill_unset_slots(slots.data_ptr(), nb, s)
+    ticket = torch.zeros(native.TICKET_WORDS, dtype=torch.int32, device="cuda")
+    fused = torch.zeros(1, dtype=torch.float64, device="cuda")
+    native.launch_table2d_fused(*args, slots.data_ptr(), ticket.data_ptr(), fused.data_ptr(), s)
+    buf = torch.full((2, nb), float("nan"), dtype=torch.float64, device="cuda")
+    out = torch.full((3,), float("nan"), dtype=torch.float64, device="cuda")
+    for j in range(3):
+        prev = buf[(j - 1) & 1].data_ptr() if j else 0
+        native.launch_table2d_chained(*args, buf[j & 1].data_ptr(), prev,
+                                      out[j - 1].data_ptr() if j else 0, s)
+    native.launch_table2d_finalize(buf[0].data_ptr(), nb, out[2].data_ptr(), s)
+    torch.cuda.synchronize()
+    f = float(fused.item())
+    assert all(float(x) == f for x in out.cpu()), (out, f)
+    if rows is None and grid >= 1000:
+        assert f == pytest.approx(native.table2d_oracle(grid), rel=1e-14)
 
 
 def test_trainscan_native(native, cuda):

@@ -183,25 +183,28 @@ def test_trainscan_loopback_replicate(native, cuda, world):
 
 @pytest.mark.parametrize("world", [2, 3, 8])
 @pytest.mark.parametrize("grid", [4096, 1000])
-@pytest.mark.parametrize("bucket", [True, False])
-def test_table2d_loopback_matches_single(native, cuda, world, grid, bucket):
+@pytest.mark.parametrize("bucket,chain", [(True, True), (True, False), (False, True)])
+def test_table2d_loopback_matches_single(native, cuda, world, grid, bucket, chain):
     """The 2-D field (BASELINE #5) with its sample rows split over W ranks and the partials
     meeting in all-reduces, direct and as group-captured graph replays: bucketed (the 32
     integrations of one replay -> one 32-double all-reduce) or one 8-byte all-reduce per
-    integration. The timed replays' last global value equals the direct run's."""
+    integration. Bucketed replays run chained launches (launch j closes launch j-1) unless
+    chain=False. The timed replays' last global value equals the direct run's."""
     want = native.Table2DPlan(grid).run()
 
     def body(rank, comm):
-        p = native.Table2DPlan(grid, 1800.0, 0, comm, bucket)
+        p = native.Table2DPlan(grid, 1800.0, 0, comm, bucket, chain)
         v = p.run()
         ms = p.time(64, True)
         vt = p.last_result()
         v2 = p.run()
-        return dict(v=v, vt=vt, v2=v2, ms=ms, rows=(p.row0, p.row1), bucketed=p.bucketed)
+        return dict(v=v, vt=vt, v2=v2, ms=ms, rows=(p.row0, p.row1), bucketed=p.bucketed,
+                    chained=p.chained)
     out = loopback.run_ranks(world, body)
     assert sum(o["rows"][1] - o["rows"][0] for o in out) == grid
     for o in out:
         assert o["bucketed"] == bucket
+        assert o["chained"] == (chain and bucket)
         assert o["v"] == pytest.approx(want, rel=1e-15, abs=0)
         assert o["vt"] == o["v"] and o["v2"] == o["v"] and o["ms"] > 0
     grp = loopback.run_ranks.last_group

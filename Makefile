@@ -25,7 +25,7 @@ LDLIBS   := -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lrccl -lamdhip64 -lpthread
 
 HIP_SRC  := $(wildcard csrc/kernels/*.hip)
 RT_SRC   := $(wildcard csrc/runtime/*.cpp)
-HDRS     := $(wildcard csrc/include/miint/*.hpp)
+HDRS     := $(wildcard csrc/include/miint/*.hpp) $(wildcard csrc/runtime/*.inc)
 HIP_OBJ  := $(patsubst csrc/kernels/%.hip,$(OBJ)/k_%.o,$(HIP_SRC))
 RT_OBJ   := $(patsubst csrc/runtime/%.cpp,$(OBJ)/r_%.o,$(RT_SRC))
 LIB      := $(BUILD)/libmiint.a
@@ -78,7 +78,9 @@ clean:
 SAN := -fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-omit-frame-pointer -g -O1
 .PHONY: sanitize
 sanitize: $(BIN)/host_selftest_asan
-$(BIN)/host_selftest_asan: csrc/cli/host_selftest.cpp csrc/runtime/oracle.cpp csrc/runtime/profile_data.cpp csrc/runtime/comm.cpp csrc/runtime/runtime.cpp csrc/cli/cli_common.hpp $(HDRS) | $(BIN)
+SAN_SRC := csrc/cli/host_selftest.cpp csrc/runtime/oracle.cpp csrc/runtime/profile_data.cpp \
+           csrc/runtime/comm.cpp csrc/runtime/runtime.cpp csrc/runtime/host.cpp csrc/runtime/host_comm.cpp
+$(BIN)/host_selftest_asan: $(SAN_SRC) csrc/cli/cli_common.hpp $(HDRS) | $(BIN)
 	$(HIPCC) -x c++ -std=c++17 -Icsrc/include -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ $(SAN) \
-	  -o $@ csrc/cli/host_selftest.cpp csrc/runtime/oracle.cpp csrc/runtime/profile_data.cpp csrc/runtime/comm.cpp csrc/runtime/runtime.cpp \
+	  -o $@ $(SAN_SRC) \
 	  -L/opt/rocm/lib -lamdhip64 -lrccl -lpthread

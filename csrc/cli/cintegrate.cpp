@@ -15,12 +15,16 @@
 //                        (121999.800663 at 32x2; the last 8 s are dropped, B5)
 //   --kernel sin         the disabled cuda_function path: sin on [0, pi], STEPS = 1e9
 //   --gpus G / torchrun  split the samples across GPUs, RCCL all-reduce
+//   --device cpu [--threads T]  the same integrals on the host (miint/host.hpp): per-sample
+//                        interpolation on vector threads, host ranks under torchrun-style
+//                        env; --parity there is the reference's 64 sequential thread sums
 // "seconds" is the reference's process-start-to-print wall clock; --json's device_ms is one
 // warm integration (hipEvents), after an untimed cold one.
 #include <cmath>
 #include <cstdio>
 
 #include "cli_common.hpp"
+#include "miint/host.hpp"
 #include "miint/integrator.hpp"
 #include "miint/kernels.hpp"
 #include "miint/oracle.hpp"
@@ -30,7 +34,8 @@ using namespace miint;
 int main(int argc, char** argv) {
   try {
     cli::Args a(argc, argv);
-    const cli::Topology topo = cli::topology(a);
+    const bool cpu = cli::on_cpu(a);
+    const cli::Topology topo = cpu ? cli::Topology{} : cli::topology(a);
     const int sps = static_cast<int>(a.integer("steps-per-sec", oracle::kStepsPerSec));
     double seconds = oracle::kProfileSeconds;
     if (a.flag("parity")) {
@@ -41,6 +46,47 @@ int main(int argc, char** argv) {
     double result = 0.0, dev_ms = 0.0;
     std::mutex mu;
 
+    if (cpu) {  // the host engine; rank 0 prints
+      cli::HostRanks hr = cli::host_ranks(a);
+      HostPool pool(hr.threads);
+      RiemannConfig cfg;
+      if (sin_kernel) {
+        cfg.integrand = Integrand::kSin;
+        cfg.b = 3.14159265358979323846;
+        cfg.n = static_cast<uint64_t>(a.num("n", 1e9));
+      } else {
+        cfg.integrand = Integrand::kTable;
+        cfg.b = seconds;
+        cfg.n = static_cast<uint64_t>(seconds) * static_cast<uint64_t>(sps);
+      }
+      const double t0 = wall_seconds();
+      if (a.flag("parity") && !sin_kernel) {
+        MIINT_CHECK(sps == oracle::kStepsPerSec, "--parity uses the reference's 1e4 samples/s");
+        result = oracle::cintegrate_parity(static_cast<int>(a.integer("sp", 32)),
+                                           static_cast<int>(a.integer("sm", 2)));
+      } else {
+        uint64_t b = 0, c = 0;
+        rank_slice(cfg.n, hr.rank, hr.world, &b, &c);
+        result = c ? host_riemann(cfg, b, c, pool) : 0.0;
+        if (hr.comm) hr.comm->allreduce_sum(&result, 1);
+      }
+      const double host_ms = (wall_seconds() - t0) * 1e3;
+      if (hr.rank != 0) return 0;
+      const double secs = wall_seconds() - process_start_seconds();
+      std::printf("%lf seconds\n", secs);
+      std::printf("final distance is:%lf\n", result);
+      cli::emit(a, cli::JsonRecord()
+                       .add("program", "cintegrate")
+                       .add("device", "cpu")
+                       .add("isa", host_isa())
+                       .add("ranks", hr.world)
+                       .add("threads_per_rank", pool.threads())
+                       .add("parity", a.flag("parity"))
+                       .add("result", result)
+                       .add("host_ms", host_ms)
+                       .add("seconds_wall", secs));
+      return 0;
+    }
     if (a.flag("materialize") && !sin_kernel) {
       cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
         DeviceGuard g(dev);

@@ -11,6 +11,7 @@
 //     exercises every world > 1 path on a one-GPU box)
 #pragma once
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -24,6 +25,7 @@
 #include <vector>
 
 #include "miint/comm.hpp"
+#include "miint/host.hpp"
 #include "miint/runtime.hpp"
 
 namespace miint {
@@ -150,6 +152,36 @@ inline void run_ranks(const Topology& t,
   }
   for (auto& x : th) x.join();
   if (!err.empty()) throw Error(err);
+}
+
+// --device cpu: the reference's MPI side on this host (riemann.cpp / 4main.c are CPU
+// programs). Ranks are processes — under torchrun-style env (WORLD_SIZE, RANK,
+// LOCAL_WORLD_SIZE, MASTER_ADDR, MASTER_PORT; host collectives on MASTER_PORT + 19) — or
+// this one process; each rank runs --threads T workers (default: the cores shared among the
+// node's ranks). No HIP call is made on this path, so it runs on a GPU-less box.
+inline bool on_cpu(const Args& a) {
+  const std::string d = a.str("device", "gpu");
+  MIINT_CHECK(d == "gpu" || d == "cpu", "--device must be gpu|cpu");
+  return d == "cpu";
+}
+struct HostRanks {
+  int rank = 0, world = 1, threads = 1;
+  std::unique_ptr<HostComm> comm;  // world > 1
+};
+inline HostRanks host_ranks(const Args& a) {
+  HostRanks h;
+  h.world = env_int("WORLD_SIZE", 1);
+  h.rank = env_int("RANK", 0);
+  const int local = std::max(1, env_int("LOCAL_WORLD_SIZE", h.world));
+  const int cores = std::max(1, static_cast<int>(std::thread::hardware_concurrency()));
+  h.threads = static_cast<int>(a.integer("threads", 0));
+  if (h.threads <= 0) h.threads = std::max(1, cores / local);
+  if (h.world > 1) {
+    const char* addr = std::getenv("MASTER_ADDR");
+    h.comm.reset(new HostComm(addr ? addr : "127.0.0.1", env_int("MASTER_PORT", 29500) + 19,
+                              h.rank, h.world));
+  }
+  return h;
 }
 
 // --integrand names shared by every tool (SURVEY §5 config flags); unknown names fail.

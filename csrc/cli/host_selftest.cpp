@@ -6,7 +6,8 @@
 // sanitizers are not available on the target pool, so this binary exercises every host
 // code path that needs no device — profile generation, oracles, parity emulation of all
 // three reference programs, 64-bit slicing, CLI argument parsing, run records, the TCP
-// rendezvous of the native multi-process launch — under ASan/UBSan.
+// rendezvous of the native multi-process launch, the host engine (thread pool, vector
+// kernels, TCP host collectives, threaded train scan) — under ASan/UBSan.
 #include <cmath>
 #include <cstdio>
 #include <fstream>
@@ -18,6 +19,7 @@
 #include <unistd.h>
 
 #include "miint/comm.hpp"
+#include "miint/host.hpp"
 #include "miint/integrator.hpp"
 #include "miint/oracle.hpp"
 
@@ -119,6 +121,44 @@ int main() {
     timed_out = true;
   }
   expect(timed_out, "rendezvous: a rank whose rank 0 never listens times out");
+
+  // host engine (miint/host.hpp): vector kernels on a thread pool, the threaded reference
+  // program, the train scan with carries across 3 host ranks over the TCP star
+  {
+    HostPool pool(3);
+    RiemannConfig c;
+    c.integrand = Integrand::kSin;
+    c.b = M_PI;
+    c.n = 1000003;
+    c.rule = Rule::kMid;
+    expect(std::fabs(host_riemann(c, 0, c.n, pool) - 2.0) < 1e-12, "host engine: sin mid N=1e6+3");
+    c.integrand = Integrand::kTable;
+    c.b = 1800.0;
+    c.n = 18000000 / 64;
+    c.rule = Rule::kLeft;
+    expect(std::fabs(host_riemann(c, 0, c.n, pool) - 122000.004) < 1e-3, "host engine: table");
+    expect(host_riemann_mpi_parity(8, 1e6, M_PI, pool) == oracle::riemann_mpi_parity(8, 1e6),
+           "host engine: threaded riemann.cpp == serial parity oracle");
+    HostScanConfig sc;
+    sc.seconds = 30;
+    sc.keep = true;
+    const HostScanResult one = host_trainscan(sc, pool, nullptr);
+    std::vector<HostScanResult> rs(3);
+    std::vector<std::vector<double>> vel(3), posv(3);
+    std::vector<std::thread> hr;
+    const int hport = 20000 + (::getpid() + 7919) % 20000;
+    for (int k = 2; k >= 0; --k)
+      hr.emplace_back([&, k] {
+        HostComm comm("127.0.0.1", hport, k, 3, 30.0);
+        HostPool p2(2);
+        rs[k] = host_trainscan(sc, p2, &comm, &vel[k], &posv[k]);
+      });
+    for (auto& t : hr) t.join();
+    expect(std::fabs(rs[0].distance - one.distance) < 1e-9 * one.distance &&
+               rs[2].distance == rs[0].distance && vel[2].size() == rs[2].count &&
+               std::fabs(vel[2].back() / sc.steps_per_sec - one.distance) < 1e-9 * one.distance,
+           "host engine: train scan over 3 ranks (TCP star) == one rank");
+  }
 
   std::printf("%s\n", g_bad ? "HOST SELFTEST FAILED" : "HOST SELFTEST OK");
   return g_bad ? 1 : 0;

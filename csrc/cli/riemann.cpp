@@ -9,14 +9,21 @@
 // --parity reproduces the master/worker partition numerics (P-1 workers, (int)(N/W)
 // samples each, rank-order sum, P=1 -> 0) on the GPU.
 //
+// --device cpu runs the reference's own side of the comparison natively on the host: every
+// rank (process) integrates its slice on --threads T vector threads (miint/host.hpp), and
+// the ranks' partials meet in a rank-order host all-reduce; --parity emulates --ranks P
+// master/worker ranks (riemann.cpp:65-86) in this process.
+//
 //   ./riemann [--n 1e9] [--gpus G] [--integrand sin|pi4|poly|train] [--rule left|mid]
 //             [--dtype fp64|fp32] [--iters K] [--parity] [--json] [--jsonl FILE]
+//             [--device cpu [--threads T] [--ranks P]]
 #include <cmath>
 #include <cstdio>
 #include <iostream>
 #include <sstream>
 
 #include "cli_common.hpp"
+#include "miint/host.hpp"
 #include "miint/integrator.hpp"
 #include "miint/oracle.hpp"
 #include "miint/trace.hpp"
@@ -30,6 +37,74 @@ Rule parse_rule(const std::string& s) {
   if (s == "mid") return Rule::kMid;
   if (s == "right") return Rule::kRight;
   fail("unknown rule " + s, __FILE__, __LINE__);
+}
+
+void print_result(double secs, double hi, double nd, double result) {
+  std::printf("%lf seconds\n", secs);
+  std::cout.precision(15);
+  std::cout << "The integral of f(x) from 0.0 to " << hi << " with " << nd << " steps is "
+            << result << std::endl;
+}
+
+// --device cpu (see the header comment).
+int run_host(const cli::Args& a, const RiemannConfig& cfg, double nd, int iters) {
+  cli::HostRanks hr = cli::host_ranks(a);
+  HostPool pool(hr.threads);
+  double result = 0.0, host_ms = 0.0;
+  int ranks = hr.world;
+  if (a.flag("parity")) {
+    // riemann.cpp:65-86 as the reference runs it: P ranks -> P-1 workers on host threads,
+    // scalar libm sin and sequential sums, rank-order gather; P = 1 -> 0 (B10)
+    MIINT_CHECK(hr.world == 1, "--device cpu --parity emulates --ranks P in one process");
+    MIINT_CHECK(cfg.integrand == Integrand::kSin && cfg.a == 0.0,
+                "--device cpu --parity is the reference's sin on [0, b] program");
+    ranks = static_cast<int>(a.integer("ranks", 8));
+    MIINT_CHECK(ranks >= 1, "--ranks must be >= 1");
+    const double t0 = wall_seconds();
+    result = host_riemann_mpi_parity(ranks, nd, cfg.b, pool);
+    host_ms = (wall_seconds() - t0) * 1e3;
+  } else {
+    uint64_t b = 0, c = 0;
+    rank_slice(cfg.n, hr.rank, hr.world, &b, &c);
+    for (int i = 0; i < iters; ++i) {  // best of --iters
+      if (hr.comm) hr.comm->barrier();
+      const double t0 = wall_seconds();
+      double v = c ? host_riemann(cfg, b, c, pool) : 0.0;
+      if (hr.comm) hr.comm->allreduce_sum(&v, 1);
+      const double ms = (wall_seconds() - t0) * 1e3;
+      if (i == 0 || ms < host_ms) host_ms = ms;
+      result = v;
+    }
+    if (hr.comm) {  // the slowest rank's time
+      double t = -host_ms;
+      std::vector<double> all(hr.world);
+      hr.comm->allgather(&t, all.data(), 1);
+      for (double x : all) host_ms = std::max(host_ms, -x);
+    }
+  }
+  if (hr.rank != 0) return 0;
+  const double secs = wall_seconds() - process_start_seconds();
+  print_result(secs, cfg.b, nd, result);
+  const double exact = oracle::analytic(cfg.integrand, cfg.a, cfg.b, cfg.coef, cfg.p0, cfg.p1);
+  cli::emit(a, cli::JsonRecord()
+                   .add("program", "riemann")
+                   .add("device", "cpu")
+                   .add("isa", host_isa())
+                   .add("integrand", a.str("integrand", "sin"))
+                   .add("dtype", "fp64")
+                   .add("rule", a.str("rule", "left"))
+                   .add("n", nd)
+                   .add("ranks", ranks)
+                   .add("threads_per_rank", pool.threads())
+                   .add("parity", a.flag("parity"))
+                   .add("result", result)
+                   .add("analytic", exact)
+                   .add("abs_err", std::fabs(result - exact))
+                   .add("rel_err", std::fabs(result - exact) / std::fabs(exact))
+                   .add("host_ms", host_ms)
+                   .add("subintervals_per_s", host_ms > 0 ? nd / (host_ms * 1e-3) : 0.0)
+                   .add("seconds_wall", secs));
+  return 0;
 }
 
 }  // namespace
@@ -48,7 +123,7 @@ int main(int argc, char** argv) {
     const double nd = a.num("n", 1e9);  // riemann.cpp:10 STEPS
     const auto n = static_cast<uint64_t>(nd);
     const int iters = static_cast<int>(a.integer("iters", 1));
-    const cli::Topology topo = cli::topology(a);
+    MIINT_CHECK(iters >= 1, "--iters must be >= 1");
 
     RiemannConfig cfg;
     cfg.integrand = f;
@@ -62,6 +137,9 @@ int main(int argc, char** argv) {
     if (f == Integrand::kTrainVel) { cfg.p0 = oracle::kTrainTs; cfg.p1 = oracle::kTrainVs; }
     if (f == Integrand::kTable) cfg.table = oracle::profile_table();
     if (f == Integrand::kPoly) cfg.coef = {1.0, -0.5, 0.25, 0.125};
+
+    if (cli::on_cpu(a)) return run_host(a, cfg, nd, iters);
+    const cli::Topology topo = cli::topology(a);
 
     double result = 0.0, dev_ms = 0.0;
     if (a.flag("parity")) {
@@ -94,10 +172,7 @@ int main(int argc, char** argv) {
     }
     if (topo.rank0 != 0) return 0;
     const double secs = wall_seconds() - process_start_seconds();
-    std::printf("%lf seconds\n", secs);
-    std::cout.precision(15);
-    std::cout << "The integral of f(x) from 0.0 to " << hi << " with " << nd << " steps is "
-              << result << std::endl;
+    print_result(secs, hi, nd, result);
     const double exact = oracle::analytic(f, lo, hi, cfg.coef, cfg.p0, cfg.p1);
     cli::emit(a, cli::JsonRecord()
                      .add("program", "riemann")

@@ -13,19 +13,80 @@
 // printed element (P=7 -> 0.000000, P=16 -> 117642.707174). --replicate allgathers the full
 // table to every rank like 4main.c:157.
 //
+// --device cpu runs the pipeline on host threads (and host ranks under torchrun-style env):
+// per-thread closed totals, an exclusive scan of the thread/rank totals, one compensated
+// write pass of vel and pos (2 x 144 MB, as 4main.c materialises them; --no-keep forms the
+// totals only); --parity there is the reference's sequential emulation for --ranks P.
+//
 //   ./trainscan [--gpus G] [--parity] [--replicate] [--no-phase2] [--algo onepass|fused|lookback]
 //               [--steps-per-sec S] [--iters K] [--json] [--jsonl FILE]
+//               [--device cpu [--threads T] [--ranks P] [--no-keep]]
 #include <cstdio>
 
 #include "cli_common.hpp"
+#include "miint/host.hpp"
 #include "miint/oracle.hpp"
 #include "miint/trainscan.hpp"
 
 using namespace miint;
 
+namespace {
+
+int run_host(const cli::Args& a) {
+  cli::HostRanks hr = cli::host_ranks(a);
+  HostPool pool(hr.threads);
+  HostScanConfig c;
+  c.steps_per_sec = static_cast<int>(a.integer("steps-per-sec", oracle::kStepsPerSec));
+  c.keep = !a.flag("no-keep");
+  const int iters = static_cast<int>(a.integer("iters", 1));
+  if (hr.rank == 0) std::printf("Step size of %ld\n", static_cast<long>(c.steps_per_sec));
+  double distance = 0.0, sos = 0.0, best = 0.0;
+  int ranks = hr.world;
+  if (a.flag("parity")) {  // 4main.c's partitions and sequential sums for --ranks P
+    MIINT_CHECK(hr.world == 1 && c.steps_per_sec == oracle::kStepsPerSec,
+                "--device cpu --parity emulates --ranks P of 4main.c in one process");
+    ranks = static_cast<int>(a.integer("ranks", 1));
+    const double t0 = wall_seconds();
+    const oracle::TrainScanParity r = oracle::trainscan_parity(ranks);
+    distance = r.distance;
+    sos = r.sum_of_sums;
+    best = (wall_seconds() - t0) * 1e3;
+  } else {
+    std::vector<double> vel, pos;  // this rank's slice, materialised like 4main.c's arrays
+    for (int i = 0; i < iters; ++i) {  // best of --iters
+      if (hr.comm) hr.comm->barrier();
+      const HostScanResult r = host_trainscan(c, pool, hr.comm.get(), c.keep ? &vel : nullptr,
+                                              c.keep ? &pos : nullptr);
+      if (i == 0 || r.seconds * 1e3 < best) best = r.seconds * 1e3;
+      distance = r.distance;
+      sos = r.sum_of_sums;
+    }
+  }
+  if (hr.rank != 0) return 0;
+  const double secs = wall_seconds() - process_start_seconds();
+  std::printf("%lf seconds\n", secs);
+  std::printf("Total distance traveled = %lf\n", distance);
+  cli::emit(a, cli::JsonRecord()
+                   .add("program", "trainscan")
+                   .add("device", "cpu")
+                   .add("isa", host_isa())
+                   .add("ranks", ranks)
+                   .add("threads_per_rank", pool.threads())
+                   .add("parity", a.flag("parity"))
+                   .add("materialized", c.keep && !a.flag("parity"))
+                   .add("distance", distance)
+                   .add("sum_of_sums", sos)
+                   .add("host_ms", best)
+                   .add("seconds_wall", secs));
+  return 0;
+}
+
+}  // namespace
+
 int main(int argc, char** argv) {
   try {
     cli::Args a(argc, argv);
+    if (cli::on_cpu(a)) return run_host(a);
     const cli::Topology topo = cli::topology(a);
     TrainScanConfig cfg;
     cfg.steps_per_sec = static_cast<int>(a.integer("steps-per-sec", oracle::kStepsPerSec));

@@ -10,6 +10,7 @@
 #include <string>
 
 #include "miint/comm.hpp"
+#include "miint/host.hpp"
 #include "miint/integrator.hpp"
 #include "miint/kernels.hpp"
 #include "miint/oracle.hpp"
@@ -444,6 +445,66 @@ PYBIND11_MODULE(_miint, m) {
       .def("position_ptr", [](const TrainScan& t) { return reinterpret_cast<uintptr_t>(t.position()); })
       .def("replicated_ptr", [](const TrainScan& t) { return reinterpret_cast<uintptr_t>(t.replicated()); })
       .def_property_readonly("total", &TrainScan::total);
+
+  // ------------------------------------------------------------------ host (CPU) engine
+  m.def("host_isa", &host_isa, "vector ISA the host kernels dispatch to: avx512|avx2|base");
+  py::class_<HostPool>(m, "HostPool", "persistent host worker threads (0 = one per core)")
+      .def(py::init<int>(), py::arg("threads") = 0)
+      .def_property_readonly("threads", &HostPool::threads);
+  m.def("host_riemann", &host_riemann, py::arg("config"), py::arg("begin"), py::arg("count"),
+        py::arg("pool"), py::call_guard<py::gil_scoped_release>(),
+        "h * scale * sum of f over samples [begin, begin + count), per-sample fp64 on threads");
+  m.def("host_riemann_mpi_parity", &host_riemann_mpi_parity, py::arg("comm_size"), py::arg("n"),
+        py::arg("range"), py::arg("pool"), py::call_guard<py::gil_scoped_release>(),
+        "the reference's mpirun -np P ./riemann, bit for bit, with its P-1 workers on threads");
+  py::class_<HostComm>(m, "HostComm", "host collectives between processes (TCP star via rank 0)")
+      .def(py::init<const std::string&, int, int, int, double>(), py::arg("addr"),
+           py::arg("port"), py::arg("rank"), py::arg("world"), py::arg("timeout_s") = 120.0,
+           py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("rank", &HostComm::rank)
+      .def_property_readonly("world", &HostComm::world)
+      .def("allreduce_sum", [](HostComm& c, std::vector<double> v) {
+             py::gil_scoped_release nogil;
+             c.allreduce_sum(v.data(), v.size());
+             return v;
+           })
+      .def("allgather", [](HostComm& c, std::vector<double> v) {
+             std::vector<double> out(v.size() * c.world());
+             py::gil_scoped_release nogil;
+             c.allgather(v.data(), out.data(), v.size());
+             return out;
+           })
+      .def("broadcast", [](HostComm& c, std::vector<double> v, int root) {
+             py::gil_scoped_release nogil;
+             c.broadcast(v.data(), v.size(), root);
+             return v;
+           })
+      .def("barrier", &HostComm::barrier, py::call_guard<py::gil_scoped_release>());
+  m.def("host_trainscan", [](int sps, int seconds, HostPool& pool, HostComm* comm, bool keep) {
+          HostScanConfig c;
+          c.steps_per_sec = sps;
+          c.seconds = seconds;
+          c.keep = keep;
+          std::vector<double> vel, pos;
+          HostScanResult r;
+          {
+            py::gil_scoped_release nogil;
+            r = host_trainscan(c, pool, comm, keep ? &vel : nullptr, keep ? &pos : nullptr);
+          }
+          py::dict d;
+          d["distance"] = r.distance;
+          d["sum_of_sums"] = r.sum_of_sums;
+          d["seconds"] = r.seconds;
+          d["begin"] = r.begin;
+          d["count"] = r.count;
+          if (keep) {
+            d["velocity"] = vel;
+            d["position"] = pos;
+          }
+          return d;
+        },
+        py::arg("steps_per_sec") = 10000, py::arg("seconds") = 1800, py::arg("pool"),
+        py::arg("comm") = nullptr, py::arg("keep") = false);
 
   // ------------------------------------------------------------------ oracle
   py::module_ o = m.def_submodule("oracle", "host oracles, generated fixtures, parity emulation");

@@ -10,6 +10,9 @@ SURVEY §2.6) on top of the Python API, and adds JSON output:
     table2d     2-D velocity field v(x) v(y), bilinear, JSON      [--grid 4096 --iters 100]
     oracle      print every SURVEY §6.1 oracle value (CPU only)
     scale       GPU-count sweep 1,2,4,8: weak/strong efficiency, RCCL latency [--gpus 1,2,4,8]
+    compare     the reference's CUDA-vs-MPI comparison, measured here: the same integral on
+                the MI355X and on this host's cores (host engine; for sin also the reference's
+                own scalar MPI program on threads)        [--integrand sin --n 1e9 --ranks 8]
     info        devices and build
 
 Multi-GPU: launch under torchrun (one process per GPU); the process group is created from
@@ -44,7 +47,7 @@ def _ctx(backend=None):
 def cmd_riemann(a) -> int:
     from . import Integrator
 
-    ctx = _ctx()
+    ctx = _ctx("gloo" if a.backend in ("cpu", "host") else None)
     spec_b = {"sin": math.pi, "pi4": 1.0}.get(a.integrand, None)
     it = Integrator(a.integrand, n=int(a.n), rule=a.rule, dtype=a.dtype, ctx=ctx,
                     backend=a.backend)
@@ -62,7 +65,7 @@ def cmd_cintegrate(a) -> int:
     from . import Integrator
     from .parallel.decomposition import coverage_seconds
 
-    ctx = _ctx()
+    ctx = _ctx("gloo" if a.backend in ("cpu", "host") else None)
     seconds = coverage_seconds(a.sp * a.sm) if a.parity else 1800
     it = Integrator("table", n=seconds * 10000, rule="left", b=float(seconds), ctx=ctx,
                     backend=a.backend)
@@ -94,6 +97,62 @@ def cmd_trainscan(a) -> int:
         if a.json:
             print(json.dumps(r))
     ctx.destroy()
+    return 0
+
+
+def cmd_compare(a) -> int:
+    """The reference is a CUDA-vs-MPI comparison (its name; riemann.cpp vs cintegrate.cu):
+    one JSON row per side, measured in this process, plus the ratio."""
+    import time
+
+    from . import Integrator
+    from ._native import native
+
+    m = native()
+    n = int(a.n)
+    rows = []
+
+    def timed(fn, reps):
+        fn()  # warm: threads, code, clocks
+        best, v = float("inf"), None
+        for _ in range(reps):
+            t = time.perf_counter()
+            v = fn()
+            best = min(best, time.perf_counter() - t)
+        return v, best
+
+    host = Integrator(a.integrand, n=n, rule=a.rule, backend="host", threads=a.threads)
+    v, s = timed(lambda: host.run().value, a.reps)
+    rows.append({"side": "host", "what": f"host engine, {host._pool.threads} threads, "
+                 f"{m.host_isa()}, per-sample fp64", "value": v,
+                 "abs_err": abs(v - host.spec.analytic()), "seconds": s,
+                 "subintervals_per_s": n / s})
+    if a.integrand == "sin" and a.rule == "left":
+        pool = m.HostPool(a.threads)
+        v, s = timed(lambda: m.host_riemann_mpi_parity(a.ranks, float(n), math.pi, pool), 1)
+        rows.append({"side": "reference-program", "what": f"riemann.cpp as mpirun -np {a.ranks} "
+                     f"runs it ({a.ranks - 1} workers on threads, scalar libm sin)", "value": v,
+                     "abs_err": abs(v - 2.0), "seconds": s, "subintervals_per_s": n / s})
+    if m.device_count() > 0:
+        gpu = Integrator(a.integrand, n=n, rule=a.rule)
+        gpu.plan.prepare_steps(a.steps)
+        gpu.run_steps(a.steps)
+        t = gpu.run_steps(a.steps)
+        v = gpu.plan.host_result(gpu.plan.host_index_of(a.steps - 1, True))
+        s = t["device_ms"] * 1e-3 / a.steps
+        rows.append({"side": "gpu", "what": f"MI355X HIP kernels, hipGraph batches of {a.steps}",
+                     "value": v, "abs_err": abs(v - gpu.spec.analytic()), "seconds": s,
+                     "subintervals_per_s": n / s})
+    else:
+        rows.append({"side": "gpu", "skipped": "no HIP device visible"})
+    rate = {r["side"]: r.get("subintervals_per_s") for r in rows}
+    for r in rows:
+        print(json.dumps(r))
+    if rate.get("gpu") and rate.get("host"):
+        print(json.dumps({"speedup_gpu_vs_host": rate["gpu"] / rate["host"],
+                          "speedup_gpu_vs_reference_program":
+                          rate["gpu"] / rate["reference-program"]
+                          if rate.get("reference-program") else None}))
     return 0
 
 
@@ -192,7 +251,7 @@ def main(argv=None) -> int:
         sp.add_argument("--rule", default="left", choices=["left", "mid", "right"])
         sp.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
         sp.add_argument("--div", default="series", choices=["series", "ieee", "series_direct"])
-        sp.add_argument("--backend", default="hip", choices=["hip", "cpu"])
+        sp.add_argument("--backend", default="hip", choices=["hip", "host", "cpu"])
         sp.add_argument("--json", action="store_true")
 
     common(sub.add_parser("riemann"))
@@ -200,7 +259,7 @@ def main(argv=None) -> int:
     c.add_argument("--parity", action="store_true")
     c.add_argument("--sp", type=int, default=32)
     c.add_argument("--sm", type=int, default=2)
-    c.add_argument("--backend", default="hip", choices=["hip", "cpu"])
+    c.add_argument("--backend", default="hip", choices=["hip", "host", "cpu"])
     c.add_argument("--json", action="store_true")
     t = sub.add_parser("trainscan")
     t.add_argument("--parity", action="store_true")
@@ -213,6 +272,14 @@ def main(argv=None) -> int:
     t2.add_argument("--backend", default="hip", choices=["hip", "cpu"])
     sub.add_parser("oracle")
     sub.add_parser("info")
+    cp = sub.add_parser("compare")
+    cp.add_argument("--integrand", default="sin")
+    cp.add_argument("--n", type=float, default=1e9)
+    cp.add_argument("--rule", default="left", choices=["left", "mid", "right"])
+    cp.add_argument("--threads", type=int, default=0)
+    cp.add_argument("--ranks", type=int, default=8, help="reference program: mpirun -np P")
+    cp.add_argument("--reps", type=int, default=3)
+    cp.add_argument("--steps", type=int, default=48)
     sc = sub.add_parser("scale")
     sc.add_argument("--gpus", default="1,2,4,8")
     sc.add_argument("--steps", type=int, default=200)
@@ -230,7 +297,7 @@ def main(argv=None) -> int:
                             (["--md", a.md] if a.md else []))
     return {"riemann": cmd_riemann, "cintegrate": cmd_cintegrate, "trainscan": cmd_trainscan,
             "integrate": cmd_integrate, "table2d": cmd_table2d, "oracle": cmd_oracle,
-            "info": cmd_info}[a.cmd](a)
+            "info": cmd_info, "compare": cmd_compare}[a.cmd](a)
 
 
 if __name__ == "__main__":

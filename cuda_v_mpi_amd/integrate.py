@@ -10,6 +10,10 @@ Backends
            ``comm="torch"``: kernels on the torch stream + torch.distributed all_reduce;
            ``comm_obj=``: any native communicator, e.g. a loopback rank, see
            parallel/loopback.py)
+  ``host`` the native host engine (miint/host.hpp): the rank's slice evaluated per sample
+           in fp64 on ``threads`` vector threads (AVX-512 / AVX2 / baseline, picked at run
+           time), world > 1 reduced with torch.distributed (gloo). The reference's own (MPI,
+           CPU) side of its CUDA-vs-MPI comparison; needs no GPU.
   ``cpu``  plain PyTorch fp64 evaluation of the rank's slice + torch.distributed (gloo)
            all_reduce. Exists so the decomposition / collective logic can be exercised
            without a GPU; it is never used implicitly.
@@ -65,7 +69,7 @@ class Integrator:
                  backend: str = "hip", ctx: DistContext | None = None, comm: str = "native",
                  fused: bool = True, grid: int = 0, slots: int = 16, a: float | None = None,
                  b: float | None = None, force_collective: bool = False, bucket: bool = True,
-                 chain: bool = True, comm_obj=None, **spec_kw):
+                 chain: bool = True, comm_obj=None, threads: int = 0, **spec_kw):
         spec = integrands.get(integrand, **spec_kw) if isinstance(integrand, str) else integrand
         if a is not None or b is not None:
             spec = dataclasses.replace(spec, a=spec.a if a is None else a,
@@ -85,12 +89,14 @@ class Integrator:
         self.begin, self.count = decomposition.rank_slice(self.n, self.ctx.rank, self.ctx.world)
         self._plan = None
         self._comm = None
-        if backend == "hip":
+        self._pool = None
+        if backend in ("hip", "host"):
             from ._native import native
 
             m = native()
-            if m.device_count() < 1:
-                raise RuntimeError("backend='hip' needs a HIP device; use backend='cpu' explicitly")
+            if backend == "hip" and m.device_count() < 1:
+                raise RuntimeError("backend='hip' needs a HIP device; use backend='host' or "
+                                   "'cpu' explicitly")
             cfg = m.RiemannConfig()
             cfg.integrand = getattr(m.Integrand, spec.name)
             cfg.a, cfg.b, cfg.n = spec.a, spec.b, self.n
@@ -104,6 +110,11 @@ class Integrator:
             cfg.force_collective = force_collective
             cfg.bucket = bucket
             cfg.chain = chain
+            self._m = m
+            if backend == "host":
+                self._cfg = cfg
+                self._pool = m.HostPool(threads)
+                return
             if comm_obj is not None:
                 self._comm = comm_obj
                 self._plan = m.RiemannPlan(cfg, comm_obj.device, comm_obj)
@@ -113,9 +124,8 @@ class Integrator:
             else:
                 cfg.rank, cfg.world = self.ctx.rank, self.ctx.world
                 self._plan = m.RiemannPlan(cfg, self.ctx.device)
-            self._m = m
         elif backend != "cpu":
-            raise ValueError("backend must be 'hip' or 'cpu'")
+            raise ValueError("backend must be 'hip', 'host' or 'cpu'")
 
     # ------------------------------------------------------------------ info
     @property
@@ -159,6 +169,12 @@ class Integrator:
         dev_s = 0.0
         if self.backend == "cpu":
             value = self._torch_reduce(self._cpu_local()) if self.ctx.world > 1 else self._cpu_local()
+        elif self.backend == "host":
+            t = time.perf_counter()
+            value = self._m.host_riemann(self._cfg, self.begin, self.count, self._pool)
+            dev_s = time.perf_counter() - t  # the rank's compute time ("device" = host cores)
+            if self.ctx.world > 1:
+                value = self._torch_reduce(value)
         else:
             if self._comm is not None or self.ctx.world == 1:
                 t = self._plan.run_steps(1, pipeline=False, graphs=False)

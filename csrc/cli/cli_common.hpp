@@ -173,9 +173,10 @@ inline HostRanks host_ranks(const Args& a) {
   h.world = env_int("WORLD_SIZE", 1);
   h.rank = env_int("RANK", 0);
   const int local = std::max(1, env_int("LOCAL_WORLD_SIZE", h.world));
-  const int cores = std::max(1, static_cast<int>(std::thread::hardware_concurrency()));
+  // --threads, else the node's host threads (HostPool's default: MIINT_HOST_THREADS /
+  // OMP_NUM_THREADS / affinity) shared among the node's ranks
   h.threads = static_cast<int>(a.integer("threads", 0));
-  if (h.threads <= 0) h.threads = std::max(1, cores / local);
+  if (h.threads <= 0) h.threads = std::max(1, HostPool::default_threads() / local);
   if (h.world > 1) {
     const char* addr = std::getenv("MASTER_ADDR");
     h.comm.reset(new HostComm(addr ? addr : "127.0.0.1", env_int("MASTER_PORT", 29500) + 19,

@@ -39,12 +39,14 @@ namespace miint {
 
 class HostPool {
  public:
-  // threads <= 0: std::thread::hardware_concurrency() (at least 1).
+  // threads <= 0: MIINT_HOST_THREADS, else OMP_NUM_THREADS, else the CPUs in this process's
+  // affinity mask (at least 1).
   explicit HostPool(int threads = 0);
   ~HostPool();
   HostPool(const HostPool&) = delete;
   HostPool& operator=(const HostPool&) = delete;
   int threads() const { return n_; }
+  static int default_threads();
   // fn(t) for every t in [0, threads()): t = 0 on the calling thread, the others on the
   // pool's workers. Returns when every call has returned; rethrows the first exception.
   void run(const std::function<void(int)>& fn);

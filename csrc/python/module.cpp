@@ -450,7 +450,8 @@ PYBIND11_MODULE(_miint, m) {
   m.def("host_isa", &host_isa, "vector ISA the host kernels dispatch to: avx512|avx2|base");
   py::class_<HostPool>(m, "HostPool", "persistent host worker threads (0 = one per core)")
       .def(py::init<int>(), py::arg("threads") = 0)
-      .def_property_readonly("threads", &HostPool::threads);
+      .def_property_readonly("threads", &HostPool::threads)
+      .def_static("default_threads", &HostPool::default_threads);
   m.def("host_riemann", &host_riemann, py::arg("config"), py::arg("begin"), py::arg("count"),
         py::arg("pool"), py::call_guard<py::gil_scoped_release>(),
         "h * scale * sum of f over samples [begin, begin + count), per-sample fp64 on threads");

@@ -3,6 +3,8 @@
 // and 4main.c:82-122 run by P MPI processes.
 #include "miint/host.hpp"
 
+#include <sched.h>
+
 #include <cmath>
 #include <cstdint>
 #include <algorithm>
@@ -92,8 +94,22 @@ const char* host_isa() {
 }
 
 // ------------------------------------------------------------------ pool
+// Default pool size: MIINT_HOST_THREADS, else OMP_NUM_THREADS (how a job's CPU share is
+// usually given: the GPU pool sets it to 16 per GPU), else the CPUs this process may run
+// on (sched_getaffinity), else std::thread::hardware_concurrency().
+int HostPool::default_threads() {
+  for (const char* k : {"MIINT_HOST_THREADS", "OMP_NUM_THREADS"}) {
+    const char* v = std::getenv(k);
+    if (v && std::atoi(v) > 0) return std::atoi(v);
+  }
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  if (sched_getaffinity(0, sizeof(set), &set) == 0 && CPU_COUNT(&set) > 0) return CPU_COUNT(&set);
+  return static_cast<int>(std::thread::hardware_concurrency());
+}
+
 HostPool::HostPool(int threads) {
-  n_ = threads > 0 ? threads : static_cast<int>(std::thread::hardware_concurrency());
+  n_ = threads > 0 ? threads : default_threads();
   if (n_ < 1) n_ = 1;
   for (int t = 1; t < n_; ++t) th_.emplace_back([this, t] { worker(t); });
 }

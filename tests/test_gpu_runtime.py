@@ -377,3 +377,19 @@ def test_bench_contract(native, cuda):
     b3 = js["baseline3_strong_1e10"]
     assert b3["N"] == 10**10 and abs(b3["abs_err"] - 1e-10) < 1e-13 and b3["value"] > 1e11
     assert js["rccl_version"] and js["per_rank_ms"] and js["launcher"] == "single"
+
+
+def test_compare_gpu_vs_host(native, cuda):
+    """`compare` (the reference's CUDA-vs-MPI comparison, measured on one box): the GPU row,
+    the host engine row and the reference program on threads all integrate sin on [0, pi] to
+    the same value; the GPU is faster than the host cores."""
+    p = subprocess.run(["python", "-m", "cuda_v_mpi_amd", "compare", "--n", "1e8", "--reps", "1"],
+                       capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr
+    rows = [json.loads(x) for x in p.stdout.splitlines()]
+    by = {r["side"]: r for r in rows if "side" in r}
+    assert set(by) == {"host", "reference-program", "gpu"}
+    for r in by.values():
+        assert abs(r["value"] - 2.0) < 1e-12, r
+    assert by["reference-program"]["value"] == native.oracle.riemann_mpi_parity(8, 1e8)
+    assert rows[-1]["speedup_gpu_vs_host"] > 1.0

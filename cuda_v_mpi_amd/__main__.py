@@ -136,7 +136,9 @@ def cmd_compare(a) -> int:
     if m.device_count() > 0:
         gpu = Integrator(a.integrand, n=n, rule=a.rule)
         gpu.plan.prepare_steps(a.steps)
-        gpu.run_steps(a.steps)
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 0.06:  # clock settle, as bench.py (--settle-ms)
+            gpu.run_steps(a.steps)
         t = gpu.run_steps(a.steps)
         v = gpu.plan.host_result(gpu.plan.host_index_of(a.steps - 1, True))
         s = t["device_ms"] * 1e-3 / a.steps

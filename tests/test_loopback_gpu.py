@@ -102,9 +102,11 @@ def _trainscan(native, world, **cfg_kw):
         r2 = ts.run()  # a second pipeline on the same plan: workspaces re-armed
         if ts.algo == "fused":  # fixed-order tile prefixes: bitwise reproducible
             assert r2["distance"] == r["distance"] and r2["sum_of_sums"] == r["sum_of_sums"]
-        else:  # decoupled look-back sums whatever predecessor state it finds first
-            assert r2["distance"] == pytest.approx(r["distance"], rel=1e-15, abs=0)
-            assert r2["sum_of_sums"] == pytest.approx(r["sum_of_sums"], rel=1e-15, abs=0)
+        else:  # decoupled look-back sums whatever predecessor state it finds first: the
+            # grouping of ~4400 tile aggregates varies run to run (seen: 1.1e-15 relative on
+            # the 1.1e16 sum of sums), so a few ulps, not bitwise
+            assert r2["distance"] == pytest.approx(r["distance"], rel=1e-14, abs=0)
+            assert r2["sum_of_sums"] == pytest.approx(r["sum_of_sums"], rel=1e-14, abs=0)
         out = dict(r, begin=ts.local_begin, count=ts.local_count, algo=ts.algo)
         if cfg_kw.get("replicate"):
             full = torch.empty(ts.total, dtype=torch.float64, device="cuda")

@@ -130,6 +130,13 @@ class RcclComm final : public Comm {
                   hipStream_t s) const override;
   void check_async() const override;
   void abort() const override;
+  // Thread-local capture: RCCL's own threads (proxy, bootstrap) may make HIP calls while a
+  // rank's stream is capturing; in global mode any such call invalidates the capture, in
+  // thread-local mode only this thread's calls are checked.
+  void capture(Graph& g, hipStream_t s,
+               const std::function<void(hipStream_t)>& body) const override {
+    g.capture(s, body, hipStreamCaptureModeThreadLocal);
+  }
 
   static void group_start();
   static void group_end();

@@ -6,7 +6,8 @@ every GPU count the node has,
 
   * ``bench.py --gpus N`` (one process per GPU, spawned by bench.py itself; RCCL over xGMI):
     the weak-scaling headline (1e9 samples per GPU) and, from the same run, BASELINE #3's
-    strong-scaling point (N = 1e10 in total over the N GPUs);
+    strong-scaling point (N = 1e10 in total over the N GPUs) and BASELINE #5's 2-D field
+    (4096^2 samples in total, rows split over the N GPUs);
   * ``miint comm --gpus N`` (one process driving N GPUs, ncclCommInitAll): all-reduce and
     all-gather latency at 8 B (the Riemann payload, riemann.cpp:76) and 144 MB (4main.c:157's
     broadcast table),
@@ -104,6 +105,9 @@ def sweep(counts: list[int], steps: int = 200, warmup: int = 10, comm: bool = Tr
         if s:
             row["strong_1e10_value"] = s["value"]
             row["strong_1e10_ms"] = s["ms_per_step"]
+        t2 = b.get("baseline5_table2d_4096")
+        if t2:
+            row["t2d_4096_us"] = t2["ms_per_integration"] * 1e3
         if comm:
             row.update(run_comm(n))
         rows.append(row)
@@ -115,12 +119,14 @@ def sweep(counts: list[int], steps: int = 200, warmup: int = 10, comm: bool = Tr
         r["weak_eff"] = r["value"] / (n * base["value"])
         if "strong_1e10_value" in r and "strong_1e10_value" in base:
             r["strong_eff"] = r["strong_1e10_value"] / (n * base["strong_1e10_value"])
+        if "t2d_4096_us" in r and "t2d_4096_us" in base:  # fixed total work: strong
+            r["t2d_strong_eff"] = base["t2d_4096_us"] / (n * r["t2d_4096_us"])
     return rows
 
 
 def markdown(rows: list[dict]) -> str:
     cols = ["n_gpus", "value", "ms_per_step", "weak_eff", "strong_1e10_value", "strong_eff",
-            "per_rank_spread_ms", "rccl_world", "allreduce_8B_us", "allgather_8B_us",
+            "t2d_4096_us", "t2d_strong_eff", "per_rank_spread_ms", "rccl_world", "allreduce_8B_us", "allgather_8B_us",
             "allreduce_144MB_us", "allgather_144MB_us"]
     out = ["| " + " | ".join(cols) + " |", "|" + "---|" * len(cols)]
     for r in rows:

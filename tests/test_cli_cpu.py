@@ -110,12 +110,15 @@ def test_scale_sweep_rows_and_efficiency(monkeypatch):
     monkeypatch.setattr(scaling, "run_bench", lambda n, s, w: {
         "value": fake[n], "ms_per_step": 0.075, "per_rank_spread_ms": 0.001,
         "rccl_world": n if n > 1 else None, "config": {"graphs": True}, "verified": True,
-        "baseline3_strong_1e10": {"value": fake[n] * 1.05, "ms_per_step": 0.7}})
+        "baseline3_strong_1e10": {"value": fake[n] * 1.05, "ms_per_step": 0.7},
+        "baseline5_table2d_4096": {"ms_per_integration": 0.009 / n ** 0.8}})
     monkeypatch.setattr(scaling, "run_comm", lambda n: {"allreduce_8B_us": 10.0 * n})
     rows = scaling.sweep([1, 2, 4, 8])
     assert [r["n_gpus"] for r in rows] == [1, 2, 4, 8]
     assert rows[2]["skipped"] == "only 2 devices" and rows[3]["skipped"] == "only 2 devices"
     assert rows[0]["weak_eff"] == 1.0 and abs(rows[1]["weak_eff"] - 0.95) < 1e-12
     assert abs(rows[1]["strong_eff"] - 0.95) < 1e-12
+    assert abs(rows[1]["t2d_4096_us"] - 9.0 / 2 ** 0.8) < 1e-9
+    assert abs(rows[1]["t2d_strong_eff"] - 2 ** 0.8 / 2) < 1e-12
     md = scaling.markdown(rows)
     assert "skipped: only 2 devices" in md and md.count("\n") == 5

@@ -32,7 +32,8 @@ record also gets: the same config with IEEE division per sample ("ieee_div"), th
 path's per-point error against IEEE division on a 64 K-sample window ("per_point_max_ulp"),
 BASELINE config #3 — N = 1e10 in total, strong-scaled over the same GPUs
 ("baseline3_strong_1e10") — and BASELINE config #5 — the 4096^2 2-D velocity field with its
-rows split over the same GPUs ("baseline5_table2d_4096").
+rows split over the same GPUs ("baseline5_table2d_4096") — and the same integral on the
+node's host cores (the native host engine, the reference's own CPU/MPI side: "host_engine").
 """
 from __future__ import annotations
 
@@ -91,7 +92,8 @@ def parse(argv=None) -> argparse.Namespace:
     p.add_argument("--force-collective", action="store_true",
                    help="run the RCCL all-reduce stage even on 1 GPU (tests the multi-GPU graph)")
     p.add_argument("--no-extras", action="store_true",
-                   help="skip the post-timing extras (IEEE run, per-point ulp, N=1e10 strong, 2-D field)")
+                   help="skip the post-timing extras (IEEE run, per-point ulp, N=1e10 strong, 2-D field, "
+                        "host engine)")
     p.add_argument("--sweep-gpus", default="",
                    help="e.g. 1,2,4,8: run the scaling sweep (cuda_v_mpi_amd/parallel/scaling.py) "
                         "over these GPU counts instead of one benchmark")
@@ -458,6 +460,29 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
             "rel_err_vs_oracle": abs(v - want) / want, "rows_this_rank": [p2.row0, p2.row1],
             "bucketed_allreduce": bool(p2.bucketed), "n_gpus": ctx.world}
         del p2, comm2
+    # (5) the reference's own side of its CUDA-vs-MPI comparison: the same integral on this
+    #     node's host cores (native host engine, per-sample fp64 vector threads, each rank
+    #     its slice with its share of the cores, best of 3, slowest rank)
+    import torch
+
+    from cuda_v_mpi_amd import native
+
+    m = native()
+    local = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", ctx.world)))
+    share_given = any(os.environ.get(k) for k in ("MIINT_HOST_THREADS", "OMP_NUM_THREADS"))
+    threads = m.HostPool.default_threads() if share_given else \
+        max(1, m.HostPool.default_threads() // local)
+    host = Integrator(args.integrand, n=n_total, rule=args.rule, backend="host", ctx=ctx,
+                      threads=threads)
+    host.run()  # warm: threads, pages
+    best = min(host.run().seconds_device for _ in range(3))
+    t = torch.tensor([best], dtype=torch.float64, device=dev)
+    ctx.all_reduce_max(t)
+    v = host.run().value
+    out["host_engine"] = {"value": n_total / float(t.item()), "ms": float(t.item()) * 1e3,
+                          "ranks": ctx.world, "threads_per_rank": threads,
+                          "isa": m.host_isa(), "result": v,
+                          "abs_err": abs(v - host.spec.analytic())}
     return out
 
 

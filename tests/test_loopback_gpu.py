@@ -143,8 +143,10 @@ def test_trainscan_loopback_matches_single(native, cuda, world, algo):
     for o in out:
         assert o["timeout"] == 0
         assert o["algo"] == ("fused" if algo == "onepass" else algo)  # onepass needs totals first
-        assert o["distance"] == pytest.approx(one["distance"], rel=4e-15, abs=0)
-        assert o["sum_of_sums"] == pytest.approx(one["sum_of_sums"], rel=4e-15, abs=0)
+        # look-back groupings vary run to run (1.1e-15 seen between two one-rank runs)
+        tol = 1e-14 if algo == "lookback" else 4e-15
+        assert o["distance"] == pytest.approx(one["distance"], rel=tol, abs=0)
+        assert o["sum_of_sums"] == pytest.approx(one["sum_of_sums"], rel=tol, abs=0)
 
 
 @pytest.mark.parametrize("world,want", [(1, "122000.004030"), (2, None), (7, "0.000000"),

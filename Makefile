@@ -21,7 +21,7 @@ PY_INC     := $(shell $(PYTHON) -m pybind11 --includes)
 COMMON   := -std=c++17 -O3 -fPIC -Icsrc/include -Wall -Wno-unused-function
 DEVFLAGS := $(COMMON) --offload-arch=$(ARCH)
 HOSTFLAGS:= $(COMMON) -I/opt/rocm/include -D__HIP_PLATFORM_AMD__
-LDLIBS   := -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lrccl -lamdhip64 -lpthread -ldl
+LDLIBS   := -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lrccl -lhiprtc -lamdhip64 -lpthread -ldl
 
 HIP_SRC  := $(wildcard csrc/kernels/*.hip)
 RT_SRC   := $(wildcard csrc/runtime/*.cpp)

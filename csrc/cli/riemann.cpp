@@ -14,15 +14,21 @@
 // the ranks' partials meet in a rank-order host all-reduce; --parity emulates --ranks P
 // master/worker ranks (riemann.cpp:65-86) in this process.
 //
+// --expr "EXPR" integrates any f(x) given as one C++ expression over x (HIP device math:
+// sin, exp, pow, ...), compiled at run time for gfx950 with hipRTC (miint/expr.hpp) — where
+// the reference edits riemann.cpp:37 and recompiles. --analytic V adds the error vs V.
+//
 //   ./riemann [--n 1e9] [--gpus G] [--integrand sin|pi4|poly|train] [--rule left|mid]
 //             [--dtype fp64|fp32] [--iters K] [--parity] [--json] [--jsonl FILE]
-//             [--device cpu [--threads T] [--ranks P]]
+//             [--device cpu [--threads T] [--ranks P]] [--expr EXPR --a A --b B [--analytic V]]
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <iostream>
 #include <sstream>
 
 #include "cli_common.hpp"
+#include "miint/expr.hpp"
 #include "miint/host.hpp"
 #include "miint/integrator.hpp"
 #include "miint/oracle.hpp"
@@ -107,6 +113,45 @@ int run_host(const cli::Args& a, const RiemannConfig& cfg, double nd, int iters)
   return 0;
 }
 
+// --expr (see the header comment): GPU ranks as in the default path, f compiled by hipRTC.
+int run_expr(const cli::Args& a, const RiemannConfig& cfg, double nd, int iters) {
+  MIINT_CHECK(!cli::on_cpu(a), "--expr runs on the GPU (hipRTC); drop --device cpu");
+  const std::string expr = a.str("expr", "");
+  const cli::Topology topo = cli::topology(a);
+  double result = 0.0, dev_ms = 0.0;
+  std::mutex mu;
+  cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
+    ExprIntegrator ei(expr, dev);
+    uint64_t b = 0, c = 0;
+    rank_slice(cfg.n, rank, topo.world, &b, &c);
+    const double v = ei.integrate(cfg.a, cfg.b, cfg.n, cfg.rule, b, c, 1.0, comm);
+    const double ms = ei.time(cfg.a, cfg.b, cfg.n, cfg.rule, b, c, iters);
+    std::lock_guard<std::mutex> g(mu);
+    if (rank == topo.rank0) result = v;
+    dev_ms = std::max(dev_ms, ms);
+  });
+  if (topo.rank0 != 0) return 0;
+  const double secs = wall_seconds() - process_start_seconds();
+  print_result(secs, cfg.b, nd, result);
+  cli::JsonRecord r;
+  r.add("program", "riemann")
+      .add("expr", expr)
+      .add("a", cfg.a)
+      .add("b", cfg.b)
+      .add("n", nd)
+      .add("rule", a.str("rule", "left"))
+      .add("gpus", topo.world)
+      .add("result", result);
+  if (a.has("analytic")) {
+    const double exact = a.num("analytic", 0.0);
+    r.add("analytic", exact).add("abs_err", std::fabs(result - exact));
+  }
+  cli::emit(a, r.add("device_ms", dev_ms)
+                   .add("subintervals_per_s", dev_ms > 0 ? nd / (dev_ms * 1e-3) : 0.0)
+                   .add("seconds_wall", secs));
+  return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -138,6 +183,7 @@ int main(int argc, char** argv) {
     if (f == Integrand::kTable) cfg.table = oracle::profile_table();
     if (f == Integrand::kPoly) cfg.coef = {1.0, -0.5, 0.25, 0.125};
 
+    if (a.has("expr")) return run_expr(a, cfg, nd, iters);
     if (cli::on_cpu(a)) return run_host(a, cfg, nd, iters);
     const cli::Topology topo = cli::topology(a);
 

@@ -10,6 +10,7 @@
 #include <string>
 
 #include "miint/comm.hpp"
+#include "miint/expr.hpp"
 #include "miint/host.hpp"
 #include "miint/integrator.hpp"
 #include "miint/kernels.hpp"
@@ -445,6 +446,29 @@ PYBIND11_MODULE(_miint, m) {
       .def("position_ptr", [](const TrainScan& t) { return reinterpret_cast<uintptr_t>(t.position()); })
       .def("replicated_ptr", [](const TrainScan& t) { return reinterpret_cast<uintptr_t>(t.replicated()); })
       .def_property_readonly("total", &TrainScan::total);
+
+  // ------------------------------------------------------------------ runtime integrands
+  m.def("expr_source", &expr_source, "kernel source generated for an expression over x");
+  m.def("expr_compile", [](const std::string& e) {
+          std::string code;
+          {
+            py::gil_scoped_release nogil;
+            code = expr_compile(e);
+          }
+          return py::bytes(code);
+        },
+        "compile an expression for gfx950 with hipRTC (no device needed); the code object");
+  py::class_<ExprIntegrator>(m, "ExprIntegrator",
+                             "f(x) given as an expression, compiled with hipRTC for gfx950")
+      .def(py::init<const std::string&, int, int>(), py::arg("expr"), py::arg("device") = 0,
+           py::arg("grid") = 2048)
+      .def("integrate", &ExprIntegrator::integrate, py::arg("a"), py::arg("b"), py::arg("n"),
+           py::arg("rule"), py::arg("begin"), py::arg("count"), py::arg("scale") = 1.0,
+           py::arg("comm") = nullptr, py::call_guard<py::gil_scoped_release>())
+      .def("time", &ExprIntegrator::time, py::arg("a"), py::arg("b"), py::arg("n"),
+           py::arg("rule"), py::arg("begin"), py::arg("count"), py::arg("iters"),
+           py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("expression", &ExprIntegrator::expression);
 
   // ------------------------------------------------------------------ host (CPU) engine
   m.def("host_isa", &host_isa, "vector ISA the host kernels dispatch to: avx512|avx2|base");

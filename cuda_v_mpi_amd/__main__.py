@@ -7,6 +7,7 @@ SURVEY §2.6) on top of the Python API, and adds JSON output:
     cintegrate  train distance from the profile (cintegrate.cu)  [--parity --sp 32 --sm 2]
     trainscan   two-phase prefix scan (4main.c)                   [--parity --algo lookback]
     integrate   any integrand, JSON result                        [--integrand --n --rule ...]
+                or any f(x):  --expr "exp(-x*x)" --a 0 --b 3 (compiled at run time, hipRTC)
     table2d     2-D velocity field v(x) v(y), bilinear, JSON      [--grid 4096 --iters 100]
     oracle      print every SURVEY §6.1 oracle value (CPU only)
     scale       GPU-count sweep 1,2,4,8: weak/strong efficiency, RCCL latency [--gpus 1,2,4,8]
@@ -161,6 +162,18 @@ def cmd_compare(a) -> int:
 def cmd_integrate(a) -> int:
     from . import Integrator
 
+    if a.expr:  # any f(x): compiled at run time with hipRTC (ops.kernels.riemann_expr)
+        from .ops import kernels
+
+        lo = 0.0 if a.a is None else a.a
+        hi = 1.0 if a.b is None else a.b
+        v = kernels.riemann_expr(a.expr, lo, hi, int(a.n), rule=a.rule)
+        rec = {"expr": a.expr, "a": lo, "b": hi, "n": int(a.n), "rule": a.rule, "value": v}
+        if a.analytic is not None:
+            rec.update(analytic=a.analytic, abs_err=abs(v - a.analytic))
+        print(json.dumps(rec))
+        return 0
+
     ctx = _ctx()
     r = Integrator(a.integrand, n=int(a.n), rule=a.rule, dtype=a.dtype, div=a.div, ctx=ctx,
                    backend=a.backend).run()
@@ -267,7 +280,12 @@ def main(argv=None) -> int:
     t.add_argument("--parity", action="store_true")
     t.add_argument("--algo", default="fused", choices=["fused", "onepass", "lookback"])
     t.add_argument("--json", action="store_true")
-    common(sub.add_parser("integrate"), integrand="pi4")
+    ig = sub.add_parser("integrate")
+    common(ig, integrand="pi4")
+    ig.add_argument("--expr", default="", help="any f(x) as one C++ expression over x (hipRTC)")
+    ig.add_argument("--a", type=float, default=None)
+    ig.add_argument("--b", type=float, default=None)
+    ig.add_argument("--analytic", type=float, default=None)
     t2 = sub.add_parser("table2d")
     t2.add_argument("--grid", type=int, default=4096)
     t2.add_argument("--iters", type=int, default=100)

@@ -330,3 +330,25 @@ def block_ops(x: torch.Tensor, block: int) -> tuple[torch.Tensor, torch.Tensor]:
     native().selftest_block_ops(x.data_ptr(), x.numel(), block, f32, sums.data_ptr(),
                                 scan.data_ptr(), _stream())
     return sums, scan
+
+
+_EXPR_CACHE: dict = {}
+
+
+def riemann_expr(expr: str, a: float, b: float, n: int, rule: str = "left",
+                 i_begin: int = 0, n_local: int | None = None) -> float:
+    """Riemann sum of any f(x) given as one C++ expression over ``x`` (HIP device math:
+    ``"exp(-x*x)"``, ``"sin(x)/x"``, ...), compiled for gfx950 at run time with hipRTC
+    (csrc/runtime/expr.cpp) and cached per (expression, device). Every sample is evaluated
+    in fp64; the value is h * sum over samples [i_begin, i_begin + n_local) of the n-sample
+    rule on [a, b]. The reference hard-wires sin (riemann.cpp:37) and recompiles to change it.
+    """
+    m = native()
+    dev = _device().index
+    key = (expr, dev)
+    ei = _EXPR_CACHE.get(key)
+    if ei is None:
+        ei = _EXPR_CACHE[key] = m.ExprIntegrator(expr, dev)
+    n_local = n - i_begin if n_local is None else n_local
+    return ei.integrate(float(a), float(b), int(n), getattr(m.Rule, rule), int(i_begin),
+                        int(n_local))

@@ -4,11 +4,13 @@
 // changing it means editing the source and recompiling (no argv, no config).
 // Here `riemann --expr "exp(-x*x)" --a 0 --b 3` (or kernels.riemann_expr in Python) turns
 // the expression into a HIP device function `double f(double x) { return (EXPR); }`, builds a
-// grid-stride partial-sum kernel and a finalize kernel around it with hipRTC
+// partial-sum kernel and a finalize kernel around it with hipRTC
 // (--offload-arch=gfx950 -O3), loads the code object and integrates:
 //
-//   miint_expr_partials  2048 x 256 lanes, every sample evaluated per lane in fp64, wave64
-//                        butterfly (__shfl_xor) + 4-wave LDS sum -> one partial per workgroup
+//   miint_expr_partials  2048 x 256 lanes, each a contiguous run of samples walked with an
+//                        exact fp64 index, every sample evaluated in fp64 (4 accumulators),
+//                        wave64 butterfly (__shfl_xor) + 4-wave LDS sum -> one partial per
+//                        workgroup
 //   miint_expr_finalize  one workgroup sums the partials in index order -> h * scale * sum
 //
 // Fixed grid and fixed reduction order: bitwise reproducible. Compiled programs are cached

@@ -49,16 +49,34 @@ std::string expr_source(const std::string& expr) {
   return R"(
 __device__ __forceinline__ double miint_f(double x) { return ()" + expr + R"(); }
 
-// Every sample on its own: x = a + (i + off) h with the index converted exactly (i < 2^52).
+// Every sample on its own. Lane g owns a contiguous run of the slice (balanced: the first
+// n mod lanes lanes take one more) and walks it with an exact fp64 index (idx += 1, exact
+// below 2^52), so a sample costs fma(idx, h, a), f and an add: no per-sample 64-bit integer
+// to fp64 conversion. Four independent accumulators for ILP.
 extern "C" __global__ __launch_bounds__(256) void miint_expr_partials(
     double a, double h, double off, unsigned long long i0, unsigned long long n,
     double* partials) {
   __shared__ double red[4];
   const unsigned long long lanes = (unsigned long long)gridDim.x * 256ull;
-  double acc = 0.0;
-  for (unsigned long long i = (unsigned long long)blockIdx.x * 256ull + threadIdx.x; i < n;
-       i += lanes)
-    acc += miint_f(fma((double)(i0 + i) + off, h, a));
+  const unsigned long long g = (unsigned long long)blockIdx.x * 256ull + threadIdx.x;
+  const unsigned long long q = n / lanes, r = n % lanes;
+  const unsigned long long start = g * q + (g < r ? g : r);
+  const unsigned cnt = (unsigned)(q + (g < r ? 1ull : 0ull));
+  double idx = (double)(i0 + start) + off;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  unsigned k = 0;
+  for (; k + 4 <= cnt; k += 4) {
+    a0 += miint_f(fma(idx, h, a));
+    a1 += miint_f(fma(idx + 1.0, h, a));
+    a2 += miint_f(fma(idx + 2.0, h, a));
+    a3 += miint_f(fma(idx + 3.0, h, a));
+    idx += 4.0;
+  }
+  for (; k < cnt; ++k) {
+    a0 += miint_f(fma(idx, h, a));
+    idx += 1.0;
+  }
+  double acc = (a0 + a1) + (a2 + a3);
   for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);  // wave64 butterfly
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();

@@ -38,7 +38,7 @@ def test_expr_pi4_headline_config(native, cuda):
 @pytest.mark.parametrize("expr,a,b,want", [
     ("exp(-x*x)", 0.0, 3.0, math.sqrt(math.pi) / 2 * math.erf(3.0)),
     ("1.0 / sqrt(1.0 - x*x)", -0.5, 0.5, 2 * math.asin(0.5)),
-    ("x > 1.0 ? 2.0 : x", 0.0, 2.0, 2.5),
+    ("x > 1.0 ? 2.0 * x - 1.0 : x * x", 0.0, 2.0, 7.0 / 3.0),
     ("pow(x, 3.0) - 2.0 * x", -1.0, 3.0, (81 - 1) / 4 - (9 - 1)),
 ])
 def test_expr_midpoint_analytic(cuda, expr, a, b, want):

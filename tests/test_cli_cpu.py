@@ -7,6 +7,8 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -122,3 +124,36 @@ def test_scale_sweep_rows_and_efficiency(monkeypatch):
     assert abs(rows[1]["t2d_strong_eff"] - 2 ** 0.8 / 2) < 1e-12
     md = scaling.markdown(rows)
     assert "skipped: only 2 devices" in md and md.count("\n") == 5
+
+
+def test_bench_driver_launch_form_json_contract():
+    """The driver's exact launch form (torch.distributed.run, 127.0.0.1, a chosen port) on the
+    CPU (gloo ranks): rank 0 prints ONE line carrying every field of the bench contract, with
+    the whole-job value and the MAX over ranks as the step time."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+                        "--master-port", str(port), os.path.join(REPO, "bench.py"),
+                        "--gpus", "2", "--steps", "3", "--warmup", "1", "--device", "cpu",
+                        "--backend", "gloo", "--samples", "3e4", "--settle-ms", "0"],
+                       capture_output=True, text=True, timeout=300, cwd=REPO)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.strip().splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    js = json.loads(lines[0])
+    for k, t in (("metric", str), ("value", float), ("unit", str), ("n_gpus", int),
+                 ("steps", int), ("warmup", int), ("ms_per_step", float),
+                 ("higher_is_better", bool), ("scaling", str), ("vs_baseline", float),
+                 ("dtype", str), ("data", str), ("config", dict)):
+        assert isinstance(js[k], t), k
+    for k in ("model", "global_batch", "seq_len", "parallelism"):
+        assert k in js["config"], k
+    assert js["n_gpus"] == 2 and js["steps"] == 3 and js["warmup"] == 1
+    assert js["launcher"] == "torchrun" and js["scaling"] == "weak"
+    assert js["metric"].startswith("Riemann subintervals/sec at N=1e9 fp64")
+    assert js["ms_per_step"] == pytest.approx(max(js["per_rank_ms"]))
+    assert js["value"] == pytest.approx(js["config"]["N"] * 3 / (js["ms_per_step"] * 3e-3))

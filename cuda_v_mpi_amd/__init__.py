@@ -9,7 +9,12 @@ Capabilities of the reference (Excalibur1224/Cuda-v-MPI: riemann.cpp, cintegrate
     fused sums, and a single-pass decoupled look-back prefix scan;
   * multi-GPU: one process per GPU, RCCL all-reduce / all-gather over xGMI, hipGraph replay;
   * the reference's CLIs and stdout format (build/bin/{riemann,cintegrate,trainscan,miint}
-    and ``python -m cuda_v_mpi_amd``), with --parity emulation of its partition arithmetic.
+    and ``python -m cuda_v_mpi_amd``), with --parity emulation of its partition arithmetic;
+  * the reference's CPU (MPI) side, native: per-ISA vector kernels on host threads, host
+    ranks with rank-order TCP collectives (``backend="host"``, ``--device cpu``,
+    ``python -m cuda_v_mpi_amd compare``);
+  * any integrand at run time: one C++ expression over x compiled for gfx950 with hipRTC
+    (``ops.kernels.riemann_expr``, ``riemann --expr``).
 
 Layout: models/ (integrands), ops/ (kernel entry points), parallel/ (decomposition,
 process groups), utils/ (fixtures, oracles, output formats), integrate.py (high-level API).

@@ -8,6 +8,7 @@
 # for the CUDA or 4main programs, a target whose source does not exist — SURVEY C18/B17).
 
 HIPCC    ?= /opt/rocm/bin/hipcc
+HOSTCXX  ?= g++
 ARCH     ?= gfx950
 PYTHON   ?= python3
 BUILD    := build
@@ -30,7 +31,7 @@ HIP_OBJ  := $(patsubst csrc/kernels/%.hip,$(OBJ)/k_%.o,$(HIP_SRC))
 RT_OBJ   := $(patsubst csrc/runtime/%.cpp,$(OBJ)/r_%.o,$(RT_SRC))
 LIB      := $(BUILD)/libmiint.a
 EXT      := $(PKG)/_miint$(EXT_SUFFIX)
-CLIS     := $(BIN)/riemann $(BIN)/cintegrate $(BIN)/trainscan $(BIN)/miint
+CLIS     := $(BIN)/riemann $(BIN)/cintegrate $(BIN)/trainscan $(BIN)/miint $(BIN)/miintrun
 
 .PHONY: all ext cli lib clean asm
 all: ext cli
@@ -59,6 +60,10 @@ $(EXT): $(OBJ)/py_module.o $(HIP_OBJ) $(RT_OBJ)
 
 $(OBJ)/cli_%.o: csrc/cli/%.cpp csrc/cli/cli_common.hpp $(HDRS) | $(OBJ)
 	$(HIPCC) -x c++ $(HOSTFLAGS) -c $< -o $@
+
+# the launcher links no HIP (it must never initialise a GPU: it forks and execs the ranks)
+$(BIN)/miintrun: csrc/cli/miintrun.cpp | $(BIN)
+	$(HOSTCXX) -std=c++17 -O2 -Wall -o $@ $<
 
 $(BIN)/%: $(OBJ)/cli_%.o $(LIB) | $(BIN)
 	$(HIPCC) -o $@ $< $(LIB) $(LDLIBS)

@@ -99,3 +99,23 @@ def test_bench_self_spawned_ranks(native, cuda, g):
     assert js["verified"] and js["n_gpus"] == g and js["launcher"] == "spawn"
     assert js["rccl_world"] == g and len(js["per_rank_ms"]) == g
     assert js["baseline3_strong_1e10"]["n_per_gpu"] == 10**10 // g
+
+
+@pytest.mark.parametrize("g", [1, 2, 8])
+def test_miintrun_gpu_ranks(native, cuda, g):
+    """`miintrun -np G riemann` (the mpirun form): one process per GPU, RCCL bootstrapped from
+    the launcher's environment (the native TCP rendezvous), rank 0 prints the global value —
+    equal to the one-process integration. G = 1 runs on the one-GPU pool."""
+    if _devices() < g:
+        pytest.skip(f"needs {g} HIP devices")
+    run = os.path.join(BIN, "miintrun")
+    if not os.path.exists(run):
+        pytest.skip("miintrun not built")
+    args = [os.path.join(BIN, "riemann"), "--integrand", "pi4", "--rule", "mid", "--json"]
+    one = _run(args)
+    many = _run([run, "-np", str(g), *args])
+    assert one.returncode == 0 and many.returncode == 0, many.stderr[-2000:]
+    a = json.loads(one.stdout.strip().splitlines()[-1])["result"]
+    b = json.loads(many.stdout.strip().splitlines()[-1])
+    assert b["gpus"] == g
+    assert b["result"] == pytest.approx(a, rel=1e-15, abs=0)

@@ -16,7 +16,8 @@
 //
 // --expr "EXPR" integrates any f(x) given as one C++ expression over x (HIP device math:
 // sin, exp, pow, ...), compiled at run time for gfx950 with hipRTC (miint/expr.hpp) — where
-// the reference edits riemann.cpp:37 and recompiles. --analytic V adds the error vs V.
+// the reference edits riemann.cpp:37 and recompiles; with --device cpu, compiled for the
+// host cores instead (HostExpr). --analytic V adds the error vs V.
 //
 //   ./riemann [--n 1e9] [--gpus G] [--integrand sin|pi4|poly|train] [--rule left|mid]
 //             [--dtype fp64|fp32] [--iters K] [--parity] [--json] [--jsonl FILE]
@@ -113,9 +114,44 @@ int run_host(const cli::Args& a, const RiemannConfig& cfg, double nd, int iters)
   return 0;
 }
 
+// --expr --device cpu: host ranks, f compiled for the host cores (HostExpr).
+int run_host_expr(const cli::Args& a, const RiemannConfig& cfg, double nd, int iters) {
+  const std::string expr = a.str("expr", "");
+  cli::HostRanks hr = cli::host_ranks(a);
+  HostPool pool(hr.threads);
+  const HostExpr he(expr);
+  uint64_t b = 0, c = 0;
+  rank_slice(cfg.n, hr.rank, hr.world, &b, &c);
+  double result = 0.0, host_ms = 0.0;
+  for (int i = 0; i < iters; ++i) {  // best of --iters
+    if (hr.comm) hr.comm->barrier();
+    const double t0 = wall_seconds();
+    double v = c ? he.integrate(cfg.a, cfg.b, cfg.n, cfg.rule, b, c, pool) : 0.0;
+    if (hr.comm) hr.comm->allreduce_sum(&v, 1);
+    const double ms = (wall_seconds() - t0) * 1e3;
+    if (i == 0 || ms < host_ms) host_ms = ms;
+    result = v;
+  }
+  if (hr.rank != 0) return 0;
+  const double secs = wall_seconds() - process_start_seconds();
+  print_result(secs, cfg.b, nd, result);
+  cli::JsonRecord r;
+  r.add("program", "riemann").add("device", "cpu").add("expr", expr).add("a", cfg.a)
+      .add("b", cfg.b).add("n", nd).add("rule", a.str("rule", "left")).add("ranks", hr.world)
+      .add("threads_per_rank", pool.threads()).add("result", result);
+  if (a.has("analytic")) {
+    const double exact = a.num("analytic", 0.0);
+    r.add("analytic", exact).add("abs_err", std::fabs(result - exact));
+  }
+  cli::emit(a, r.add("host_ms", host_ms)
+                   .add("subintervals_per_s", host_ms > 0 ? nd / (host_ms * 1e-3) : 0.0)
+                   .add("seconds_wall", secs));
+  return 0;
+}
+
 // --expr (see the header comment): GPU ranks as in the default path, f compiled by hipRTC.
 int run_expr(const cli::Args& a, const RiemannConfig& cfg, double nd, int iters) {
-  MIINT_CHECK(!cli::on_cpu(a), "--expr runs on the GPU (hipRTC); drop --device cpu");
+  if (cli::on_cpu(a)) return run_host_expr(a, cfg, nd, iters);
   const std::string expr = a.str("expr", "");
   const cli::Topology topo = cli::topology(a);
   double result = 0.0, dev_ms = 0.0;

@@ -31,6 +31,9 @@
 
 namespace miint {
 
+// Throws unless `expr` is one C++ expression over x (allowed characters only; no statements,
+// braces, literals, asm/volatile/goto or __builtin_amdgcn*). Shared by the GPU and host JITs.
+void expr_check(const std::string& expr);
 // The kernel source generated for `expr` (throws on a rejected expression).
 std::string expr_source(const std::string& expr);
 // Compile `expr` for gfx950 with hipRTC (no device needed); returns the code object. Throws

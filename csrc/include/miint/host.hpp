@@ -79,6 +79,25 @@ double host_riemann(const RiemannConfig& cfg, uint64_t begin, uint64_t count, Ho
 // (riemann.cpp:82-85). Equals oracle::riemann_mpi_parity, which runs the workers serially.
 double host_riemann_mpi_parity(int comm_size, double n, double range, HostPool& pool);
 
+// A runtime integrand on the host: f(x) given as one C++ expression over x (the rules of
+// expr_check, as for the GPU's hipRTC path), compiled by the system C++ compiler into a
+// shared object (-O3 -march=native, scalar libm per sample, compensated blocks; compiler:
+// MIINT_HOST_CXX, else /opt/rocm/llvm/bin/clang++, else c++) and dlopen'ed; cached per
+// expression in the process.
+class HostExpr {
+ public:
+  explicit HostExpr(const std::string& expr);
+  // h * sum f(a + (i + off) h) over [begin, begin + count) of the n-sample rule on [a, b],
+  // thread slices added in thread order.
+  double integrate(double a, double b, uint64_t n, Rule rule, uint64_t begin, uint64_t count,
+                   HostPool& pool) const;
+  const std::string& expression() const { return expr_; }
+
+ private:
+  std::string expr_;
+  void* fn_ = nullptr;
+};
+
 // Host collectives across processes: a TCP star through rank 0 (rank 0 listens on
 // addr:port, every other rank connects once and keeps its socket). Reductions sum in rank
 // order on rank 0, so every rank receives bitwise the same values. Every receive is bounded

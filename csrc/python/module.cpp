@@ -479,6 +479,13 @@ PYBIND11_MODULE(_miint, m) {
   m.def("host_riemann", &host_riemann, py::arg("config"), py::arg("begin"), py::arg("count"),
         py::arg("pool"), py::call_guard<py::gil_scoped_release>(),
         "h * scale * sum of f over samples [begin, begin + count), per-sample fp64 on threads");
+  py::class_<HostExpr>(m, "HostExpr", "f(x) as an expression, compiled for the host cores")
+      .def(py::init<const std::string&>(), py::arg("expr"),
+           py::call_guard<py::gil_scoped_release>())
+      .def("integrate", &HostExpr::integrate, py::arg("a"), py::arg("b"), py::arg("n"),
+           py::arg("rule"), py::arg("begin"), py::arg("count"), py::arg("pool"),
+           py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("expression", &HostExpr::expression);
   m.def("host_riemann_mpi_parity", &host_riemann_mpi_parity, py::arg("comm_size"), py::arg("n"),
         py::arg("range"), py::arg("pool"), py::call_guard<py::gil_scoped_release>(),
         "the reference's mpirun -np P ./riemann, bit for bit, with its P-1 workers on threads");

@@ -10,11 +10,11 @@
 namespace miint {
 
 namespace {
-
 constexpr int kExprBlock = 256;
+}  // namespace
 
 // One C++ expression over x: no statements, blocks, asm or literals that could smuggle them.
-void check_expression(const std::string& e) {
+void expr_check(const std::string& e) {
   MIINT_CHECK(!e.empty() && e.size() <= 4096, "expression must be 1..4096 characters");
   for (char c : e) {
     const bool ok = std::isalnum(static_cast<unsigned char>(c)) ||
@@ -39,12 +39,12 @@ void check_expression(const std::string& e) {
   }
 }
 
+namespace {
 std::string rtc_error(hiprtcResult r) { return hiprtcGetErrorString(r); }
-
 }  // namespace
 
 std::string expr_source(const std::string& expr) {
-  check_expression(expr);
+  expr_check(expr);
   // hipRTC compiles this with its own HIP headers (device math, __shfl_xor, blockIdx, ...).
   return R"(
 __device__ __forceinline__ double miint_f(double x) { return ()" + expr + R"(); }

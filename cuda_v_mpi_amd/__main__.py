@@ -122,19 +122,42 @@ def cmd_compare(a) -> int:
             best = min(best, time.perf_counter() - t)
         return v, best
 
-    host = Integrator(a.integrand, n=n, rule=a.rule, backend="host", threads=a.threads)
-    v, s = timed(lambda: host.run().value, a.reps)
-    rows.append({"side": "host", "what": f"host engine, {host._pool.threads} threads, "
-                 f"{m.host_isa()}, per-sample fp64", "value": v,
-                 "abs_err": abs(v - host.spec.analytic()), "seconds": s,
-                 "subintervals_per_s": n / s})
-    if a.integrand == "sin" and a.rule == "left":
+    if a.expr:  # any f(x): compiled for the host cores and, below, with hipRTC for gfx950
+        lo = 0.0 if a.a is None else a.a
+        hi = 1.0 if a.b is None else a.b
+        pool = m.HostPool(a.threads)
+        he = m.HostExpr(a.expr)
+        rl = getattr(m.Rule, a.rule)
+        v, s = timed(lambda: he.integrate(lo, hi, n, rl, 0, n, pool), a.reps)
+        rows.append({"side": "host", "what": f"{a.expr} compiled for the host, "
+                     f"{pool.threads} threads, scalar libm per sample", "value": v,
+                     "seconds": s, "subintervals_per_s": n / s})
+    else:
+        host = Integrator(a.integrand, n=n, rule=a.rule, backend="host", threads=a.threads)
+        v, s = timed(lambda: host.run().value, a.reps)
+        rows.append({"side": "host", "what": f"host engine, {host._pool.threads} threads, "
+                     f"{m.host_isa()}, per-sample fp64", "value": v,
+                     "abs_err": abs(v - host.spec.analytic()), "seconds": s,
+                     "subintervals_per_s": n / s})
+    if a.integrand == "sin" and a.rule == "left" and not a.expr:
         pool = m.HostPool(a.threads)
         v, s = timed(lambda: m.host_riemann_mpi_parity(a.ranks, float(n), math.pi, pool), 1)
         rows.append({"side": "reference-program", "what": f"riemann.cpp as mpirun -np {a.ranks} "
                      f"runs it ({a.ranks - 1} workers on threads, scalar libm sin)", "value": v,
                      "abs_err": abs(v - 2.0), "seconds": s, "subintervals_per_s": n / s})
-    if m.device_count() > 0:
+    if m.device_count() > 0 and a.expr:
+        from .ops import kernels
+
+        ei = m.ExprIntegrator(a.expr, 0)
+        rl = getattr(m.Rule, a.rule)
+        v = ei.integrate(lo, hi, n, rl, 0, n)
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 0.06:  # clock settle
+            ei.time(lo, hi, n, rl, 0, n, 4)
+        s = ei.time(lo, hi, n, rl, 0, n, a.steps) * 1e-3
+        rows.append({"side": "gpu", "what": f"{a.expr} compiled with hipRTC for gfx950",
+                     "value": v, "seconds": s, "subintervals_per_s": n / s})
+    elif m.device_count() > 0:
         gpu = Integrator(a.integrand, n=n, rule=a.rule)
         gpu.plan.prepare_steps(a.steps)
         t0 = time.perf_counter()
@@ -300,6 +323,9 @@ def main(argv=None) -> int:
     cp.add_argument("--ranks", type=int, default=8, help="reference program: mpirun -np P")
     cp.add_argument("--reps", type=int, default=3)
     cp.add_argument("--steps", type=int, default=48)
+    cp.add_argument("--expr", default="", help="any f(x) as one C++ expression over x")
+    cp.add_argument("--a", type=float, default=None)
+    cp.add_argument("--b", type=float, default=None)
     sc = sub.add_parser("scale")
     sc.add_argument("--gpus", default="1,2,4,8")
     sc.add_argument("--steps", type=int, default=200)

@@ -88,3 +88,17 @@ def test_cli_riemann_expr(cuda):
     assert lines[1].startswith("The integral of f(x) from 0.0 to 3 with 100000000 steps is 0.8862")
     rec = json.loads(lines[-1])
     assert rec["abs_err"] < 1e-13 and rec["subintervals_per_s"] > 1e10
+
+
+def test_compare_expr_gpu_and_host(native, cuda):
+    """`compare --expr`: the same expression compiled for gfx950 (hipRTC) and for the host
+    cores agrees to 1e-12; the GPU row is the faster one."""
+    p = subprocess.run(["python", "-m", "cuda_v_mpi_amd", "compare", "--expr", "exp(-x*x)",
+                        "--a", "0", "--b", "3", "--n", "1e8", "--rule", "mid", "--reps", "1"],
+                       capture_output=True, text=True, timeout=300, cwd=REPO)
+    assert p.returncode == 0, p.stderr
+    rows = [json.loads(x) for x in p.stdout.splitlines()]
+    by = {r["side"]: r for r in rows if "side" in r}
+    assert by["gpu"]["value"] == pytest.approx(by["host"]["value"], rel=1e-12)
+    assert by["gpu"]["value"] == pytest.approx(math.sqrt(math.pi) / 2 * math.erf(3.0), rel=1e-12)
+    assert rows[-1]["speedup_gpu_vs_host"] > 1.0

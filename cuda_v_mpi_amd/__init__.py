@@ -24,5 +24,5 @@ from __future__ import annotations
 __version__ = "0.1.0"
 
 from ._native import native, require_gpu  # noqa: F401
-from .integrate import IntegrationResult, Integrator, integrate  # noqa: F401
+from .integrate import IntegrationResult, Integrator, integrate, integrate_expr  # noqa: F401
 from .models import integrands  # noqa: F401

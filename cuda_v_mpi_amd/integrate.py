@@ -207,3 +207,40 @@ class Integrator:
 
 def integrate(integrand: str = "pi4", n: int = 10**9, **kw) -> IntegrationResult:
     return Integrator(integrand, n=n, **kw).run()
+
+
+def integrate_expr(expr: str, a: float, b: float, n: int = 10**9, rule: str = "left",
+                   backend: str = "hip", ctx: DistContext | None = None, threads: int = 0,
+                   analytic: float | None = None) -> IntegrationResult:
+    """Integrate any f(x) given as one C++ expression over ``x`` (``"exp(-x*x)"``): compiled
+    for gfx950 with hipRTC (``backend="hip"``) or for the host cores (``backend="host"``),
+    this rank's slice of the n-sample rule evaluated per sample in fp64, world > 1 reduced
+    with torch.distributed. ``analytic`` (if known) sets the result's error reference.
+    """
+    from ._native import native
+
+    if rule not in ("left", "mid", "right"):
+        raise ValueError("rule must be left|mid|right")
+    m = native()
+    ctx = ctx or DistContext()
+    begin, count = decomposition.rank_slice(int(n), ctx.rank, ctx.world)
+    rl = getattr(m.Rule, rule)
+    t0 = time.perf_counter()
+    if backend == "hip":
+        value = m.ExprIntegrator(expr, ctx.device).integrate(float(a), float(b), int(n), rl,
+                                                              begin, count)
+    elif backend == "host":
+        value = m.HostExpr(expr).integrate(float(a), float(b), int(n), rl, begin, count,
+                                           m.HostPool(threads))
+    else:
+        raise ValueError("integrate_expr backend must be 'hip' or 'host'")
+    dev_s = time.perf_counter() - t0
+    if ctx.world > 1:
+        dev = "cuda" if ctx.backend == "nccl" else "cpu"
+        t = torch.tensor([value], dtype=torch.float64, device=dev)
+        ctx.all_reduce_sum(t)
+        value = float(t.item())
+    return IntegrationResult(value=value, analytic=float("nan") if analytic is None else analytic,
+                             n=int(n), integrand=f"expr:{expr}", rule=rule, dtype="fp64",
+                             gpus=ctx.world, seconds_wall=time.perf_counter() - t0,
+                             seconds_device=dev_s)

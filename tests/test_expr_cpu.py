@@ -95,3 +95,14 @@ def test_cli_and_compare_host_expr():
     rows = [json.loads(x) for x in c.stdout.splitlines()]
     host = next(r for r in rows if r.get("side") == "host")
     assert host["value"] == pytest.approx(rec["result"], rel=1e-14)
+
+
+def test_integrate_expr_host_api(native):
+    from cuda_v_mpi_amd import integrate_expr
+
+    want = math.sqrt(math.pi) / 2 * math.erf(3.0)
+    r = integrate_expr("exp(-x*x)", 0.0, 3.0, n=10**6, rule="mid", backend="host", threads=2,
+                       analytic=want)
+    assert r.abs_err < 1e-12 and r.integrand == "expr:exp(-x*x)" and r.seconds_device > 0
+    with pytest.raises(ValueError):
+        integrate_expr("x", 0, 1, backend="cpu")

@@ -102,3 +102,10 @@ def test_compare_expr_gpu_and_host(native, cuda):
     assert by["gpu"]["value"] == pytest.approx(by["host"]["value"], rel=1e-12)
     assert by["gpu"]["value"] == pytest.approx(math.sqrt(math.pi) / 2 * math.erf(3.0), rel=1e-12)
     assert rows[-1]["speedup_gpu_vs_host"] > 1.0
+
+
+def test_integrate_expr_hip_api(cuda):
+    from cuda_v_mpi_amd import integrate_expr
+
+    r = integrate_expr("4.0 / (1.0 + x * x)", 0.0, 1.0, n=10**8, rule="mid", analytic=math.pi)
+    assert r.abs_err < 1e-14

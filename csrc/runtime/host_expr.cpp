@@ -104,21 +104,26 @@ Compiled compile_host(const std::string& expr) {
                             "\"$0\" -std=c++17 -O3 -march=native -fPIC -shared -o \"$1\" \"$2\" "
                             "> \"$3\" 2>&1",
                             host_compiler(), so, src, log});
+  auto cleanup = [&] {  // the loaded object stays mapped; the files can go
+    std::remove(src.c_str());
+    std::remove(so.c_str());
+    std::remove(log.c_str());
+    ::rmdir(dir.c_str());
+  };
   if (rc != 0) {
     std::ifstream l(log);
     const std::string text((std::istreambuf_iterator<char>(l)), std::istreambuf_iterator<char>());
+    cleanup();
     fail("host expression '" + expr + "' does not compile (" + host_compiler() + "): " + text,
          __FILE__, __LINE__);
   }
   Compiled c;
   c.handle = ::dlopen(so.c_str(), RTLD_NOW | RTLD_LOCAL);
-  MIINT_CHECK(c.handle != nullptr, std::string("host expression: dlopen: ") + ::dlerror());
+  const std::string dl_err = c.handle ? "" : ::dlerror();
+  cleanup();
+  MIINT_CHECK(c.handle != nullptr, "host expression: dlopen: " + dl_err);
   c.fn = reinterpret_cast<SumFn>(::dlsym(c.handle, "miint_host_expr_sum"));
   MIINT_CHECK(c.fn != nullptr, "host expression: symbol missing");
-  std::remove(src.c_str());  // the loaded object stays mapped; the files can go
-  std::remove(so.c_str());
-  std::remove(log.c_str());
-  ::rmdir(dir.c_str());
   return cache[expr] = c;
 }
 

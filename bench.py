@@ -30,10 +30,13 @@ Weak scaling: every GPU integrates its own 1e9-sample slice of a global N = 1e9 
 global sums) are checked on the host against pi. After the timed region (outside it) the
 record also gets: the same config with IEEE division per sample ("ieee_div"), the series
 path's per-point error against IEEE division on a 64 K-sample window ("per_point_max_ulp"),
-BASELINE config #3 — N = 1e10 in total, strong-scaled over the same GPUs
-("baseline3_strong_1e10") — and BASELINE config #5 — the 4096^2 2-D velocity field with its
-rows split over the same GPUs ("baseline5_table2d_4096") — and the same integral on the
-node's host cores (the native host engine, the reference's own CPU/MPI side: "host_engine").
+and the other BASELINE configs: #1, the serial CPU sum at N = 1e6 on one host thread
+("baseline1_serial_cpu_1e6"); #3, N = 1e10 in total strong-scaled over the same GPUs
+("baseline3_strong_1e10"); #4, the same integral through the packed-fp32 path
+("baseline4_fp32", with its difference from the fp64 value); #5, the 4096^2 2-D velocity
+field with its rows split over the same GPUs ("baseline5_table2d_4096") — and the same
+integral on the node's host cores (the native host engine, the reference's own CPU/MPI side:
+"host_engine").
 """
 from __future__ import annotations
 
@@ -92,7 +95,7 @@ def parse(argv=None) -> argparse.Namespace:
     p.add_argument("--force-collective", action="store_true",
                    help="run the RCCL all-reduce stage even on 1 GPU (tests the multi-GPU graph)")
     p.add_argument("--no-extras", action="store_true",
-                   help="skip the post-timing extras (IEEE run, per-point ulp, N=1e10 strong, 2-D field, "
+                   help="skip the post-timing extras (IEEE run, per-point ulp, BASELINE #1, #3, #4, #5, "
                         "host engine)")
     p.add_argument("--sweep-gpus", default="",
                    help="e.g. 1,2,4,8: run the scaling sweep (cuda_v_mpi_amd/parallel/scaling.py) "
@@ -460,6 +463,32 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
             "rel_err_vs_oracle": abs(v - want) / want, "rows_this_rank": [p2.row0, p2.row1],
             "bucketed_allreduce": bool(p2.bucketed), "n_gpus": ctx.world}
         del p2, comm2
+    # (4b) BASELINE config #4: the same integral through the packed-fp32 path (fp64 tile
+    #      set-up and fold), its error against pi and against the fp64 headline value
+    if args.integrand == "pi4" and args.dtype == "fp64":
+        f32 = Integrator("pi4", n=n_total, div=args.div,
+                         **dict(kw, dtype="fp32"))
+        steps = 40
+        ms = _timed_steps(ctx, f32.plan, steps, pipeline, dev)
+        v = f32.plan.host_result(f32.plan.host_index_of(steps - 1, True))
+        ref = integ.plan.host_result(integ.plan.host_index_of(0, True))
+        out["baseline4_fp32"] = {"value": n_total / (ms * 1e-3), "ms_per_step": ms,
+                                 "steps": steps, "result": v, "abs_err": abs(v - math.pi),
+                                 "rel_diff_vs_fp64": abs(v - ref) / abs(ref), "dtype": "fp32"}
+        del f32
+    # (1) BASELINE config #1: the serial CPU sum at N = 1e6 (the reference's plumbing case),
+    #     on one host thread of the native host engine
+    if args.integrand == "pi4":
+        from cuda_v_mpi_amd import native as _native
+
+        mm = _native()
+        c1 = Integrator("pi4", n=10**6, rule=args.rule, backend="host", threads=1)
+        best1 = min(c1.run().seconds_device for _ in range(3))
+        v1 = c1.run().value
+        out["baseline1_serial_cpu_1e6"] = {"N": 10**6, "value": 10**6 / best1,
+                                           "ms": best1 * 1e3, "result": v1,
+                                           "abs_err": abs(v1 - math.pi), "threads": 1,
+                                           "isa": mm.host_isa()}
     # (5) the reference's own side of its CUDA-vs-MPI comparison: the same integral on this
     #     node's host cores (native host engine, per-sample fp64 vector threads, each rank
     #     its slice with its share of the cores, best of 3, slowest rank)

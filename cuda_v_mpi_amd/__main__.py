@@ -146,8 +146,6 @@ def cmd_compare(a) -> int:
                      f"runs it ({a.ranks - 1} workers on threads, scalar libm sin)", "value": v,
                      "abs_err": abs(v - 2.0), "seconds": s, "subintervals_per_s": n / s})
     if m.device_count() > 0 and a.expr:
-        from .ops import kernels
-
         ei = m.ExprIntegrator(a.expr, 0)
         rl = getattr(m.Rule, a.rule)
         v = ei.integrate(lo, hi, n, rl, 0, n)

@@ -377,7 +377,16 @@ def _timed_steps(ctx, plan, steps, pipeline, dev) -> float:
     import torch
 
     plan.prepare_steps(steps)
+    # warm + clock settle: >= 30 ms of the same replays. The replay count is agreed across
+    # ranks (MAX) — every replay holds a collective, so every rank must run the same number.
+    t_w = time.perf_counter()
     plan.launch_steps(steps, pipeline, True)
+    plan.sync()
+    per = max(time.perf_counter() - t_w, 1e-6)
+    reps = torch.tensor([math.ceil(0.03 / per)], dtype=torch.float64, device=dev)
+    ctx.all_reduce_max(reps)
+    for _ in range(int(reps.item())):
+        plan.launch_steps(steps, pipeline, True)
     plan.sync()
     ctx.barrier()
     torch.cuda.synchronize()

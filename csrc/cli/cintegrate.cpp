@@ -14,6 +14,7 @@
 //   --parity [--sp 32 --sm 2]  the reference's coverage: W=SP*SM workers of floor(1800/W) s
 //                        (121999.800663 at 32x2; the last 8 s are dropped, B5)
 //   --kernel sin         the disabled cuda_function path: sin on [0, pi], STEPS = 1e9
+//   --profile FILE       integrate a velocity profile of one's own (CSV/text, 1 s spacing)
 //   --gpus G / torchrun  split the samples across GPUs, RCCL all-reduce
 //   --device cpu [--threads T]  the same integrals on the host (miint/host.hpp): per-sample
 //                        interpolation on vector threads, host ranks under torchrun-style
@@ -37,7 +38,12 @@ int main(int argc, char** argv) {
     const bool cpu = cli::on_cpu(a);
     const cli::Topology topo = cpu ? cli::Topology{} : cli::topology(a);
     const int sps = static_cast<int>(a.integer("steps-per-sec", oracle::kStepsPerSec));
-    double seconds = oracle::kProfileSeconds;
+    // --profile FILE: a velocity profile of one's own (1 s spacing; the reference's table came
+    // from a spreadsheet CSV, ex4vel.h:1-5) instead of the built-in one
+    const std::vector<double> prof =
+        a.has("profile") ? oracle::load_profile(a.str("profile", "")) : oracle::profile_table();
+    MIINT_CHECK(!(a.has("profile") && a.flag("parity")), "--parity emulates the built-in profile");
+    double seconds = static_cast<double>(prof.size() - 1);
     if (a.flag("parity")) {
       const int w = static_cast<int>(a.integer("sp", 32) * a.integer("sm", 2));
       seconds = (oracle::kProfileSeconds / w) * w;  // cintegrate.cu:81-82 coverage
@@ -56,6 +62,7 @@ int main(int argc, char** argv) {
         cfg.n = static_cast<uint64_t>(a.num("n", 1e9));
       } else {
         cfg.integrand = Integrand::kTable;
+        cfg.table = prof;
         cfg.b = seconds;
         cfg.n = static_cast<uint64_t>(seconds) * static_cast<uint64_t>(sps);
       }
@@ -93,7 +100,7 @@ int main(int argc, char** argv) {
         const uint64_t total = static_cast<uint64_t>(seconds) * sps;
         uint64_t b, c;
         rank_slice(total, rank, topo.world, &b, &c);
-        const auto& tab = oracle::profile_table();
+        const auto& tab = prof;
         DeviceBuffer<double> dtab(tab.size()), prof(c + 2), out(1);
         const int grid = default_reduce_grid(device_info(dev).num_cus);
         DeviceBuffer<double> partials(static_cast<size_t>(grid));
@@ -124,7 +131,7 @@ int main(int argc, char** argv) {
         cfg.n = static_cast<uint64_t>(a.num("n", 1e9));  // cintegrate.cu:20 STEPS
       } else {
         cfg.integrand = Integrand::kTable;
-        cfg.table = oracle::profile_table();
+        cfg.table = prof;
         cfg.a = 0.0;
         cfg.b = seconds;
         cfg.n = static_cast<uint64_t>(seconds) * static_cast<uint64_t>(sps);

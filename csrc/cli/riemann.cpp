@@ -92,7 +92,9 @@ int run_host(const cli::Args& a, const RiemannConfig& cfg, double nd, int iters)
   if (hr.rank != 0) return 0;
   const double secs = wall_seconds() - process_start_seconds();
   print_result(secs, cfg.b, nd, result);
-  const double exact = oracle::analytic(cfg.integrand, cfg.a, cfg.b, cfg.coef, cfg.p0, cfg.p1);
+  const double exact = cfg.integrand == Integrand::kTable
+                           ? oracle::table_integral(cfg.table, cfg.a, cfg.b)
+                           : oracle::analytic(cfg.integrand, cfg.a, cfg.b, cfg.coef, cfg.p0, cfg.p1);
   cli::emit(a, cli::JsonRecord()
                    .add("program", "riemann")
                    .add("device", "cpu")
@@ -198,7 +200,11 @@ int main(int argc, char** argv) {
     const double pi = 3.14159265358979323846;
     double lo = 0.0, hi = pi;  // riemann.cpp:6 RANGE = M_PI
     if (f == Integrand::kPi4) hi = 1.0;
-    if (f == Integrand::kTrainVel || f == Integrand::kTable) hi = 1800.0;
+    std::vector<double> prof;  // table integrand: --profile FILE or the built-in profile
+    if (f == Integrand::kTable)
+      prof = a.has("profile") ? oracle::load_profile(a.str("profile", "")) : oracle::profile_table();
+    if (f == Integrand::kTrainVel) hi = 1800.0;
+    if (f == Integrand::kTable) hi = static_cast<double>(prof.size() - 1);
     lo = a.num("a", lo);
     hi = a.num("b", hi);
     const double nd = a.num("n", 1e9);  // riemann.cpp:10 STEPS
@@ -216,7 +222,7 @@ int main(int argc, char** argv) {
     cfg.div = a.str("div", "series") == "ieee" ? DivMode::kIeee : DivMode::kSeries;
     cfg.fused = !a.flag("unfused");
     if (f == Integrand::kTrainVel) { cfg.p0 = oracle::kTrainTs; cfg.p1 = oracle::kTrainVs; }
-    if (f == Integrand::kTable) cfg.table = oracle::profile_table();
+    if (f == Integrand::kTable) cfg.table = prof;
     if (f == Integrand::kPoly) cfg.coef = {1.0, -0.5, 0.25, 0.125};
 
     if (a.has("expr")) return run_expr(a, cfg, nd, iters);
@@ -255,7 +261,8 @@ int main(int argc, char** argv) {
     if (topo.rank0 != 0) return 0;
     const double secs = wall_seconds() - process_start_seconds();
     print_result(secs, hi, nd, result);
-    const double exact = oracle::analytic(f, lo, hi, cfg.coef, cfg.p0, cfg.p1);
+    const double exact = f == Integrand::kTable ? oracle::table_integral(prof, lo, hi)
+                                                : oracle::analytic(f, lo, hi, cfg.coef, cfg.p0, cfg.p1);
     cli::emit(a, cli::JsonRecord()
                      .add("program", "riemann")
                      .add("integrand", a.str("integrand", "sin"))

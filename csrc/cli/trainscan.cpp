@@ -20,7 +20,7 @@
 //
 //   ./trainscan [--gpus G] [--parity] [--replicate] [--no-phase2] [--algo onepass|fused|lookback]
 //               [--steps-per-sec S] [--iters K] [--json] [--jsonl FILE]
-//               [--device cpu [--threads T] [--ranks P] [--no-keep]]
+//               [--device cpu [--threads T] [--ranks P] [--no-keep]] [--profile FILE]
 #include <cstdio>
 
 #include "cli_common.hpp"
@@ -37,11 +37,16 @@ int run_host(const cli::Args& a) {
   HostPool pool(hr.threads);
   HostScanConfig c;
   c.steps_per_sec = static_cast<int>(a.integer("steps-per-sec", oracle::kStepsPerSec));
+  if (a.has("profile")) {
+    c.table = oracle::load_profile(a.str("profile", ""));
+    c.seconds = static_cast<int>(c.table.size() - 1);
+  }
   c.keep = !a.flag("no-keep");
   const int iters = static_cast<int>(a.integer("iters", 1));
   if (hr.rank == 0) std::printf("Step size of %ld\n", static_cast<long>(c.steps_per_sec));
   double distance = 0.0, sos = 0.0, best = 0.0;
   int ranks = hr.world;
+  MIINT_CHECK(!(a.has("profile") && a.flag("parity")), "--parity emulates the built-in profile");
   if (a.flag("parity")) {  // 4main.c's partitions and sequential sums for --ranks P
     MIINT_CHECK(hr.world == 1 && c.steps_per_sec == oracle::kStepsPerSec,
                 "--device cpu --parity emulates --ranks P of 4main.c in one process");
@@ -90,7 +95,12 @@ int main(int argc, char** argv) {
     const cli::Topology topo = cli::topology(a);
     TrainScanConfig cfg;
     cfg.steps_per_sec = static_cast<int>(a.integer("steps-per-sec", oracle::kStepsPerSec));
+    if (a.has("profile")) {  // a velocity profile of one's own (CSV/text, 1 s spacing)
+      cfg.table = oracle::load_profile(a.str("profile", ""));
+      cfg.seconds = static_cast<int>(cfg.table.size() - 1);
+    }
     cfg.parity = a.flag("parity");
+    MIINT_CHECK(!(a.has("profile") && cfg.parity), "--parity emulates the built-in profile");
     cfg.replicate = a.flag("replicate");
     cfg.phase2 = !a.flag("no-phase2");
     const std::string algo = a.str("algo", "fused");

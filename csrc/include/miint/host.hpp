@@ -128,6 +128,7 @@ struct HostScanConfig {
   int steps_per_sec = 10000;  // 4main.c:26
   int seconds = 1800;         // 4main.c:27
   bool keep = false;          // keep vel / pos (else only the totals are formed)
+  std::vector<double> table;  // velocity table at 1 s spacing (empty: the built-in profile)
 };
 struct HostScanResult {
   double distance = 0.0;     // vel[T-1] / steps_per_sec (the complete running integral)

@@ -34,6 +34,13 @@ const std::vector<double>& profile_table();
 // Within 1.1e-13 of profile_table(); kept as an independent check of the data.
 const std::vector<double>& generated_profile_table();
 
+// A velocity profile from a text/CSV file (the reference's table was "Auto-generated from
+// Excel CSV", ex4vel.h:1-5): numbers separated by commas, whitespace or newlines, one sample
+// per second; '#' starts a comment line. At least 2 finite values, else an error.
+std::vector<double> load_profile(const std::string& path);
+// Exact integral over [a, b] (inside [0, len - 1]) of the table's piecewise-linear
+// interpolant at unit spacing.
+double table_integral(const std::vector<double>& table, double a, double b);
 // Linear interpolation of a 1-s-spaced table at t, segment index clamped to the table.
 double interp(const std::vector<double>& table, double t);
 

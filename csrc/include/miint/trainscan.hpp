@@ -44,6 +44,9 @@ struct TrainScanConfig {
   bool replicate = false;     // allgather full tables to every rank (4main.c:157)
   bool phase2 = true;         // second integral (4main.c:178-221)
   ScanAlgo algo = ScanAlgo::kFused;
+  // velocity table at 1 s spacing (empty: the built-in ex4vel.h profile); `seconds` must not
+  // exceed its length - 1 (a user profile: --profile FILE, oracle::load_profile)
+  std::vector<double> table;
 };
 
 struct TrainScanResult {
@@ -116,6 +119,7 @@ class TrainScan {
   int device_;
   const Comm* comm_;
   int rank_ = 0, world_ = 1;
+  int tn_ = 0;  // table entries
   uint64_t total_ = 0, begin_ = 0, count_ = 0;
   uint64_t win_lo_ = 0, win_hi_ = ~uint64_t(0);
   Stream stream_;

@@ -373,6 +373,7 @@ PYBIND11_MODULE(_miint, m) {
       .def_readwrite("parity", &TrainScanConfig::parity)
       .def_readwrite("replicate", &TrainScanConfig::replicate)
       .def_readwrite("phase2", &TrainScanConfig::phase2)
+      .def_readwrite("table", &TrainScanConfig::table)
       .def_property("algo", [](const TrainScanConfig& c) { return scan_algo_name(c.algo); },
                     [](TrainScanConfig& c, const std::string& s) {
                       c.algo = scan_algo_of(s);
@@ -512,11 +513,13 @@ PYBIND11_MODULE(_miint, m) {
              return v;
            })
       .def("barrier", &HostComm::barrier, py::call_guard<py::gil_scoped_release>());
-  m.def("host_trainscan", [](int sps, int seconds, HostPool& pool, HostComm* comm, bool keep) {
+  m.def("host_trainscan", [](int sps, int seconds, HostPool& pool, HostComm* comm, bool keep,
+                             std::vector<double> table) {
           HostScanConfig c;
           c.steps_per_sec = sps;
           c.seconds = seconds;
           c.keep = keep;
+          c.table = std::move(table);
           std::vector<double> vel, pos;
           HostScanResult r;
           {
@@ -536,7 +539,8 @@ PYBIND11_MODULE(_miint, m) {
           return d;
         },
         py::arg("steps_per_sec") = 10000, py::arg("seconds") = 1800, py::arg("pool"),
-        py::arg("comm") = nullptr, py::arg("keep") = false);
+        py::arg("comm") = nullptr, py::arg("keep") = false,
+        py::arg("table") = std::vector<double>{});
 
   // ------------------------------------------------------------------ oracle
   py::module_ o = m.def_submodule("oracle", "host oracles, generated fixtures, parity emulation");
@@ -545,6 +549,10 @@ PYBIND11_MODULE(_miint, m) {
   o.def("faccel_ref", [](double t) { return oracle::faccel_ref(oracle::profile_table(), t); });
   o.def("interp", [](double t) { return oracle::interp(oracle::profile_table(), t); });
   o.def("profile_exact_integral", &oracle::profile_exact_integral);
+  o.def("load_profile", &oracle::load_profile, py::arg("path"),
+        "a velocity profile (CSV/text numbers, 1 s spacing)");
+  o.def("table_integral", &oracle::table_integral, py::arg("table"), py::arg("a"), py::arg("b"),
+        "exact integral of the table's piecewise-linear interpolant over [a, b]");
   o.def("analytic", &oracle::analytic, py::arg("integrand"), py::arg("a"), py::arg("b"),
         py::arg("coef") = std::vector<double>{}, py::arg("p0") = 0.0, py::arg("p1") = 0.0);
   o.def("riemann_serial", [](Integrand f, double a, double b, uint64_t n, Rule r,

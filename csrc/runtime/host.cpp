@@ -241,7 +241,9 @@ HostScanResult host_trainscan(const HostScanConfig& cfg, HostPool& pool, HostCom
   HostScanResult r;
   rank_slice(total, rank, world, &r.begin, &r.count);
   MIINT_CHECK(r.count >= 1, "empty train-scan slice");
-  const auto& tab = oracle::profile_table();
+  const std::vector<double>& tab = cfg.table.empty() ? oracle::profile_table() : cfg.table;
+  MIINT_CHECK(tab.size() >= 2 && static_cast<size_t>(cfg.seconds) <= tab.size() - 1,
+              "train scan: seconds exceeds the table");
   HostArgs p{};
   p.integrand = static_cast<int>(Integrand::kTable);
   p.tab = tab.data();

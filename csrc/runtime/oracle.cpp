@@ -4,6 +4,9 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <fstream>
+#include <sstream>
+#include <string>
 
 namespace miint {
 namespace oracle {
@@ -60,6 +63,47 @@ const std::vector<double>& generated_profile_table() {
   return t;
 }
 
+std::vector<double> load_profile(const std::string& path) {
+  std::ifstream in(path);
+  MIINT_CHECK(in.good(), "cannot read profile " + path);
+  std::vector<double> v;
+  std::string line;
+  int lineno = 0;
+  while (std::getline(in, line)) {
+    ++lineno;
+    const size_t first = line.find_first_not_of(" \t\r");
+    if (first == std::string::npos || line[first] == '#') continue;
+    for (char& c : line)
+      if (c == ',' || c == ';' || c == '\t' || c == '\r') c = ' ';
+    std::istringstream ls(line);
+    std::string tok;
+    while (ls >> tok) {
+      char* end = nullptr;
+      const double x = std::strtod(tok.c_str(), &end);
+      MIINT_CHECK(end && *end == '\0' && std::isfinite(x),
+                  path + ":" + std::to_string(lineno) + ": not a finite number: '" + tok + "'");
+      v.push_back(x);
+    }
+  }
+  MIINT_CHECK(v.size() >= 2, path + ": a profile needs at least 2 samples");
+  return v;
+}
+
+double table_integral(const std::vector<double>& v, double a, double b) {
+  const int len = static_cast<int>(v.size());
+  auto prim = [&](double t) {  // integral of the interpolant from 0 to t (t within the table)
+    long double s = 0.0L;
+    int i = 0;
+    for (; i + 1 < len && i + 1 <= t; ++i) s += 0.5L * ((long double)v[i] + v[i + 1]);
+    if (i + 1 < len && t > i) {
+      const double fr = t - i;
+      s += fr * v[i] + 0.5L * fr * fr * (v[i + 1] - v[i]);
+    }
+    return s;
+  };
+  return static_cast<double>(prim(b) - prim(a));
+}
+
 double interp(const std::vector<double>& table, double t) {
   const int nseg = static_cast<int>(table.size()) - 1;
   int i = static_cast<int>(t);
@@ -96,21 +140,8 @@ double analytic(Integrand f, double a, double b, const std::vector<double>& coef
       const double ts = p0, vs = p1;
       return vs * ((b - ts * std::sin(b / ts)) - (a - ts * std::sin(a / ts)));
     }
-    case Integrand::kTable: {
-      // exact integral of the linear interpolant of the generated profile over [a, b]
-      const auto& v = profile_table();
-      auto prim = [&](double t) {  // integral from 0 to t
-        long double s = 0.0L;
-        int i = 0;
-        for (; i + 1 < kProfileLen && i + 1 <= t; ++i) s += 0.5L * ((long double)v[i] + v[i + 1]);
-        if (i + 1 < kProfileLen && t > i) {
-          const double fr = t - i;
-          s += fr * v[i] + 0.5L * fr * fr * (v[i + 1] - v[i]);
-        }
-        return s;
-      };
-      return static_cast<double>(prim(b) - prim(a));
-    }
+    case Integrand::kTable:
+      return table_integral(profile_table(), a, b);
   }
   return 0.0;
 }

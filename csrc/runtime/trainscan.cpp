@@ -42,7 +42,11 @@ TrainScan::TrainScan(const TrainScanConfig& cfg, int device, const Comm* comm)
     rank_slice(total_, rank_, world_, &begin_, &count_);
   }
   MIINT_CHECK(count_ >= 1, "empty slice");
-  const auto& tab = oracle::profile_table();
+  const std::vector<double>& tab = cfg.table.empty() ? oracle::profile_table() : cfg.table;
+  MIINT_CHECK(tab.size() >= 2 && tab.size() <= 2048, "train table needs 2..2048 entries");
+  MIINT_CHECK(static_cast<size_t>(cfg.seconds) <= tab.size() - 1,
+              "trainscan: seconds exceeds the table (" + std::to_string(tab.size() - 1) + " s)");
+  tn_ = static_cast<int>(tab.size());
   table_ = DeviceBuffer<double>(tab.size());
   MIINT_HIP(hipMemcpy(table_.get(), tab.data(), table_.bytes(), hipMemcpyHostToDevice));
   vel_ = DeviceBuffer<double>(count_);
@@ -96,7 +100,7 @@ double TrainScan::pick_global(const double* slice, uint64_t gi, hipStream_t s) {
 // the already-carried last element of block q-1, one fp64 add per element) is replayed in
 // rank order: G_0 = last_0, G_q = last_q + G_{q-1}, element = at_q + G_{q-1}.
 double TrainScan::parity_serial_element(uint64_t gi, hipStream_t s) {
-  TrainScanKernelParams p{table_.get(), static_cast<int>(oracle::profile_table().size()),
+  TrainScanKernelParams p{table_.get(), tn_,
                           1.0 / cfg_.steps_per_sec, begin_, count_, win_lo_, win_hi_};
   double* sc = scratch_.get();
   launch_trainscan_parity_serial(p, gi, sc + kParity, s);
@@ -118,7 +122,7 @@ double TrainScan::parity_serial_element(uint64_t gi, hipStream_t s) {
 }
 
 void TrainScan::enqueue_fused(hipStream_t s) {
-  TrainScanKernelParams p{table_.get(), static_cast<int>(oracle::profile_table().size()),
+  TrainScanKernelParams p{table_.get(), tn_,
                           1.0 / cfg_.steps_per_sec, begin_, count_, win_lo_, win_hi_};
   double* sc = scratch_.get();
   const bool fold = !(comm_ && world_ > 1);  // one GPU: no totals needed, no carries
@@ -135,14 +139,14 @@ void TrainScan::enqueue_fused(hipStream_t s) {
 }
 
 void TrainScan::enqueue_onepass(hipStream_t s) {
-  TrainScanKernelParams p{table_.get(), static_cast<int>(oracle::profile_table().size()),
+  TrainScanKernelParams p{table_.get(), tn_,
                           1.0 / cfg_.steps_per_sec, begin_, count_, win_lo_, win_hi_};
   launch_trainscan_onepass(p, state_.get(), vel_.get(), pos_.get(), scratch_.get() + kTotals, s);
 }
 
 void TrainScan::enqueue_lookback(hipStream_t s) {
   const double dt = 1.0 / cfg_.steps_per_sec;
-  const int tn = static_cast<int>(oracle::profile_table().size());
+  const int tn = tn_;
   // Phase 1: velocity samples -> running integral (4main.c:95-160)
   launch_interp_scan_window(table_.get(), tn, dt, begin_, count_, win_lo_, win_hi_, vel_.get(),
                             state_.get(), nullptr, s);

@@ -138,6 +138,22 @@ struct Pi4 : TileDefaults<Pi4> {
 
   __device__ __forceinline__ double point(double x) const { return 1.0 / fma(x, x, 1.0); }
 
+  // 1/d for 1 <= d <= 2^500, bitwise equal to IEEE division (the kIeee tiles). This is the
+  // sequence hipcc -O3 emits for 1.0 / d on gfx950 —
+  //   v_div_scale x2, v_rcp_f64, two Newton steps, q = 1 * r, rem = 1 - d q,
+  //   v_div_fmas(rem, r, q), v_div_fixup
+  // — without its range handling: for such d, v_div_scale returns its operands unscaled (no
+  // denormal operand or quotient, exponent gap far below 768), so v_div_fmas is a plain fma,
+  // and v_div_fixup returns the finite normal quotient unchanged. Every intermediate, and
+  // the result, is therefore the library division's: 7 VALU (one v_rcp_f64) instead of 10.
+  // The dispatcher runs Pi4Wide (the full division) when |x| can reach 2^249.
+  __device__ __forceinline__ static double recip_narrow(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    r = fma(r, fma(-d, r, 1.0), r);
+    r = fma(r, fma(-d, r, 1.0), r);
+    return fma(fma(-d, r, 1.0), r, r);
+  }
+
   // Per-tile seed for kSeriesDirect (also the reciprocal seed of kSeries).
   struct Seed {
     double s, em, a, b;
@@ -186,7 +202,7 @@ struct Pi4 : TileDefaults<Pi4> {
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const double x = fma(static_cast<double>(u), h, x0);
-        acc += 1.0 / fma(x, x, 1.0);
+        acc += recip_narrow(fma(x, x, 1.0));
       }
       return acc;
     } else {
@@ -261,6 +277,24 @@ struct Pi4 : TileDefaults<Pi4> {
     return sd.s * fma(g, g, 0.75);
   }
 };
+
+// 4/(1+x^2) by the library's full IEEE division, for kIeee launches whose coordinates can
+// reach |x| >= 2^249 (1 + x^2 beyond Pi4::recip_narrow's range: the quotient nears the
+// denormals, 1 + x^2 may overflow). The dispatcher picks it from the launch's end points.
+struct Pi4Wide : TileDefaults<Pi4Wide> {
+  static constexpr double kScale = 4.0;
+  __device__ __forceinline__ double point(double x) const { return 1.0 / fma(x, x, 1.0); }
+  template <int U, DivMode M>
+  __device__ __forceinline__ double tile(double x0, double h) const {
+    static_assert(M == DivMode::kIeee, "wide-domain Pi4 runs IEEE division only");
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += point(fma(static_cast<double>(u), h, x0));
+    return acc;
+  }
+};
+// Largest |x| for which every 1 + x^2 stays inside Pi4::recip_narrow's range.
+constexpr double kPi4NarrowMaxX = 0x1p249;
 
 // ------------------------------------------------------------------ tile seed: sin and cos
 // sin and cos of a tile midpoint angle (|theta| up to ~1e5; the integrands use [0, 2 pi]):

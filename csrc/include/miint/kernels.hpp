@@ -119,6 +119,13 @@ void launch_riemann_chained(const RiemannParams& p, DType dtype, DivMode div, La
 void launch_riemann_point_values(const RiemannParams& p, DivMode div, const double* table,
                                  int table_n, double* out, hipStream_t stream);
 
+// Validation: out[i] = the kIeee Pi4 tiles' reciprocal of d[i] (Pi4::recip_narrow; equal to
+// IEEE 1.0 / d[i] for 1 <= d[i] <= 2^500).
+void launch_pi4_recip_narrow(const double* d, uint64_t n, double* out, hipStream_t stream);
+// Validation: when on, kIeee Pi4 launches run the library division everywhere (Pi4Wide), so
+// tests can check that the two give bitwise the same sums.
+void set_pi4_library_division(bool on);
+
 // Samples per lane tile of the kernel that launch_riemann_* would run for these arguments
 // (32; 64 or 128 on the series paths): host-side grid sizing.
 int riemann_tile_len(const RiemannParams& p, DType dtype, DivMode div);

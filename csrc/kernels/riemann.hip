@@ -19,6 +19,7 @@
 //   * fp32 path: packed float2 math (v_pk_fma_f32), tile coordinates from an fp64 base.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cmath>
 
 #include "miint/common.hpp"
@@ -212,6 +213,10 @@ template <> struct Maker<Pi4> {
     return f;
   }
 };
+template <> struct Maker<Pi4Wide> {
+  static constexpr int kLds = 1;
+  __device__ static Pi4Wide make(const RiemannParams&, const double*, int, double*) { return {}; }
+};
 template <> struct Maker<Pi4F32> {
   static constexpr int kLds = 1;
   __device__ static Pi4F32 make(const RiemannParams&, const double*, int, double*) { return {}; }
@@ -311,6 +316,8 @@ __device__ __forceinline__ F make_functor(const RiemannParams& p, const double* 
     F f = Maker<F>::make(p, table, n, lds);
     f.init_series(p.coef_h, p.ncoef, p.h);
     return f;
+  } else if constexpr (__is_same(F, Pi4) && M != DivMode::kSeries) {
+    return Pi4{};  // the register-pinned pair tables (Pi4::init) serve only kSeries
   } else if constexpr (__is_same(F, Table) && M == DivMode::kSeries) {
     Table f{{}, table, n - 1};
     f.init();
@@ -489,11 +496,22 @@ __global__ __launch_bounds__(B) void point_values_kernel(RiemannParams p, const 
       const Pi4::Seed sd = Pi4::seed(xm, p.h);
       const double e = fma(-fma(x, x, 1.0), sd.s, 1.0);
       v = fma(sd.s, e + e * e, sd.s);
+    } else if constexpr (M == DivMode::kIeee && __is_same(F, Pi4)) {
+      v = full ? Pi4::recip_narrow(fma(x, x, 1.0)) : f.point(x);  // as Pi4::tile<U, kIeee>
     } else {
       v = f.point(x);
     }
     out[t * T + u] = v * F::kScale;
   }
+}
+
+// Validation: Pi4::recip_narrow of arbitrary operands (tests compare it bit for bit with
+// IEEE division).
+__global__ __launch_bounds__(B) void recip_narrow_kernel(const double* d, uint64_t n,
+                                                         double* out) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * B;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * B + threadIdx.x; i < n; i += stride)
+    out[i] = Pi4::recip_narrow(d[i]);
 }
 
 template <DivMode M, class F>
@@ -526,6 +544,17 @@ void launch_chained_t(const RiemannParams& p, LaunchShape shape, const double* t
   else
     riemann_chained_kernel<M, F><<<shape.grid, B, 0, stream>>>(p, table, table_n, partials,
                                                                prev, nprev, scale, out_prev);
+}
+
+// kIeee Pi4 launches take Pi4::recip_narrow when both end coordinates (the extremes: x is
+// linear in the sample index) stay below kPi4NarrowMaxX in magnitude; NaN ends do not.
+std::atomic<bool> g_pi4_library_division{false};  // validation switch: always Pi4Wide
+inline bool pi4_narrow(const RiemannParams& p) {
+  if (g_pi4_library_division.load(std::memory_order_relaxed)) return false;
+  const double first = static_cast<double>(p.i_begin) + p.off;
+  const double last = static_cast<double>(p.i_begin + (p.n > 0 ? p.n - 1 : 0)) + p.off;
+  return std::fabs(std::fma(first, p.h, p.a)) < kPi4NarrowMaxX &&
+         std::fabs(std::fma(last, p.h, p.a)) < kPi4NarrowMaxX;
 }
 
 // Dispatch (integrand, dtype, division mode) to a template instantiation. Transcendental
@@ -568,7 +597,8 @@ void dispatch(const RiemannParams& p, DType dtype, DivMode m, A&&... a) {
     case Integrand::kPi4:
       if (m == DivMode::kSeries) Op<DivMode::kSeries, Pi4>::run(a...);
       else if (m == DivMode::kSeriesDirect) Op<DivMode::kSeriesDirect, Pi4>::run(a...);
-      else Op<DivMode::kIeee, Pi4>::run(a...);
+      else if (pi4_narrow(p)) Op<DivMode::kIeee, Pi4>::run(a...);
+      else Op<DivMode::kIeee, Pi4Wide>::run(a...);
       return;
     case Integrand::kSin:
       if (m == DivMode::kSeries) Op<DivMode::kSeries, Sin>::run(a...);
@@ -740,6 +770,16 @@ void launch_riemann_point_values(const RiemannParams& p, DivMode div, const doub
   MIINT_CHECK(p.n >= 1, "empty range");
   const DivMode eff = effective_div(p, div, DType::kF64);
   dispatch<PointsOp>(p, DType::kF64, eff, prepared(p, eff), table, table_n, out, stream);
+  MIINT_HIP(hipGetLastError());
+}
+
+void set_pi4_library_division(bool on) { g_pi4_library_division.store(on); }
+
+void launch_pi4_recip_narrow(const double* d, uint64_t n, double* out, hipStream_t stream) {
+  if (n == 0) return;
+  const uint64_t blocks = (n + B - 1) / B;
+  const int grid = static_cast<int>(blocks < 8192 ? blocks : 8192);
+  recip_narrow_kernel<<<grid, B, 0, stream>>>(d, n, out);
   MIINT_HIP(hipGetLastError());
 }
 

@@ -295,6 +295,11 @@ PYBIND11_MODULE(_miint, m) {
           launch_riemann_point_values(p, div, ptr<const double>(table), table_n, ptr<double>(out),
                                       stream(s));
         });
+  m.def("launch_pi4_recip_narrow", [](uintptr_t d, uint64_t n, uintptr_t out, uintptr_t s) {
+    launch_pi4_recip_narrow(ptr<const double>(d), n, ptr<double>(out), stream(s));
+  });
+  m.def("set_pi4_library_division", &set_pi4_library_division,
+        "validation: kIeee Pi4 launches use the full library division (bitwise the same sums)");
   m.def("launch_finalize", [](uintptr_t partials, int n, double scale, uintptr_t out, uintptr_t s) {
     launch_finalize(ptr<const double>(partials), n, scale, ptr<double>(out), stream(s));
   });

@@ -152,6 +152,15 @@ def point_values(spec: IntegrandSpec, n: int, rule: str = "left", div: str = "se
     return out
 
 
+def pi4_recip_narrow(d: torch.Tensor) -> torch.Tensor:
+    """The IEEE-division kIeee Pi4 tiles' reciprocal of every element of ``d`` (validation:
+    bitwise 1 / d for 1 <= d <= 2**500)."""
+    _check(d, name="d")
+    out = torch.empty_like(d)
+    native().launch_pi4_recip_narrow(d.data_ptr(), d.numel(), out.data_ptr(), _stream())
+    return out
+
+
 def sum_array(x: torch.Tensor, scale: float = 1.0) -> torch.Tensor:
     _check(x, name="x")
     m = native()

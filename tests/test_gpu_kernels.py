@@ -537,3 +537,63 @@ def test_table2d_row_split(cuda):
     parts = [float(kernels.table2d(T, 1800.0, 1800.0, g, g, r0, r1).item())
              for r0, r1 in [(0, 333), (333, 700), (700, 1000)]]
     assert math.fsum(parts) == pytest.approx(whole, rel=1e-13)
+
+
+# ---------------------------------------------------------------- kIeee Pi4 reciprocal
+def _recip_operands() -> torch.Tensor:
+    """Divisors for the narrow-range reciprocal: uniform [1, 2); random significands at every
+    exponent 0..499; the integrand's own 1 + x^2 at both ends of a 1e9-sample [0, 1] grid; and
+    the first / last 4096 significands (1 + k ulp, 2 - k ulp) at exponents 0, 1, 10, 100, 499."""
+    g = torch.Generator().manual_seed(7)
+    m = 1 << 21
+    uni = 1.0 + torch.rand(m, generator=g, dtype=torch.float64)
+    exps = torch.randint(0, 500, (m,), generator=g)
+    wide = torch.ldexp(1.0 + torch.rand(m, generator=g, dtype=torch.float64), exps)
+    i = torch.arange(1 << 20, dtype=torch.float64)
+    x = torch.cat([i * 1e-9, 1.0 - i * 1e-9])
+    grid = 1.0 + x * x
+    k = torch.arange(4096, dtype=torch.float64)
+    sig = torch.cat([1.0 + k * 2.0**-52, 2.0 - (k + 1) * 2.0**-52])
+    edges = torch.cat([torch.ldexp(sig, torch.full_like(sig, s, dtype=torch.int64))
+                       for s in (0, 1, 10, 100, 499)] +
+                      [torch.tensor([2.0**500], dtype=torch.float64)])
+    return torch.cat([uni, wide, grid, edges])
+
+
+def test_pi4_recip_narrow_bitwise_ieee(cuda):
+    """The kIeee Pi4 tiles' reciprocal (the library division sequence without its range
+    handling, integrands.hpp Pi4::recip_narrow) is bitwise IEEE 1/d on [1, 2^500]."""
+    d = _recip_operands()
+    got = kernels.pi4_recip_narrow(d.to(cuda)).cpu()
+    want = 1.0 / d  # host IEEE division (correctly rounded)
+    bad = (got.view(torch.int64) != want.view(torch.int64)).nonzero().flatten()
+    assert bad.numel() == 0, f"{bad.numel()} of {d.numel()} differ, first d = {d[bad[:4]].tolist()}"
+
+
+@pytest.mark.parametrize("n,rule", [(1_000_003, "mid"), (48_000_001, "left"), (10**8 + 17, "right")])
+def test_pi4_ieee_tiles_equal_library_division(native, cuda, n, rule):
+    """Riemann sums and per-point values of the kIeee Pi4 path are bitwise those of the full
+    library division (Pi4Wide, forced by the validation switch)."""
+    spec = integrands.pi4()
+    fast = float(kernels.riemann(spec, n, rule=rule, div="ieee").item())
+    i0 = n // 3 + 5
+    pv_fast = kernels.point_values(spec, n, rule=rule, div="ieee", i_begin=i0, n_local=1 << 16)
+    native.set_pi4_library_division(True)
+    try:
+        lib = float(kernels.riemann(spec, n, rule=rule, div="ieee").item())
+        pv_lib = kernels.point_values(spec, n, rule=rule, div="ieee", i_begin=i0, n_local=1 << 16)
+    finally:
+        native.set_pi4_library_division(False)
+    assert fast == lib
+    assert torch.equal(pv_fast.view(torch.int64), pv_lib.view(torch.int64))
+
+
+def test_pi4_ieee_wide_domain(cuda):
+    """Coordinates beyond 2^249 run the library division: finite sums where 1 + x^2 is large,
+    and exact zeros (not NaN) where it overflows."""
+    spec = integrands.IntegrandSpec("pi4", 1e150, 2e150)
+    got = float(kernels.riemann(spec, 1_000_003, rule="mid", div="ieee").item())
+    assert got == pytest.approx(_ref_sum(spec, 1_000_003, rule="mid"), rel=1e-12)
+    assert got == pytest.approx(spec.analytic(), rel=1e-9)
+    over = integrands.IntegrandSpec("pi4", 1e160, 2e160)
+    assert float(kernels.riemann(over, 4097, rule="mid", div="ieee").item()) == 0.0

@@ -51,26 +51,43 @@ HostComm::HostComm(const std::string& addr, int port, int rank, int world, doubl
       fail("host comm: bind failed on port " + std::to_string(port), __FILE__, __LINE__);
     }
     ::listen(srv, world);
-    for (int got = 1; got < world; ++got) {
-      pollfd pf{srv, POLLIN, 0};
-      const double left = timeout_s - (wall_seconds() - t0);
-      if (left <= 0 || ::poll(&pf, 1, static_cast<int>(left * 1e3) + 1) <= 0) {
-        ::close(srv);
-        fail("host comm: " + std::to_string(got - 1) + " of " + std::to_string(world - 1) +
-                 " ranks connected before the timeout",
-             __FILE__, __LINE__);
+    // any failure below closes the listener and every accepted peer before it propagates
+    // (a constructor that throws runs no destructor)
+    auto drop_all = [&] {
+      ::close(srv);
+      for (int& fd : peers_) {
+        if (fd >= 0) ::close(fd);
+        fd = -1;
       }
-      const int c = ::accept(srv, nullptr, nullptr);
-      MIINT_CHECK(c >= 0, "host comm: accept()");
-      no_delay(c);
-      int32_t who = -1;
-      recv_from(c, &who, sizeof(who));
-      if (who < 1 || who >= world || peers_[who] >= 0) {
-        ::close(c);
-        ::close(srv);
-        fail("host comm: bad or duplicate rank " + std::to_string(who), __FILE__, __LINE__);
+    };
+    try {
+      for (int got = 1; got < world; ++got) {
+        pollfd pf{srv, POLLIN, 0};
+        const double left = timeout_s - (wall_seconds() - t0);
+        if (left <= 0 || ::poll(&pf, 1, static_cast<int>(left * 1e3) + 1) <= 0) {
+          fail("host comm: " + std::to_string(got - 1) + " of " + std::to_string(world - 1) +
+                   " ranks connected before the timeout",
+               __FILE__, __LINE__);
+        }
+        const int c = ::accept(srv, nullptr, nullptr);
+        MIINT_CHECK(c >= 0, "host comm: accept()");
+        no_delay(c);
+        int32_t who = -1;
+        try {
+          recv_from(c, &who, sizeof(who));
+        } catch (...) {
+          ::close(c);
+          throw;
+        }
+        if (who < 1 || who >= world || peers_[who] >= 0) {
+          ::close(c);
+          fail("host comm: bad or duplicate rank " + std::to_string(who), __FILE__, __LINE__);
+        }
+        peers_[who] = c;
       }
-      peers_[who] = c;
+    } catch (...) {
+      drop_all();
+      throw;
     }
     ::close(srv);
     return;
@@ -97,7 +114,12 @@ HostComm::HostComm(const std::string& addr, int port, int rank, int world, doubl
   }
   ::freeaddrinfo(res);
   const int32_t me = rank;
-  send_to(peers_[0], &me, sizeof(me));
+  try {
+    send_to(peers_[0], &me, sizeof(me));
+  } catch (...) {
+    ::close(peers_[0]);
+    throw;
+  }
 }
 
 HostComm::~HostComm() {

@@ -122,8 +122,10 @@ void launch_riemann_point_values(const RiemannParams& p, DivMode div, const doub
 // Validation: out[i] = the kIeee Pi4 tiles' reciprocal of d[i] (Pi4::recip_narrow; equal to
 // IEEE 1.0 / d[i] for 1 <= d[i] <= 2^500).
 void launch_pi4_recip_narrow(const double* d, uint64_t n, double* out, hipStream_t stream);
-// Validation: when on, kIeee Pi4 launches run the library division everywhere (Pi4Wide), so
-// tests can check that the two give bitwise the same sums.
+// The same for the fp32 kIeee tiles (Pi4F32::recip_narrow; IEEE 1.0f / d for 1 <= d <= 2^100).
+void launch_pi4_recip_narrow_f32(const float* d, uint64_t n, float* out, hipStream_t stream);
+// Validation: when on, kIeee Pi4 launches run the library division everywhere (Pi4Wide,
+// Pi4F32Wide), so tests can check that the two give bitwise the same sums.
 void set_pi4_library_division(bool on);
 
 // Samples per lane tile of the kernel that launch_riemann_* would run for these arguments

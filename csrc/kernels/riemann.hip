@@ -85,6 +85,20 @@ struct Pi4F32 : TileDefaults<Pi4F32> {
     const float x = static_cast<float>(xd);
     return static_cast<double>(1.0f / fmaf(x, x, 1.0f));
   }
+  // 1/d for 1 <= d <= 2^100, bitwise IEEE fp32 division, two samples at once: the fp32
+  // sequence hipcc emits for 1.0f / d (v_div_scale x2, v_rcp_f32, one Newton step, q = 1 * r,
+  // two residual corrections, v_div_fmas, v_div_fixup) without the range handling, which is
+  // the identity there (as Pi4::recip_narrow); the fmas run packed. 2 v_rcp_f32 + 6
+  // v_pk_fma_f32 per pair against ~11 VALU per sample. Pi4F32Wide runs the full division
+  // when |x| can reach 2^49.
+  __device__ __forceinline__ static f32x2 recip_narrow(f32x2 d) {
+    const f32x2 one = {1.0f, 1.0f};
+    const f32x2 nd = -d;
+    f32x2 r = {__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+    r = pk_fma(pk_fma(nd, r, one), r, r);
+    const f32x2 q = pk_fma(pk_fma(nd, r, one), r, r);
+    return pk_fma(pk_fma(nd, q, one), r, q);
+  }
   template <int UU, DivMode M>
   __device__ __forceinline__ double tile(double x0d, double h) const {
     const float x0 = static_cast<float>(x0d);
@@ -98,7 +112,7 @@ struct Pi4F32 : TileDefaults<Pi4F32> {
       for (int u = 0; u < UU; u += 2) {
         const f32x2 uu = {static_cast<float>(u), static_cast<float>(u + 1)};
         const f32x2 x = pk_fma(uu, hh, xb);
-        acc += one / pk_fma(x, x, one);
+        acc += recip_narrow(pk_fma(x, x, one));
       }
       return static_cast<double>(acc.x) + static_cast<double>(acc.y);
     } else {
@@ -194,6 +208,31 @@ struct Pi4F32 : TileDefaults<Pi4F32> {
     }
   }
 };
+// fp32 4/(1+x^2) by the library's full IEEE division, for kIeee launches whose coordinates can
+// reach |x| >= 2^49 (the dispatcher picks it, as Pi4Wide for fp64).
+struct Pi4F32Wide : Pi4F32 {
+  template <int UU, DivMode M>
+  __device__ __forceinline__ double tile(double x0d, double h) const {
+    static_assert(M == DivMode::kIeee, "wide-domain fp32 Pi4 runs IEEE division only");
+    const float x0 = static_cast<float>(x0d);
+    const float hf = static_cast<float>(h);
+    float acc0 = 0.0f, acc1 = 0.0f;
+#pragma unroll
+    for (int u = 0; u < UU; u += 2) {  // the same pairing as Pi4F32::tile
+      const float xa = fmaf(static_cast<float>(u), hf, x0);
+      const float xb = fmaf(static_cast<float>(u + 1), hf, x0);
+      acc0 += 1.0f / fmaf(xa, xa, 1.0f);
+      acc1 += 1.0f / fmaf(xb, xb, 1.0f);
+    }
+    return static_cast<double>(acc0) + static_cast<double>(acc1);
+  }
+  template <int UU, DivMode M>
+  __device__ __forceinline__ double tile_acc(double x0d, double h, double acc) const {
+    return acc + tile<UU, M>(x0d, h);
+  }
+};
+constexpr double kPi4F32NarrowMaxX = 0x1p49;
+
 // The host's series validity check (series_ok: kSeriesHalfSpan * h <= 2e-6) must bound the
 // farthest sample offset of both Pi4 series tiles.
 static_assert(2 * AngleSeries<12>::kPairs + 12 == kSinTrig, "trig table sized for Sin");
@@ -216,6 +255,12 @@ template <> struct Maker<Pi4> {
 template <> struct Maker<Pi4Wide> {
   static constexpr int kLds = 1;
   __device__ static Pi4Wide make(const RiemannParams&, const double*, int, double*) { return {}; }
+};
+template <> struct Maker<Pi4F32Wide> {
+  static constexpr int kLds = 1;
+  __device__ static Pi4F32Wide make(const RiemannParams&, const double*, int, double*) {
+    return {};
+  }
 };
 template <> struct Maker<Pi4F32> {
   static constexpr int kLds = 1;
@@ -346,7 +391,7 @@ __device__ __forceinline__ F make_functor(const RiemannParams& p, const double* 
 template <DivMode M, class F>
 constexpr bool occupancy_hint() {
   if constexpr (__is_same(F, Pi4)) return M == DivMode::kSeriesDirect;
-  else if constexpr (__is_same(F, Pi4F32)) return M == DivMode::kIeee;
+  else if constexpr (__is_same(F, Pi4F32) || __is_same(F, Pi4F32Wide)) return M == DivMode::kIeee;
   else if constexpr (__is_same(F, Sin)) return M == DivMode::kIeee;
   else if constexpr (__is_same(F, PolyF32<16>)) return true;
   else if constexpr (IsPoly<F>::value) return M == DivMode::kSeries;
@@ -513,6 +558,12 @@ __global__ __launch_bounds__(B) void recip_narrow_kernel(const double* d, uint64
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * B + threadIdx.x; i < n; i += stride)
     out[i] = Pi4::recip_narrow(d[i]);
 }
+__global__ __launch_bounds__(B) void recip_narrow_f32_kernel(const float* d, uint64_t n,
+                                                             float* out) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * B;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * B + threadIdx.x; i < n; i += stride)
+    out[i] = Pi4F32::recip_narrow(f32x2{d[i], d[i]}).x;
+}
 
 template <DivMode M, class F>
 void launch_partials_t(const RiemannParams& p, LaunchShape shape, const double* table,
@@ -549,12 +600,12 @@ void launch_chained_t(const RiemannParams& p, LaunchShape shape, const double* t
 // kIeee Pi4 launches take Pi4::recip_narrow when both end coordinates (the extremes: x is
 // linear in the sample index) stay below kPi4NarrowMaxX in magnitude; NaN ends do not.
 std::atomic<bool> g_pi4_library_division{false};  // validation switch: always Pi4Wide
-inline bool pi4_narrow(const RiemannParams& p) {
+inline bool pi4_narrow(const RiemannParams& p, double max_x = kPi4NarrowMaxX) {
   if (g_pi4_library_division.load(std::memory_order_relaxed)) return false;
   const double first = static_cast<double>(p.i_begin) + p.off;
   const double last = static_cast<double>(p.i_begin + (p.n > 0 ? p.n - 1 : 0)) + p.off;
-  return std::fabs(std::fma(first, p.h, p.a)) < kPi4NarrowMaxX &&
-         std::fabs(std::fma(last, p.h, p.a)) < kPi4NarrowMaxX;
+  return std::fabs(std::fma(first, p.h, p.a)) < max_x &&
+         std::fabs(std::fma(last, p.h, p.a)) < max_x;
 }
 
 // Dispatch (integrand, dtype, division mode) to a template instantiation. Transcendental
@@ -567,7 +618,8 @@ void dispatch(const RiemannParams& p, DType dtype, DivMode m, A&&... a) {
     switch (f) {
       case Integrand::kPi4:
         if (ser) Op<DivMode::kSeries, Pi4F32>::run(a...);
-        else Op<DivMode::kIeee, Pi4F32>::run(a...);
+        else if (pi4_narrow(p, kPi4F32NarrowMaxX)) Op<DivMode::kIeee, Pi4F32>::run(a...);
+        else Op<DivMode::kIeee, Pi4F32Wide>::run(a...);
         return;
       case Integrand::kSin:
         if (ser) Op<DivMode::kSeries, SinF32>::run(a...);
@@ -780,6 +832,14 @@ void launch_pi4_recip_narrow(const double* d, uint64_t n, double* out, hipStream
   const uint64_t blocks = (n + B - 1) / B;
   const int grid = static_cast<int>(blocks < 8192 ? blocks : 8192);
   recip_narrow_kernel<<<grid, B, 0, stream>>>(d, n, out);
+  MIINT_HIP(hipGetLastError());
+}
+
+void launch_pi4_recip_narrow_f32(const float* d, uint64_t n, float* out, hipStream_t stream) {
+  if (n == 0) return;
+  const uint64_t blocks = (n + B - 1) / B;
+  const int grid = static_cast<int>(blocks < 8192 ? blocks : 8192);
+  recip_narrow_f32_kernel<<<grid, B, 0, stream>>>(d, n, out);
   MIINT_HIP(hipGetLastError());
 }
 

@@ -120,11 +120,10 @@ PYBIND11_MODULE(_miint, m) {
     return f;
   });
   m.def("process_start_seconds", &process_start_seconds);
-  m.def("enable_tracing", &enable_tracing, "roctx ranges around runtime phases (MIINT_ROCTX=1)");
+  m.def("enable_tracing", &enable_tracing, py::arg("on"),
+        "roctx ranges around runtime phases (MIINT_ROCTX=1)");
   m.def("tracing_enabled", &tracing_enabled);
   m.def("trace_mark", &trace_mark);
-  m.def("enable_tracing", &enable_tracing, py::arg("on"));
-  m.def("tracing_enabled", &tracing_enabled);
   m.def("wait_with_timeout", [](uintptr_t s, double timeout_s) {
     py::gil_scoped_release nogil;
     return wait_with_timeout(stream(s), timeout_s, nullptr);
@@ -297,6 +296,9 @@ PYBIND11_MODULE(_miint, m) {
         });
   m.def("launch_pi4_recip_narrow", [](uintptr_t d, uint64_t n, uintptr_t out, uintptr_t s) {
     launch_pi4_recip_narrow(ptr<const double>(d), n, ptr<double>(out), stream(s));
+  });
+  m.def("launch_pi4_recip_narrow_f32", [](uintptr_t d, uint64_t n, uintptr_t out, uintptr_t s) {
+    launch_pi4_recip_narrow_f32(ptr<const float>(d), n, ptr<float>(out), stream(s));
   });
   m.def("set_pi4_library_division", &set_pi4_library_division,
         "validation: kIeee Pi4 launches use the full library division (bitwise the same sums)");

@@ -154,10 +154,12 @@ def point_values(spec: IntegrandSpec, n: int, rule: str = "left", div: str = "se
 
 def pi4_recip_narrow(d: torch.Tensor) -> torch.Tensor:
     """The IEEE-division kIeee Pi4 tiles' reciprocal of every element of ``d`` (validation:
-    bitwise 1 / d for 1 <= d <= 2**500)."""
-    _check(d, name="d")
+    bitwise 1 / d for 1 <= d <= 2**500 in fp64, 2**100 in fp32 — the fp32 tiles' form)."""
+    f32 = d.dtype == torch.float32
+    _check(d, dtype=torch.float32 if f32 else torch.float64, name="d")
     out = torch.empty_like(d)
-    native().launch_pi4_recip_narrow(d.data_ptr(), d.numel(), out.data_ptr(), _stream())
+    launch = native().launch_pi4_recip_narrow_f32 if f32 else native().launch_pi4_recip_narrow
+    launch(d.data_ptr(), d.numel(), out.data_ptr(), _stream())
     return out
 
 

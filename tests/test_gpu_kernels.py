@@ -597,3 +597,40 @@ def test_pi4_ieee_wide_domain(cuda):
     assert got == pytest.approx(spec.analytic(), rel=1e-9)
     over = integrands.IntegrandSpec("pi4", 1e160, 2e160)
     assert float(kernels.riemann(over, 4097, rule="mid", div="ieee").item()) == 0.0
+
+
+def test_pi4_recip_narrow_f32_bitwise_ieee(cuda):
+    """The fp32 kIeee tiles' packed reciprocal (Pi4F32::recip_narrow) is bitwise IEEE fp32
+    1/d on [1, 2^100]: uniform [1, 2), random significands at exponents 0..99, the first and
+    last 4096 significands of a few binades."""
+    g = torch.Generator().manual_seed(11)
+    m = 1 << 21
+    uni = 1.0 + torch.rand(m, generator=g, dtype=torch.float64)
+    wide = torch.ldexp(1.0 + torch.rand(m, generator=g, dtype=torch.float64),
+                       torch.randint(0, 100, (m,), generator=g))
+    k = torch.arange(4096, dtype=torch.float64)
+    sig = torch.cat([1.0 + k * 2.0**-23, 2.0 - (k + 1) * 2.0**-23])
+    edges = torch.cat([torch.ldexp(sig, torch.full_like(sig, s, dtype=torch.int64))
+                       for s in (0, 1, 20, 99)])
+    d = torch.cat([uni, wide, edges]).to(torch.float32)
+    got = kernels.pi4_recip_narrow(d.to(cuda)).cpu()
+    want = 1.0 / d  # host IEEE fp32 division
+    bad = (got.view(torch.int32) != want.view(torch.int32)).nonzero().flatten()
+    assert bad.numel() == 0, f"{bad.numel()} of {d.numel()} differ, first d = {d[bad[:4]].tolist()}"
+
+
+@pytest.mark.parametrize("n", [4097, 1_000_003, 40_000_001])
+def test_pi4_fp32_ieee_tiles_equal_library_division(native, cuda, n):
+    """fp32 kIeee sums (the IEEE fallback below N = 4.8e7) are bitwise those of the full
+    library division (Pi4F32Wide); a domain beyond 2^49 runs that division."""
+    spec = integrands.pi4()
+    fast = float(kernels.riemann(spec, n, rule="mid", dtype="fp32", div="ieee").item())
+    native.set_pi4_library_division(True)
+    try:
+        lib = float(kernels.riemann(spec, n, rule="mid", dtype="fp32", div="ieee").item())
+    finally:
+        native.set_pi4_library_division(False)
+    assert fast == lib
+    far = integrands.IntegrandSpec("pi4", 1e16, 2e16)
+    got = float(kernels.riemann(far, 4097, rule="mid", dtype="fp32", div="ieee").item())
+    assert got == pytest.approx(far.analytic(), rel=1e-5)

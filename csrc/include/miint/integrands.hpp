@@ -42,9 +42,10 @@ struct TileDefaults {
 
 // ------------------------------------------------------------------ 4/(1+x^2), fp64
 //
-// Division is the whole cost of this integrand. The IEEE path (DivMode::kIeee) lets the
-// compiler emit v_div_scale/v_rcp_f64/v_fma_f64 x4/v_div_fmas/v_div_fixup per point
-// (~14 VALU f64 ops per sample with the coordinate and the accumulation).
+// Division is the whole cost of this integrand. The IEEE path (DivMode::kIeee) runs the
+// library's division sequence per point, minus its range handling (recip_narrow: v_rcp_f64
+// and 6 fma, bitwise IEEE; 10.4 VALU per sample with the coordinate and the accumulation,
+// against 14.5 with v_div_scale/v_div_fmas/v_div_fixup).
 //
 // The series paths evaluate the same reciprocal per point from a per-tile seed:
 //   s  ~= 1/d(x_m)                   (v_rcp_f64 once per tile; x_m = tile midpoint; the

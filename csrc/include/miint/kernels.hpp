@@ -29,7 +29,7 @@ inline bool direct_ok(double h) { return kDirectHalfSpan * (h < 0 ? -h : h) <= 2
 
 // Division mode actually used for step h: the 192-sample series tiles need N > 4.8e7 on
 // [0, 1]; a coarser step still fits the 32-sample kSeriesDirect tiles down to N = 8e6
-// (5 VALU per sample against ~14 for IEEE division); coarser steps use IEEE division.
+// (5 VALU per sample against ~10 for IEEE division); coarser steps use IEEE division.
 inline DivMode effective_div(DivMode d, double h) {
   if (d == DivMode::kIeee) return d;
   if (d == DivMode::kSeries && series_ok(h)) return d;

@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""Speed-of-light table of the hot kernels from rocprofv3 PMC runs (tools/profile_counters.sh).
+
+    python tools/roofline.py gpurun_out/pmc > profiles/r2/roofline.md
+
+For every (workload, kernel) whose median dispatch is at least --min-us long:
+  valu_bound_us  (4 cycles x non-transcendental VALU + 16 x SQ_INSTS_VALU_TRANS_F64) /
+                 (1024 SIMDs x 2.4 GHz): a wave64 fp64 or packed-fp32 VALU instruction occupies
+                 its SIMD for 4 cycles, a v_rcp_f64 for 16 (valu_rate_probe: 4.69 vs 16.3
+                 nominal cycles, profiles/r2/valu_rate_probe2.jsonl); the issue-limited time of
+                 the whole dispatch at the nominal clock. (Plain fp32 VALU issues in ~2.6, so
+                 fp32 kernels with many unpacked ops are over-charged here.)
+  hbm_bound_us   (FETCH_SIZE + WRITE_SIZE) / 8 TB/s (MI355X spec; ~6.3-6.9 TB/s is what a
+                 streaming kernel reaches, profiles/r1 and r2 trainscan rows), when collected
+  sol            max(bounds) / measured median dispatch time: the fraction of the tighter
+                 roofline the kernel reaches
+  valu_per_sample, when the workload's sample count is known (Riemann workloads: 1e9)
+Counters of one workload come from several runs (one counter group each); per counter the
+median over that workload's dispatches of the kernel is used.
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import csv
+import glob
+import os
+import statistics
+
+SIMDS = 256 * 4
+CLOCK_HZ = 2.4e9
+VALU_CYCLES = 4
+TRANS_F64_CYCLES = 16
+HBM_BPS = 8.0e12
+
+SAMPLES = {  # samples per dispatch of the Riemann workloads (miint bench default N)
+    "pi4_series": 1e9, "pi4_ieee": 1e9, "pi4_fp32": 1e9, "sin": 1e9, "sin_ocml": 1e9,
+    "train": 1e9, "poly": 1e9, "table": 1e9, "table2d": 4096 * 4096, "trainscan": 18e6,
+    "materialize": 18e6,
+}
+
+
+def short(name: str) -> str:
+    n = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    n = n.replace("miint::", "").replace("(miint::DivMode)", "div")
+    depth, out = 0, []
+    for ch in n:
+        if ch == "(" and depth == 0:
+            break
+        depth += ch == "<"
+        depth -= ch == ">"
+        out.append(ch)
+    return "".join(out)[:70]
+
+
+def collect(root: str):
+    ctr = collections.defaultdict(lambda: collections.defaultdict(list))
+    dur = collections.defaultdict(list)
+    for d in sorted(glob.glob(os.path.join(root, "*_G*"))):
+        if not os.path.isdir(d):
+            continue
+        workload = os.path.basename(d).rsplit("_G", 1)[0]
+        for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+            seen = set()
+            with open(f) as fh:
+                for r in csv.DictReader(fh):
+                    k = (workload, short(r.get("Kernel_Name", "?")))
+                    try:
+                        ctr[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+                    except (KeyError, ValueError):
+                        continue
+                    did = (r.get("Dispatch_Id"), r.get("Correlation_Id"))
+                    if did not in seen:
+                        seen.add(did)
+                        try:
+                            dur[k].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+                        except (KeyError, ValueError):
+                            pass
+    return ctr, dur
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("root", nargs="?", default="gpurun_out/pmc")
+    ap.add_argument("--min-us", type=float, default=4.0)
+    a = ap.parse_args()
+    ctr, dur = collect(a.root)
+    print("| workload | kernel | median us | VALU insts | VALU/sample | VALU bound us | "
+          "HBM bytes | HBM bound us | speed of light |")
+    print("|---|---|---|---|---|---|---|---|---|")
+    for (w, kname), cs in sorted(ctr.items()):
+        if "rocclr" in kname or not dur[(w, kname)]:
+            continue
+        t_us = statistics.median(dur[(w, kname)]) / 1e3
+        if t_us < a.min_us:
+            continue
+        med = {c: statistics.median(v) for c, v in cs.items()}
+        valu = med.get("SQ_INSTS_VALU")
+        trans = med.get("SQ_INSTS_VALU_TRANS_F64", 0.0)
+        vb = ((valu - trans) * VALU_CYCLES + trans * TRANS_F64_CYCLES) / (SIMDS * CLOCK_HZ) * 1e6 \
+            if valu else None
+        nbytes = None
+        if "FETCH_SIZE" in med or "WRITE_SIZE" in med:  # kilobytes
+            nbytes = (med.get("FETCH_SIZE", 0.0) + med.get("WRITE_SIZE", 0.0)) * 1024
+        hb = nbytes / HBM_BPS * 1e6 if nbytes else None
+        bound = max(b for b in (vb, hb, 0.0) if b is not None)
+        per = f"{valu * 64 / SAMPLES[w]:.2f}" if valu and w in SAMPLES else "—"
+        print(f"| {w} | `{kname}` | {t_us:.1f} | {valu:.3g} | {per} | "
+              f"{vb:.1f} | {'—' if nbytes is None else f'{nbytes:.3g}'} | "
+              f"{'—' if hb is None else f'{hb:.1f}'} | {bound / t_us:.0%} |"
+              if valu else
+              f"| {w} | `{kname}` | {t_us:.1f} | — | — | — | "
+              f"{'—' if nbytes is None else f'{nbytes:.3g}'} | {'—' if hb is None else f'{hb:.1f}'} | "
+              f"{bound / t_us:.0%} |")
+
+
+if __name__ == "__main__":
+    main()

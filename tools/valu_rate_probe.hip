@@ -1,5 +1,6 @@
 // Microbenchmark: VALU issue cost per wave instruction on gfx950 for the forms the hot loops
-// use — v_fma_f64, v_fma_f32, v_pk_fma_f32 (two fp32 lanes per op), v_pk_add_f32 — with 8
+// use — v_fma_f64, v_fma_f32, v_pk_fma_f32 (two fp32 lanes per op), v_pk_add_f32, and the
+// reciprocal seeds v_rcp_f64 / v_rcp_f32 (alone and, for fp64, in the 1 + 6 fma mix) — with 8
 // waves per SIMD and 8 independent chains per wave (throughput, not latency).
 //
 //   hipcc --offload-arch=gfx950 -O3 tools/valu_rate_probe.hip -o build/bin/valu_rate_probe
@@ -62,6 +63,38 @@ __global__ __launch_bounds__(256) void k_rate(float a, float b, float* out) {
 #pragma unroll
     for (int c = 0; c < kChains; ++c) s += x[c];
     out[blockIdx.x * 256 + threadIdx.x] = s;
+  } else if constexpr (K == 4 || K == 6) {  // v_rcp_f64 chains; 6: one rcp + 6 fma each
+    double x[kChains];
+#pragma unroll
+    for (int c = 0; c < kChains; ++c) x[c] = a + c + 1.5;
+    for (int i = 0; i < kIter; ++i) {
+#pragma unroll
+      for (int c = 0; c < kChains; ++c) {
+        x[c] = __builtin_amdgcn_rcp(x[c]);
+        if constexpr (K == 6) {
+#pragma unroll
+          for (int f = 0; f < 6; ++f) x[c] = fma_t<double>(x[c], (double)a, (double)b);
+        }
+      }
+      asm volatile("" ::: "memory");
+    }
+    double s = 0;
+#pragma unroll
+    for (int c = 0; c < kChains; ++c) s += x[c];
+    out[blockIdx.x * 256 + threadIdx.x] = (float)s;
+  } else if constexpr (K == 5) {  // v_rcp_f32 chains
+    float x[kChains];
+#pragma unroll
+    for (int c = 0; c < kChains; ++c) x[c] = a + c + 1.5f;
+    for (int i = 0; i < kIter; ++i) {
+#pragma unroll
+      for (int c = 0; c < kChains; ++c) x[c] = __builtin_amdgcn_rcpf(x[c]);
+      asm volatile("" ::: "memory");
+    }
+    float s = 0;
+#pragma unroll
+    for (int c = 0; c < kChains; ++c) s += x[c];
+    out[blockIdx.x * 256 + threadIdx.x] = s;
   } else {
     f32x2 x[kChains];
     const f32x2 va = {a, a}, vb = {b, b};
@@ -99,7 +132,8 @@ int run(const char* name, int elems_per_instr, float* out, int grid, const hipDe
     CHECK(hipEventElapsedTime(&ms, e0, e1));
     if (ms < best) best = ms;
   }
-  const double waves = grid * 4.0, instr = static_cast<double>(kIter) * kChains;
+  const double waves = grid * 4.0,
+               instr = static_cast<double>(kIter) * kChains * (K == 6 ? 7 : 1);
   const double simds = p.multiProcessorCount * 4.0, clk = p.clockRate * 1e3;
   const double cyc = best * 1e-3 * clk * simds / (waves * instr);
   std::printf("{\"form\": \"%s\", \"ms\": %.4f, \"cycles_per_instr_per_simd\": %.3f, "
@@ -118,6 +152,10 @@ int main() {
   if (run<1>("v_fma_f32", 1, out, grid, p)) return 1;
   if (run<2>("v_pk_fma_f32", 2, out, grid, p)) return 1;
   if (run<3>("v_pk_add_f32", 2, out, grid, p)) return 1;
+  if (run<4>("v_rcp_f64", 1, out, grid, p)) return 1;
+  if (run<5>("v_rcp_f32", 1, out, grid, p)) return 1;
+  // the narrow reciprocal's mix (integrands.hpp Pi4::recip_narrow): per instruction of 1 rcp + 6 fma
+  if (run<6>("v_rcp_f64 + 6 v_fma_f64", 1, out, grid, p)) return 1;
   CHECK(hipFree(out));
   return 0;
 }

@@ -507,9 +507,19 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
 
     m = native()
     local = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", ctx.world)))
-    share_given = any(os.environ.get(k) for k in ("MIINT_HOST_THREADS", "OMP_NUM_THREADS"))
-    threads = m.HostPool.default_threads() if share_given else \
-        max(1, m.HostPool.default_threads() // local)
+    # torch.distributed.run sets OMP_NUM_THREADS=1 for every rank when it starts several per
+    # node and the variable was unset: that is its default, not a share someone chose, so
+    # the ranks then split this process's CPU affinity instead
+    torchrun_default = ("TORCHELASTIC_RUN_ID" in os.environ and local > 1 and
+                        os.environ.get("OMP_NUM_THREADS") == "1" and
+                        not os.environ.get("MIINT_HOST_THREADS"))
+    share_given = not torchrun_default and \
+        any(os.environ.get(k) for k in ("MIINT_HOST_THREADS", "OMP_NUM_THREADS"))
+    if torchrun_default:
+        threads = max(1, len(os.sched_getaffinity(0)) // local)
+    else:
+        threads = m.HostPool.default_threads() if share_given else \
+            max(1, m.HostPool.default_threads() // local)
     host = Integrator(args.integrand, n=n_total, rule=args.rule, backend="host", ctx=ctx,
                       threads=threads)
     host.run()  # warm: threads, pages

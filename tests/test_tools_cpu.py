@@ -1,0 +1,60 @@
+"""CPU tests of the profiling report tools (tools/roofline.py, tools/summarize_counters.py) on
+a synthetic rocprofv3 counter-collection tree: the speed-of-light arithmetic the committed
+profiles/r2/roofline.md rests on."""
+from __future__ import annotations
+
+import csv
+import os
+import subprocess
+import sys
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+KERNEL = "void miint::(anonymous namespace)::riemann_chained_kernel<(miint::DivMode)1, miint::Pi4>(x)"
+
+
+def _write_group(d, counters, start=1000, end=1000 + 359_400):
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "run_counter_collection.csv"), "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=["Dispatch_Id", "Correlation_Id", "Kernel_Name",
+                                          "Counter_Name", "Counter_Value", "Start_Timestamp",
+                                          "End_Timestamp"])
+        w.writeheader()
+        for name, value in counters.items():
+            w.writerow({"Dispatch_Id": 1, "Correlation_Id": 1, "Kernel_Name": KERNEL,
+                        "Counter_Name": name, "Counter_Value": value,
+                        "Start_Timestamp": start, "End_Timestamp": end})
+
+
+def test_roofline_valu_bound_with_transcendentals(tmp_path):
+    # the IEEE-division kernel's measured counters: 1.642e8 VALU of which 1.5625e7 v_rcp_f64,
+    # 359.4 us -> bound (4 x 1.4795e8 + 16 x 1.5625e7) / (1024 x 2.4e9) = 343.5 us, 96 %
+    _write_group(str(tmp_path / "pi4_ieee_G1"),
+                 {"SQ_INSTS_VALU": 1.642e8, "SQ_INSTS_VALU_TRANS_F64": 1.5625e7})
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "roofline.py"),
+                          str(tmp_path)], capture_output=True, text=True, check=True).stdout
+    row = [ln for ln in out.splitlines() if ln.startswith("| pi4_ieee")]
+    assert len(row) == 1, out
+    cells = [c.strip() for c in row[0].strip("|").split("|")]
+    assert cells[2] == "359.4"           # median dispatch, us
+    assert cells[4] == "10.51"           # VALU per sample (N = 1e9)
+    assert cells[5] == "343.5"           # VALU issue bound, us
+    assert cells[8] == "96%"
+
+
+def test_roofline_hbm_bound(tmp_path):
+    # a 288 MB store stream in 46.9 us: HBM bound 288e6 / 8e12 = 36 us -> 77 %
+    _write_group(str(tmp_path / "trainscan_G3"),
+                 {"SQ_INSTS_VALU": 8.51e6, "FETCH_SIZE": 415.2, "WRITE_SIZE": 281250.0},
+                 end=1000 + 46_900)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "roofline.py"),
+                          str(tmp_path)], capture_output=True, text=True, check=True).stdout
+    row = [ln for ln in out.splitlines() if ln.startswith("| trainscan")][0]
+    cells = [c.strip() for c in row.strip("|").split("|")]
+    assert cells[7] == "36.1" and cells[8] == "77%"
+
+
+def test_summarize_counters_table(tmp_path):
+    _write_group(str(tmp_path / "pi4_ieee_G1"), {"SQ_INSTS_VALU": 1.642e8})
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "summarize_counters.py"),
+                          str(tmp_path)], capture_output=True, text=True, check=True).stdout
+    assert "riemann_chained_kernel<(DivMode)1, Pi4>" in out and "SQ_INSTS_VALU=1.642e+08" in out

@@ -222,6 +222,11 @@ __global__ __launch_bounds__(kB) void table2d_kernel(Table2DParams p, double* pa
 constexpr int kSCols = 4;                 // columns per lane: a workgroup spans 256 columns
 constexpr int kSW = kWave * kSCols / 2;   // LDS footprint width (cells), 128
 constexpr int kSH = 32;                   // LDS footprint height (cells)
+// A launch whose row footprint fits half of it stages a kSH / 2-row tile instead: the
+// branch-free staging loads every tile row whatever the footprint, so the short footprints of
+// the 4-rows-per-wave shapes (multi-GPU row slices) load and write half the rows
+// (profiles/r2/table2d_short_tile.jsonl).
+constexpr int kSHShort = kSH / 2;
 
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
   const long long bits = __builtin_bit_cast(long long, v);
@@ -239,11 +244,11 @@ __device__ __forceinline__ double fma_sv(double a, double s, double c) {
   return r;
 }
 
-template <int MODE>
+template <int MODE, int SH>
 __global__ __launch_bounds__(kB) void table2d_stream_kernel(Table2DParams p, int rows_per_wave,
                                                             double* partials, unsigned* ticket,
                                                             double* out, Table2DChain chain) {
-  __shared__ double tile[kSH * kSW];
+  __shared__ double tile[SH * kSW];
   __shared__ double red[kB / kWave];
   __shared__ int is_last;
   const double sx = p.X / p.gx, sy = p.Y / p.gy;
@@ -269,7 +274,7 @@ __global__ __launch_bounds__(kB) void table2d_stream_kernel(Table2DParams p, int
     // kSW consecutive lanes per table row, 2 rows per pass; every pass's load in flight
     // before the LDS writes. Branch-free: a lane outside the footprint loads the corner
     // (its LDS slot is never read), and addresses are a uniform base plus 32-bit offsets.
-    constexpr int kRowsPer = kB / kSW, kPasses = kSH / kRowsPer;
+    constexpr int kRowsPer = kB / kSW, kPasses = SH / kRowsPer;
     const int w = tx1 - tx0 + 1, hgt = ty1 - ty0 + 1;
     const int lx = threadIdx.x % kSW, ly = threadIdx.x / kSW;
     const double* tb = p.table + static_cast<size_t>(ty0) * p.nx + tx0;
@@ -405,6 +410,7 @@ void launch_outer_product(const double* v, int n, double* table, hipStream_t str
 namespace {
 struct Table2DShape {
   bool stream;
+  bool short_tile;    // stream: the footprint fits kSHShort rows
   int rows_per_wave;  // stream
   int tile;           // tile kernel: 128 or 64
   dim3 grid;
@@ -424,6 +430,7 @@ Table2DShape table2d_shape(const Table2DParams& p) {
       const long nwg = static_cast<long>(gxs) * ((rows + 4 * r - 1) / (4 * r));
       sh.stream = true;
       sh.rows_per_wave = r;
+      sh.short_tile = span(4 * r, step_y) <= kSHShort;
       sh.grid = dim3(gxs, (rows + 4 * r - 1) / (4 * r));
       if (nwg >= 512) break;
     }
@@ -456,9 +463,12 @@ static void launch_table2d(const Table2DParams& p, double* partials, unsigned* t
                            double* out, Table2DChain chain, hipStream_t stream) {
   check_table2d(p);
   const Table2DShape sh = table2d_shape(p);
-  if (sh.stream)
-    table2d_stream_kernel<MODE><<<sh.grid, kB, 0, stream>>>(p, sh.rows_per_wave, partials,
-                                                            ticket, out, chain);
+  if (sh.stream && sh.short_tile)
+    table2d_stream_kernel<MODE, kSHShort><<<sh.grid, kB, 0, stream>>>(
+        p, sh.rows_per_wave, partials, ticket, out, chain);
+  else if (sh.stream)
+    table2d_stream_kernel<MODE, kSH><<<sh.grid, kB, 0, stream>>>(p, sh.rows_per_wave, partials,
+                                                                 ticket, out, chain);
   else if (sh.tile == 128)
     table2d_kernel<128, MODE><<<sh.grid, kB, 0, stream>>>(p, partials, ticket, out, chain);
   else

@@ -11,7 +11,6 @@ import os
 import socket
 
 import pytest
-import torch
 import torch.multiprocessing as mp
 
 from cuda_v_mpi_amd.parallel import decomposition

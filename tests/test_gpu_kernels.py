@@ -6,7 +6,6 @@ from __future__ import annotations
 
 import math
 
-import numpy as np
 import pytest
 import torch
 

@@ -234,6 +234,8 @@ int main(int argc, char** argv) {
       // riemann.cpp:65-86 numerics on the GPU: P = world ranks -> W = P-1 workers.
       const int P = topo.world;
       const int W = P - 1;
+      MIINT_CHECK(W < 1 || nd / W < 2147483648.0,
+                  "--parity reproduces riemann.cpp's int local_n: N / (P - 1) must stay below 2^31");
       double g_sum = 0.0;
       for (int w = 0; w < W; ++w) {
         RiemannConfig c = cfg;

@@ -213,6 +213,9 @@ double host_riemann(const RiemannConfig& cfg, uint64_t begin, uint64_t count, Ho
 double host_riemann_mpi_parity(int comm_size, double n, double range, HostPool& pool) {
   const int workers = comm_size - 1;  // rank 0 only receives (P = 1 -> 0)
   if (workers < 1) return 0.0;
+  // riemann.cpp:72's `int local_n = N / W` is undefined beyond INT_MAX: refused, not emulated
+  MIINT_CHECK(n / workers < 2147483648.0,
+              "--parity reproduces riemann.cpp's int local_n: N / (P - 1) must stay below 2^31");
   std::vector<double> part(workers, 0.0);
   const int T = pool.threads();
   pool.run([&](int t) {

@@ -176,6 +176,10 @@ long double riemann_serial(Integrand f, double a, double b, uint64_t n, Rule rul
 
 double riemann_mpi_parity(int comm_size, double n, double range) {
   const int workers = comm_size - 1;
+  // the reference's `int local_n = N / W` (riemann.cpp:72): beyond INT_MAX that conversion is
+  // undefined behaviour there; here it is refused instead of emulated
+  MIINT_CHECK(workers < 1 || n / workers < 2147483648.0,
+              "--parity reproduces riemann.cpp's int local_n: N / (P - 1) must stay below 2^31");
   double g_sum = 0.0;
   for (int w = 0; w < workers; ++w) {
     const double left = w * (range / workers);

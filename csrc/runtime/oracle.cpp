@@ -106,9 +106,13 @@ double table_integral(const std::vector<double>& v, double a, double b) {
 
 double interp(const std::vector<double>& table, double t) {
   const int nseg = static_cast<int>(table.size()) - 1;
-  int i = static_cast<int>(t);
-  i = i < 0 ? 0 : (i >= nseg ? nseg - 1 : i);
-  const double fr = t - static_cast<double>(i);
+  // segment clamped in fp64 before the conversion (a coordinate far outside the table, or
+  // NaN -> segment 0, never reaches an out-of-range double -> int conversion)
+  double seg = std::trunc(t);
+  seg = seg > nseg - 1 ? nseg - 1 : seg;
+  seg = seg >= 0.0 ? seg : 0.0;
+  const int i = static_cast<int>(seg);
+  const double fr = t - seg;
   return std::fma(table[i + 1] - table[i], fr, table[i]);
 }
 

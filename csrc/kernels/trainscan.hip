@@ -104,7 +104,12 @@ __device__ __forceinline__ Sampler make_sampler(const TrainScanKernelParams& p, 
   const uint64_t t0 = static_cast<uint64_t>(tile) * kTile;
   const uint64_t last = (t0 + kTile < p.n ? t0 + kTile : p.n) - 1;
   const int s0 = seg_of(p.dt * static_cast<double>(p.i0 + t0), nseg);
-  const int s1 = seg_of(p.dt * static_cast<double>(p.i0 + last), nseg) + 1;
+  // Entries s0 .. s1: the last sample's segment, its right end, and one more. The hot form
+  // forms t = fma(k, dt, t_first), which may round one ulp above dt * i; where dt * i sits
+  // just below an integer that puts the sample in the NEXT segment with fraction 0, and the
+  // read of that segment's right end must still land on a table value (weight 0), not on a
+  // stale LDS word past the staged range (an Inf/NaN there would survive the 0 weight).
+  const int s1 = min(seg_of(p.dt * static_cast<double>(p.i0 + last), nseg) + 2, nseg);
   if (s1 - s0 + 1 > kSpan)  // coarse sampling: read the (L2-resident) table directly
     return {p.table, false, 0, nseg, p.dt, p.i0, p.n, p.win_lo, p.win_hi};
   for (int k = threadIdx.x; k <= s1 - s0; k += kB) tab[k] = p.table[s0 + k];

@@ -617,7 +617,9 @@ __global__ __launch_bounds__(256) void ts_parity_serial(TrainScanKernelParams p,
       const uint64_t i = p.i0 + j;
       if (i >= p.win_lo && i < p.win_hi) {
         const double t = 0.0 + p.dt * static_cast<double>(i);
-        const int k = static_cast<int>(t);
+        // the reference's truncating index; its windows never reach the last entry, and the
+        // clamp (a no-op there) keeps any other window inside the table
+        const int k = min(static_cast<int>(t), p.table_n - 2);
         const double delta = t - static_cast<double>(k);
         const double prod = (p.table[k + 1] - p.table[k]) * delta;
         v = p.table[k] + prod;

@@ -1,4 +1,5 @@
-"""CPU tests of the profiling report tools (tools/roofline.py, tools/summarize_counters.py) on
+"""CPU tests of the profiling report tools (tools/roofline.py, tools/summarize_counters.py,
+tools/gap_report.py) on
 a synthetic rocprofv3 counter-collection tree: the speed-of-light arithmetic the committed
 profiles/r2/roofline.md rests on."""
 from __future__ import annotations
@@ -58,3 +59,43 @@ def test_summarize_counters_table(tmp_path):
     out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "summarize_counters.py"),
                           str(tmp_path)], capture_output=True, text=True, check=True).stdout
     assert "riemann_chained_kernel<(DivMode)1, Pi4>" in out and "SQ_INSTS_VALU=1.642e+08" in out
+
+
+def _dispatches(n=4, dur=72_000, gap=500):
+    """n back-to-back dispatches (ns timestamps), the last one 'gap' ns after its predecessor."""
+    out, t = [], 10_000
+    for i in range(n):
+        if i == n - 1:
+            t += gap
+        out.append((KERNEL if i < n - 1 else "finalize_kernel(double const*, int)", t, t + dur))
+        t += dur
+    return out
+
+
+def _gap_report(d, last):
+    return subprocess.run([sys.executable, os.path.join(ROOT, "tools", "gap_report.py"), str(d),
+                           "--last", str(last)], capture_output=True, text=True, check=True).stdout
+
+
+def test_gap_report_rocpd_database(tmp_path):
+    # rocprofv3's default output: a rocpd SQLite database with a `kernels` view
+    import sqlite3
+
+    db = sqlite3.connect(str(tmp_path / "run_results.db"))
+    db.execute("create table kernels (name text, start integer, end integer)")
+    db.executemany("insert into kernels values (?, ?, ?)", _dispatches())
+    db.commit()
+    db.close()
+    out = _gap_report(tmp_path, 3)
+    assert out.count("riemann_chained_kernel<(DivMode)1, Pi4>") == 2, out
+    assert "gaps: max 0.50 us" in out and "span 216.5 us over 3 dispatches" in out
+
+
+def test_gap_report_csv_trace(tmp_path):
+    with open(tmp_path / "run_kernel_trace.csv", "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=["Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        w.writeheader()
+        for n, s, e in _dispatches(gap=0):
+            w.writerow({"Kernel_Name": n, "Start_Timestamp": s, "End_Timestamp": e})
+    out = _gap_report(tmp_path, 4)
+    assert "gaps: max 0.00 us" in out and "over 4 dispatches" in out

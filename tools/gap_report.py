@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""Kernel gaps of the timed region from a rocprofv3 kernel trace (CSV).
+"""Kernel gaps of the timed region from a rocprofv3 kernel trace (CSV or rocpd database).
 
-    rocprofv3 --kernel-trace --output-format csv -d OUT -o run -- python3 bench.py --steps 20 --warmup 5 --no-extras
+    rocprofv3 --kernel-trace [--output-format csv] -d OUT -o run -- python3 bench.py --steps 20 --warmup 5 --no-extras
     python tools/gap_report.py OUT --last 21
 
 Prints the last `--last` dispatches (the timed region of a bench.py run is its final graph
@@ -14,7 +14,27 @@ import argparse
 import csv
 import glob
 import os
+import sqlite3
 import statistics
+
+
+def _rows(d: str) -> list[dict]:
+    """Dispatches as CSV-style dicts, from the CSV trace files or, failing those, from the
+    rocpd SQLite databases (rocprofv3's default output format)."""
+    rows: list[dict] = []
+    for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        with open(f) as fh:
+            rows.extend(csv.DictReader(fh))
+    if rows:
+        return rows
+    for f in glob.glob(os.path.join(d, "**", "*.db"), recursive=True):
+        db = sqlite3.connect(f)
+        try:
+            rows.extend({"Kernel_Name": n, "Start_Timestamp": s, "End_Timestamp": e}
+                        for n, s, e in db.execute("select name, start, end from kernels"))
+        finally:
+            db.close()
+    return rows
 
 
 def main() -> int:
@@ -22,11 +42,10 @@ def main() -> int:
     ap.add_argument("dir")
     ap.add_argument("--last", type=int, default=21)
     a = ap.parse_args()
-    files = glob.glob(os.path.join(a.dir, "**", "*kernel_trace.csv"), recursive=True)
-    rows = []
-    for f in files:
-        with open(f) as fh:
-            rows.extend(csv.DictReader(fh))
+    rows = _rows(a.dir)
+    if not rows:
+        print(f"no kernel dispatches under {a.dir} (*kernel_trace.csv or *_results.db)")
+        return 1
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     tail = rows[-a.last:]
     prev_end = None

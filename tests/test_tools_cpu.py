@@ -1,7 +1,6 @@
 """CPU tests of the profiling report tools (tools/roofline.py, tools/summarize_counters.py,
-tools/gap_report.py) on
-a synthetic rocprofv3 counter-collection tree: the speed-of-light arithmetic the committed
-profiles/r2/roofline.md rests on."""
+tools/gap_report.py) on synthetic rocprofv3 output trees: the speed-of-light arithmetic the
+committed profiles/r2/roofline.md rests on, and the timed-region gap report."""
 from __future__ import annotations
 
 import csv

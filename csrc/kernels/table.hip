@@ -14,6 +14,8 @@
 // down the rows.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cmath>
 #include <type_traits>
 
 #include "miint/common.hpp"
@@ -52,35 +54,59 @@ __global__ __launch_bounds__(kB) void sum_array_kernel(const double* __restrict_
 
 // ---------------------------------------------------------------------------- interp fill
 constexpr int kMaxTable = 2048;
+constexpr uint64_t kFillBlocks = 2048;
+
+// Clamped segment of time t (in table steps): clamped in fp64 before the conversion, so a t
+// beyond the int range is the last segment, not an undefined conversion.
+__device__ __forceinline__ int seg_of(double t, int nseg) {
+  return t >= static_cast<double>(nseg) ? nseg - 1 : (t < 1.0 ? 0 : static_cast<int>(t));
+}
 
 __device__ __forceinline__ double interp_lds(const double* tab, int nseg, double t) {
-  int i = static_cast<int>(t);
-  i = i < 0 ? 0 : (i >= nseg ? nseg - 1 : i);
+  const int i = seg_of(t, nseg);
   const double v0 = tab[i];
   return fma(tab[i + 1] - v0, t - static_cast<double>(i), v0);
 }
 
+// Each workgroup owns one contiguous chunk of the output (C double2 vectors, walked 256 at a
+// time: every pass is one coalesced 4 KB store) and stages only the table entries its chunk
+// can touch, [k0, k1 + 1]: the clamped segment index is monotonic in the sample index, so
+// the chunk's first and last samples bound it. At the reference's 10 000 samples/s a
+// 2048-workgroup fill of 18e6 samples touches 2-3 entries per workgroup; the grid-stride form
+// this replaced staged the whole 1801-entry table in each of 8192 workgroups (118 MB of L2
+// reads beside 144 MB of stores): 28.2-29.4 -> 23.4-23.7 us, 5.0 -> 6.1 TB/s, measured
+// alternately in one process per build (profiles/r2/interp_fill_ab.jsonl; tools/fill_ab.sh).
+// One store per lane per pass: unrolling by 4, or 1024 / 4096 workgroups, measured 24.0 us.
 __global__ __launch_bounds__(kB) void interp_fill_kernel(const double* __restrict__ table,
                                                          int table_n, double dt, uint64_t i0,
-                                                         uint64_t n, double* __restrict__ y) {
+                                                         uint64_t n, uint64_t chunk,
+                                                         double* __restrict__ y) {
   __shared__ double tab[kMaxTable];
-  for (int k = threadIdx.x; k < table_n; k += kB) tab[k] = table[k];
-  __syncthreads();
   const int nseg = table_n - 1;
-  const uint64_t lanes = static_cast<uint64_t>(gridDim.x) * kB;
   const uint64_t nv = n / 2;
-  f64x2* yv = reinterpret_cast<f64x2*>(y);
-  // y may be at an odd element offset inside a larger buffer only if the caller passes
-  // an aligned pointer; the launcher checks 16-B alignment.
-  for (uint64_t v = static_cast<uint64_t>(blockIdx.x) * kB + threadIdx.x; v < nv; v += lanes) {
-    const uint64_t i = i0 + 2 * v;
-    f64x2 o;
-    o.x = interp_lds(tab, nseg, dt * static_cast<double>(i));
-    o.y = interp_lds(tab, nseg, dt * static_cast<double>(i + 1));
-    yv[v] = o;
+  const uint64_t vb = static_cast<uint64_t>(blockIdx.x) * chunk;
+  const uint64_t ve = vb + chunk < nv ? vb + chunk : nv;
+  auto seg = [&](uint64_t i) { return seg_of(dt * static_cast<double>(i), nseg); };
+  if (vb < ve) {
+    const int ka = seg(i0 + 2 * vb), kb = seg(i0 + 2 * ve - 1);
+    const int k0 = ka < kb ? ka : kb, k1 = ka < kb ? kb : ka;
+    for (int k = k0 + static_cast<int>(threadIdx.x); k <= k1 + 1; k += kB) tab[k - k0] = table[k];
+    __syncthreads();
+    auto at = [&](uint64_t i) {  // interp_lds on the staged window (tab[j] = table[k0 + j])
+      const double t = dt * static_cast<double>(i);
+      const int k = seg(i);
+      const double v0 = tab[k - k0];
+      return fma(tab[k - k0 + 1] - v0, t - static_cast<double>(k), v0);
+    };
+    f64x2* yv = reinterpret_cast<f64x2*>(y);
+#pragma unroll 1
+    for (uint64_t v = vb + threadIdx.x; v < ve; v += kB) {
+      const uint64_t i = i0 + 2 * v;
+      yv[v] = f64x2{at(i), at(i + 1)};
+    }
   }
-  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0)
-    y[n - 1] = interp_lds(tab, nseg, dt * static_cast<double>(i0 + n - 1));
+  if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0)  // the odd last sample, from global
+    y[n - 1] = interp_lds(table, nseg, dt * static_cast<double>(i0 + n - 1));
 }
 
 // ---------------------------------------------------------------------------- outer product
@@ -389,9 +415,14 @@ void launch_interp_fill(const double* table, int table_n, double dt, uint64_t i0
   MIINT_CHECK(table_n >= 2 && table_n <= kMaxTable, "table size must be in [2, 2048]");
   MIINT_CHECK((reinterpret_cast<uintptr_t>(y) & 15) == 0, "interp_fill needs 16-B alignment");
   MIINT_CHECK(n >= 1, "empty fill");
-  const uint64_t nv = (n + 1) / 2;
-  const int grid = static_cast<int>(std::min<uint64_t>((nv + kB - 1) / kB, 8192));
-  interp_fill_kernel<<<grid, kB, 0, stream>>>(table, table_n, dt, i0, n, y);
+  MIINT_CHECK(dt > 0.0 && std::isfinite(dt), "interp_fill needs a finite dt > 0");
+  // 2048 workgroups = 8 waves on each of the 256 CUs' 4 SIMDs; chunks a multiple of 256
+  // vectors so every pass but a chunk's last stores whole 4 KB lines
+  const uint64_t nv = n / 2;
+  const uint64_t per = (nv + kFillBlocks - 1) / kFillBlocks;
+  const uint64_t chunk = std::max<uint64_t>(kB, (per + kB - 1) / kB * kB);
+  const int grid = static_cast<int>(std::max<uint64_t>(1, (nv + chunk - 1) / chunk));
+  interp_fill_kernel<<<grid, kB, 0, stream>>>(table, table_n, dt, i0, n, chunk, y);
   MIINT_HIP(hipGetLastError());
 }
 

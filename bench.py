@@ -191,9 +191,6 @@ def main(argv=None) -> int:
     if cpu and args.backend != "gloo" and world_env > 1:
         print("bench.py: --device cpu needs --backend gloo", file=sys.stderr)
         return 2
-    if args.backend == "gloo" and args.comm == "native" and world_env > 1 and not cpu:
-        print("bench.py: --backend gloo shares GPUs between ranks; use --comm torch", file=sys.stderr)
-        return 2
     ctx = mdist.init(backend=args.backend, force=False)
     world = ctx.world
     for k, want in (("RANK", ctx.rank), ("LOCAL_RANK", ctx.local_rank), ("WORLD_SIZE", world)):
@@ -206,11 +203,33 @@ def main(argv=None) -> int:
         if not cpu:
             torch.cuda.synchronize()
 
+    def make_integ(comm):
+        return Integrator(args.integrand, n=n_total, rule=args.rule, dtype=args.dtype,
+                          div=args.div, backend="cpu" if cpu else "hip", ctx=ctx, comm=comm,
+                          fused=not args.unfused, grid=args.grid, slots=args.slots,
+                          force_collective=args.force_collective, bucket=not args.no_bucket)
+
+    # A native RCCL communicator that fails to come up on every rank (the failure is agreed
+    # over the torch process group, so all ranks switch together) falls back to the
+    # torch.distributed step path instead of ending the run without a record.
+    comm_fallback = None
+    try:
+        integ, init_error = make_integ(args.comm), None
+    except Exception as e:  # noqa: BLE001
+        integ, init_error = None, e
+    if world > 1 and not cpu and args.comm == "native":
+        flag = torch.tensor([0.0 if init_error is None else 1.0], dtype=torch.float64, device=dev)
+        ctx.all_reduce_max(flag)
+        if flag.item() > 0:
+            comm_fallback = (f"{type(init_error).__name__}: {init_error}" if init_error
+                             else "a peer rank failed to create the native communicator")
+            print(f"bench.py: native RCCL communicator failed ({comm_fallback}); "
+                  "falling back to --comm torch", file=sys.stderr)
+            args.comm = "torch"
+            integ, init_error = make_integ("torch"), None
+    if init_error is not None:
+        raise init_error
     use_torch = args.comm == "torch" and world > 1 and not cpu
-    integ = Integrator(args.integrand, n=n_total, rule=args.rule, dtype=args.dtype, div=args.div,
-                       backend="cpu" if cpu else "hip", ctx=ctx, comm=args.comm,
-                       fused=not args.unfused, grid=args.grid, slots=args.slots,
-                       force_collective=args.force_collective, bucket=not args.no_bucket)
     plan = integ.plan
     graphs = not args.no_graph and not use_torch and not cpu
     pipeline = not args.no_pipeline and (world > 1 or args.force_collective)
@@ -341,6 +360,7 @@ def main(argv=None) -> int:
             "per_rank_ms": per_rank_ms,
             "per_rank_spread_ms": max(per_rank_ms) - min(per_rank_ms),
             "graph_replays_timed": graph_replays,
+            "comm_fallback": comm_fallback,
             "direct_steps_timed": direct_timed,
             **extras,
             "config": {

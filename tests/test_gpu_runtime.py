@@ -349,6 +349,19 @@ def test_bench_two_ranks_shared_gpu_torch_comm(native, cuda):
     assert js["n_gpus"] == 2 and js["config"]["N"] == 400_000_000 and js["verified"]
 
 
+def test_bench_native_comm_failure_falls_back_to_torch(native, cuda):
+    """Two ranks on one GPU with the native communicator: RCCL rejects ranks that share a
+    device ("invalid usage") on both ranks, the ranks agree on the failure over the gloo
+    group and run the torch.distributed step path instead; the record names the fallback."""
+    p = _torchrun(2, [os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo",
+                      "--comm", "native", "--steps", "12", "--warmup", "2", "--samples", "2e8",
+                      "--settle-ms", "0"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    js = json.loads(p.stdout.strip().splitlines()[-1])
+    assert js["verified"] and js["n_gpus"] == 2 and js["config"]["comm"] == "torch"
+    assert js["comm_fallback"] and "falling back to --comm torch" in p.stderr
+
+
 @pytest.mark.parametrize("bucket", [True, False])
 def test_bench_force_collective_graph(native, cuda, bucket):
     p = _run(["python", os.path.join(REPO, "bench.py"), "--steps", "40", "--warmup", "8",

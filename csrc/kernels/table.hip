@@ -6,8 +6,9 @@
 //                     loads/sample, per-thread contiguous chunks (uncoalesced stores)
 //   cuda_test pass 2  cintegrate.cu:94-96  serial re-read of the 144 MB array per thread
 //   4main fill        4main.c:82-86        same fill on the host
-// Here: table staged once per workgroup in LDS, 16-byte stores/loads per lane
-// (global_store_dwordx4 / global_load_dwordx4), grid-stride over 64-bit indices.
+// Here: the fill gives each workgroup one contiguous chunk and stages only the table window
+// that chunk touches in LDS; the sum walks the array grid-stride; both move 16 bytes per lane
+// per access (global_store_dwordx4 / global_load_dwordx4) over 64-bit indices.
 // The 2-D config (BASELINE.json #5) has no reference counterpart: it integrates a
 // ny x nx fp64 field with bilinear interpolation, each workgroup staging the table
 // footprint of its 256-column block of sample rows in LDS (2-D LDS tiling) and streaming

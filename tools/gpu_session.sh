@@ -12,7 +12,14 @@ mkdir -p gpurun_out
 # Bring the in-tree build up to date from plain bash (no GPU initialised here), never from a
 # profiled or GPU-initialised process: under rocprofv3 --pmc every child process initialises
 # the GPU and exec'ing make/sh from it is refused on this pool.
-if ! make -q all >/dev/null 2>&1; then
+# (build/obj is not shipped to the box, so `make -q` alone always reports stale objects: the
+# in-tree extension and CLIs count as current when no source or build file is newer.)
+built_ok() {
+  local so; so=$(ls cuda_v_mpi_amd/_miint*.so 2>/dev/null | head -n 1)
+  [ -n "$so" ] && [ -x build/bin/miint ] && [ -x build/bin/miintrun ] || return 1
+  [ -z "$(find csrc Makefile -newer "$so" -type f -print -quit)" ]
+}
+if ! built_ok && ! make -q all >/dev/null 2>&1; then
   echo "=== build out of date: make -j16 all" | tee -a gpurun_out/session.txt
   make -j16 all > gpurun_out/build.txt 2>&1 || { echo "=== build failed"; exit 1; }
 fi

@@ -368,11 +368,12 @@ def test_interp_fill(cuda, i0, n):
 
 @pytest.mark.parametrize("i0,n,dt", [(0, 18_000_001, 1e-4), (5, 10_001, 0.37),
                                      (123, 777_777, 2.3e-3), (0, 2, 1e-4), (3, 1, 1e-4),
-                                     (0, 1_000_000, 1.7e-3)])
+                                     (0, 1_000_000, 1.7e-3), (2**33, 5, 1.0)])
 def test_interp_fill_chunk_windows(cuda, i0, n, dt):
     """The chunked fill stages only each workgroup's table window: windows of 2-3 entries
     (1e-4), of many segments (2.3e-3, 1.7e-3: whole chunks span tens of seconds), windows
-    clamped at the table's end (0.37: t runs to 3700 s), the odd last sample, n = 1 and 2."""
+    clamped at the table's end (0.37: t runs to 3700 s; 2^33 s lies beyond the int range and
+    must land on the last segment), the odd last sample, n = 1 and 2."""
     y = kernels.interp_fill(n, i0=i0, dt=dt)
     t = dt * torch.arange(i0, i0 + n, dtype=torch.float64, device="cuda")
     torch.testing.assert_close(y, integrands.table().f_torch(t), rtol=1e-13, atol=1e-12)

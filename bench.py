@@ -78,9 +78,11 @@ def parse(argv=None) -> argparse.Namespace:
     p.add_argument("--comm", default="native", choices=["native", "torch"],
                    help="native: C++ RCCL communicator captured in the step graph; "
                         "torch: torch.distributed all_reduce of each step's partial")
-    p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
-                   help="process-group backend (gloo only for functional tests on shared GPUs "
-                        "or with --device cpu)")
+    p.add_argument("--backend", default=None, choices=["nccl", "gloo"],
+                   help="torch process-group backend. Default: gloo with --comm native (the "
+                        "group carries only the control plane; the rank's one RCCL "
+                        "communicator is the native one), nccl with --comm torch, gloo with "
+                        "--device cpu")
     p.add_argument("--device", default="gpu", choices=["gpu", "cpu"],
                    help="cpu: torch fp64 evaluation + gloo (launcher / decomposition tests "
                         "on a GPU-less box; not a performance configuration)")
@@ -90,6 +92,8 @@ def parse(argv=None) -> argparse.Namespace:
     p.add_argument("--grid", type=int, default=0)
     p.add_argument("--slots", type=int, default=48,
                    help="steps per captured graph batch (= steps per bucketed all-reduce)")
+    p.add_argument("--step-streams", type=int, default=0,
+                   help="streams a chained graph batch deals its steps over (0 = auto: 4)")
     p.add_argument("--no-bucket", action="store_true",
                    help="one all-reduce per step instead of one per graph batch of steps")
     p.add_argument("--force-collective", action="store_true",
@@ -188,6 +192,9 @@ def main(argv=None) -> int:
     from cuda_v_mpi_amd.parallel import dist as mdist
 
     cpu = args.device == "cpu"
+    backend_auto = args.backend is None
+    if backend_auto:
+        args.backend = mdist.control_backend(args.comm, args.device)
     if cpu and args.backend != "gloo" and world_env > 1:
         print("bench.py: --device cpu needs --backend gloo", file=sys.stderr)
         return 2
@@ -197,7 +204,7 @@ def main(argv=None) -> int:
         assert int(os.environ.get(k, str(want))) == want, (k, os.environ.get(k), want)
     n_per = int(args.n)
     n_total = n_per * world if args.scaling == "weak" else n_per
-    dev = "cpu" if (cpu or ctx.backend != "nccl") else "cuda"
+    dev = "cpu" if (cpu or ctx.host_collectives) else "cuda"  # control-plane tensors
 
     def sync_dev():
         if not cpu:
@@ -207,7 +214,8 @@ def main(argv=None) -> int:
         return Integrator(args.integrand, n=n_total, rule=args.rule, dtype=args.dtype,
                           div=args.div, backend="cpu" if cpu else "hip", ctx=ctx, comm=comm,
                           fused=not args.unfused, grid=args.grid, slots=args.slots,
-                          force_collective=args.force_collective, bucket=not args.no_bucket)
+                          force_collective=args.force_collective, bucket=not args.no_bucket,
+                          step_streams=args.step_streams)
 
     # A native RCCL communicator that fails to come up on every rank (the failure is agreed
     # over the torch process group, so all ranks switch together) falls back to the
@@ -245,8 +253,11 @@ def main(argv=None) -> int:
     elif use_torch:  # kernels on the torch stream + torch.distributed all_reduce per step
         from cuda_v_mpi_amd.parallel.torch_steps import TorchStepper
 
+        # an auto-chosen gloo control plane gets an RCCL group for the device collectives; an
+        # explicit --backend gloo (ranks sharing one GPU) keeps gloo on CUDA tensors
+        group = ctx.nccl_group() if (backend_auto and ctx.host_collectives) else None
         stepper = TorchStepper(integ.spec, n_total, ctx, rule=args.rule, dtype=args.dtype,
-                               div=args.div, grid=args.grid or None)
+                               div=args.div, grid=args.grid or None, group=group)
         launch, finish, result = stepper.launch_steps, stepper.sync, stepper.result
     else:
         if graphs:  # capture every graph the timed pattern replays, before anything is timed
@@ -307,9 +318,8 @@ def main(argv=None) -> int:
     vals = [result(k) for k in last]
     errs = [abs(v - analytic) for v in vals]
     abs_err = max(errs)
-    # left rule truncation for 4/(1+x^2) is exactly h; anything far above is a bug
-    tol = 4.0 * (integ.spec.b - integ.spec.a) / n_total + 1e-12 if args.rule == "left" else 1e-9
-    ok = all(math.isfinite(v) for v in vals) and (args.dtype != "fp64" or abs_err <= tol)
+    ok = all(math.isfinite(v) for v in vals) and all(
+        result_ok(args.integrand, args.rule, args.dtype, n_total, e, integ.spec) for e in errs)
 
     ms_per_step = elapsed_max / args.steps * 1e3
     value = n_total * args.steps / elapsed_max
@@ -323,6 +333,7 @@ def main(argv=None) -> int:
 
         rccl_version = native().Comm.version()
     extras = {}
+    extras_ok = True
     if not cpu and not use_torch and not args.no_extras:
         # The headline is already measured: a failure in an extra must not cost the record.
         # (Every rank runs the same extras, so an exception on one is one on all; the
@@ -332,6 +343,9 @@ def main(argv=None) -> int:
         except Exception as e:  # noqa: BLE001
             extras = {"extras_error": f"{type(e).__name__}: {e}"}
             print(f"bench.py: extras failed: {extras['extras_error']}", file=sys.stderr)
+        # every extra carries its own pass/fail; the record's `verified` is the AND of all
+        extras_ok = "extras_error" not in extras and all(
+            v.get("verified", True) for v in extras.values() if isinstance(v, dict))
 
     if ctx.is_root:
         out = {
@@ -352,11 +366,19 @@ def main(argv=None) -> int:
             "data": "synthetic (analytic integrand 4/(1+x^2); no dataset)",
             "abs_err": abs_err,
             "result": vals[-1],
-            "verified": ok,
+            "verified": bool(ok and extras_ok),
+            "headline_verified": ok,
+            "extras_verified": extras_ok,
+            "verify_rule": verify_rule(args.integrand, args.rule, args.dtype),
             "launcher": launcher,
             "parent_imported_torch": os.environ.get("MIINT_BENCH_PARENT_TORCH") == "1",
             "rccl_world": rccl_world,
             "rccl_version": rccl_version,
+            # one RCCL communicator per rank: the native one (data plane); the torch group is
+            # the control plane (gloo unless --comm torch), torch RCCL groups counted here
+            "control_plane": ctx.backend,
+            "torch_nccl_groups": ctx.nccl_groups,
+            "native_rccl_comms": int(comm is not None and getattr(comm, "kind", "") == "rccl"),
             "per_rank_ms": per_rank_ms,
             "per_rank_spread_ms": max(per_rank_ms) - min(per_rank_ms),
             "graph_replays_timed": graph_replays,
@@ -381,6 +403,8 @@ def main(argv=None) -> int:
                 "bucketed_allreduce": bool(plan.bucketed) if plan is not None else False,
                 "fused_reduction": not args.unfused,
                 "chained_batches": bool(plan.chained) and graphs if plan is not None else False,
+                "step_streams": plan.step_streams(min(args.steps, plan.slots))
+                if plan is not None else 1,
                 "grid": plan.grid if plan is not None else 0,
                 "device": args.device,
             },
@@ -391,6 +415,41 @@ def main(argv=None) -> int:
                 f.write(json.dumps(out) + "\n")
     ctx.destroy()
     return 0 if ok else 1
+
+
+# ------------------------------------------------------------------ verification
+# Every number the record reports is checked against a stated bound (riemann.cpp:94-96: the
+# printed result is the program's contract). For 4/(1+x^2) on [0, 1] the truncation error of
+# each rule is known in closed form (Euler-Maclaurin with f(0) - f(1) = 2, f'(1) - f'(0) = -2):
+#   left  value - pi = h - h^2/6 + O(h^4)     right  -h - h^2/6     mid  h^2/12
+# so a run passes when |err| is that to within 1e-13 (fp64 roundoff of a 1e10-term sum is
+# ~1e-15). fp32 runs (fp32 samples, fp64 fold) pass at |err| <= 2h + 1e-10.
+PI4_TOL = 1e-13
+
+
+def pi4_expected_abs_err(rule: str, n: int) -> float:
+    h = 1.0 / n
+    return {"left": h - h * h / 6, "right": h + h * h / 6, "mid": h * h / 12}[rule]
+
+
+def verify_rule(integrand: str, rule: str, dtype: str) -> str:
+    if integrand == "pi4" and dtype == "fp64":
+        return f"| |err| - {rule}-rule truncation | <= {PI4_TOL:g}"
+    if dtype == "fp32":
+        return "|err| <= 2h + 1e-10"
+    return "finite; left: |err| <= 4(b-a)/N + 1e-12, else <= 1e-9"
+
+
+def result_ok(integrand: str, rule: str, dtype: str, n: int, abs_err: float, spec=None) -> bool:
+    if not math.isfinite(abs_err):
+        return False
+    if dtype == "fp32":
+        span = (spec.b - spec.a) if spec is not None else 1.0
+        return abs_err <= 2.0 * span / n + 1e-10
+    if integrand == "pi4":
+        return abs(abs_err - pi4_expected_abs_err(rule, n)) <= PI4_TOL
+    span = (spec.b - spec.a) if spec is not None else 1.0
+    return abs_err <= (4.0 * span / n + 1e-12 if rule == "left" else 1e-9)
 
 
 def _timed_steps(ctx, plan, steps, pipeline, dev) -> float:
@@ -421,27 +480,33 @@ def _timed_steps(ctx, plan, steps, pipeline, dev) -> float:
 
 
 def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
-    """Measured after (never inside) the timed region; every rank takes part."""
+    """Measured after (never inside) the timed region; every rank takes part. Every plan here
+    shares the headline's native communicator (one RCCL communicator per rank)."""
     from cuda_v_mpi_amd import Integrator
     from cuda_v_mpi_amd.ops import kernels
 
     out: dict = {}
+    comm = getattr(integ, "_comm", None)
     kw = dict(rule=args.rule, dtype=args.dtype, ctx=ctx, comm=args.comm, slots=args.slots,
-              bucket=not args.no_bucket, force_collective=args.force_collective)
+              bucket=not args.no_bucket, force_collective=args.force_collective,
+              comm_obj=comm, step_streams=args.step_streams)
+    pi4 = args.integrand == "pi4"
     # (1) the same config with correctly rounded division for every sample
-    if args.integrand == "pi4" and args.div != "ieee":
+    if pi4 and args.div != "ieee":
         ie = Integrator(args.integrand, n=n_total, div="ieee", **kw)
         steps = 40
         ms = _timed_steps(ctx, ie.plan, steps, pipeline, dev)
         v = ie.plan.host_result(ie.plan.host_index_of(steps - 1, True))
+        e = abs(v - math.pi)
         out["ieee_div"] = {"value": n_total / (ms * 1e-3), "ms_per_step": ms, "steps": steps,
-                           "result": v, "abs_err": abs(v - math.pi)}
+                           "result": v, "abs_err": e,
+                           "verified": result_ok("pi4", args.rule, args.dtype, n_total, e)}
         out["ieee_div_value"] = out["ieee_div"]["value"]
         del ie
     # (2) per-point accuracy of the division the headline used, on one 64 K-sample window
     #     of this rank's slice (rank 0's is reported)
     eff = str(integ.plan.effective_div).split(".")[-1]
-    if args.integrand == "pi4" and args.dtype == "fp64" and eff != "ieee":
+    if pi4 and args.dtype == "fp64" and eff != "ieee":
         import torch
 
         i0 = integ.plan.begin + integ.plan.count // 8 + 12_345
@@ -452,34 +517,55 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
                                  n_local=w)
         spacing = torch.nextafter(r.abs(), torch.full_like(r, math.inf)) - r.abs()
         u = ((v - r) / spacing).abs()
-        out["per_point_max_ulp"] = float(u.max())
-        out["per_point_frac_within_1ulp"] = float((u <= 1.0).double().mean())
-        out["per_point_window"] = [int(i0), int(w)]
-    # (3) BASELINE config #3: N = 1e10 in total over the same GPUs (strong scaling)
-    if args.integrand == "pi4" and args.scaling == "weak":
+        out["per_point"] = {"max_ulp": float(u.max()),
+                            "frac_within_1ulp": float((u <= 1.0).double().mean()),
+                            "frac_within_2ulp": float((u <= 2.0).double().mean()),
+                            "window": [int(i0), int(w)], "bound_max_ulp": 5.0,
+                            "verified": bool(float(u.max()) <= 5.0)}
+        out["per_point_max_ulp"] = out["per_point"]["max_ulp"]
+        out["per_point_frac_within_1ulp"] = out["per_point"]["frac_within_1ulp"]
+        out["per_point_window"] = out["per_point"]["window"]
+    # (3) the headline metric's own config at every GPU count: N = 1e9 IN TOTAL split over
+    #     the ranks (riemann.cpp:10,71-73: the reference keeps N fixed and divides it among
+    #     its workers), its own graph and timing — equal to the headline at G = 1
+    if pi4:
+        n1 = 10**9
+        st = Integrator("pi4", n=n1, div=args.div, **dict(kw, dtype="fp64"))
+        steps = 48
+        ms = _timed_steps(ctx, st.plan, steps, pipeline, dev)
+        v = st.plan.host_result(st.plan.host_index_of(steps - 1, True))
+        e = abs(v - math.pi)
+        out["strong_1e9"] = {"N": n1, "value": n1 / (ms * 1e-3), "ms_per_step": ms,
+                             "steps": steps, "result": v, "abs_err": e,
+                             "n_per_gpu": st.plan.count, "grid": st.plan.grid,
+                             "scaling": "strong", "n_gpus": ctx.world,
+                             "verified": result_ok("pi4", args.rule, "fp64", n1, e)}
+        del st
+    # (4) BASELINE config #3: N = 1e10 in total over the same GPUs (strong scaling)
+    if pi4:
         n3 = 10**10
-        st = Integrator("pi4", n=n3, div=args.div, **kw)
+        st = Integrator("pi4", n=n3, div=args.div, **dict(kw, dtype="fp64"))
         steps = 20
         ms = _timed_steps(ctx, st.plan, steps, pipeline, dev)
         v = st.plan.host_result(st.plan.host_index_of(steps - 1, True))
+        e = abs(v - math.pi)
         out["baseline3_strong_1e10"] = {"N": n3, "value": n3 / (ms * 1e-3), "ms_per_step": ms,
-                                        "steps": steps, "result": v, "abs_err": abs(v - math.pi),
-                                        "n_per_gpu": n3 // ctx.world, "scaling": "strong"}
+                                        "steps": steps, "result": v, "abs_err": e,
+                                        "n_per_gpu": st.plan.count, "scaling": "strong",
+                                        "verified": result_ok("pi4", args.rule, "fp64", n3, e)}
         del st
-    # (4) BASELINE config #5: the 2-D field v(x) v(y) from the velocity profile, 4096^2
+    # (5) BASELINE config #5: the 2-D field v(x) v(y) from the velocity profile, 4096^2
     #     bilinear midpoint samples, sample rows split over the same GPUs; one integration =
     #     one fused kernel per rank, the partials of a 32-integration graph replay meeting in
-    #     one RCCL all-reduce (Table2DPlan)
-    if args.integrand == "pi4":
+    #     one RCCL all-reduce (Table2DPlan) on the shared communicator
+    if pi4:
         import torch
 
         from cuda_v_mpi_amd import native
-        from cuda_v_mpi_amd.parallel.dist import native_comm
 
         m = native()
         g = 4096
-        comm2 = native_comm(ctx) if (ctx.world > 1 or args.force_collective) else None
-        p2 = m.Table2DPlan(g, 1800.0, ctx.device, comm2, not args.no_bucket)
+        p2 = m.Table2DPlan(g, 1800.0, ctx.device, comm, not args.no_bucket)
         p2.run()
         p2.time(p2.graph_steps * 4, True)  # warm replays
         ms = p2.time(p2.graph_steps * 10, True)
@@ -487,39 +573,48 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
         ctx.all_reduce_max(t)
         ms = float(t.item())
         v, want = p2.last_result(), m.table2d_oracle(g)
+        rel = abs(v - want) / want
         out["baseline5_table2d_4096"] = {
             "grid": g, "samples": g * g, "ms_per_integration": ms,
             "samples_per_s": g * g / (ms * 1e-3), "result": v, "midpoint_oracle": want,
-            "rel_err_vs_oracle": abs(v - want) / want, "rows_this_rank": [p2.row0, p2.row1],
-            "bucketed_allreduce": bool(p2.bucketed), "n_gpus": ctx.world}
-        del p2, comm2
-    # (4b) BASELINE config #4: the same integral through the packed-fp32 path (fp64 tile
-    #      set-up and fold), its error against pi and against the fp64 headline value
-    if args.integrand == "pi4" and args.dtype == "fp64":
-        f32 = Integrator("pi4", n=n_total, div=args.div,
-                         **dict(kw, dtype="fp32"))
+            "rel_err_vs_oracle": rel, "rows_this_rank": [p2.row0, p2.row1],
+            "bucketed_allreduce": bool(p2.bucketed), "n_gpus": ctx.world,
+            "verified": bool(rel <= 1e-12)}
+        del p2
+    # (6) BASELINE config #4: the same integral through the packed-fp32 path. Samples are
+    #     evaluated in packed fp32; each 192-sample tile's value is folded into an fp64 lane
+    #     accumulator and the DPP/LDS reduction runs in fp64 ("accum": "fp64-fold": an fp32
+    #     fold biases the sum by -8e-9 relative at N = 1e9, riemann.cpp's Pi4F32 notes;
+    #     the all-fp32 variant is measured in profiles/r3/fp32_accum.jsonl)
+    if pi4 and args.dtype == "fp64":
+        f32 = Integrator("pi4", n=n_total, div=args.div, **dict(kw, dtype="fp32"))
         steps = 40
         ms = _timed_steps(ctx, f32.plan, steps, pipeline, dev)
         v = f32.plan.host_result(f32.plan.host_index_of(steps - 1, True))
         ref = integ.plan.host_result(integ.plan.host_index_of(0, True))
+        e, rd = abs(v - math.pi), abs(v - ref) / abs(ref)
         out["baseline4_fp32"] = {"value": n_total / (ms * 1e-3), "ms_per_step": ms,
-                                 "steps": steps, "result": v, "abs_err": abs(v - math.pi),
-                                 "rel_diff_vs_fp64": abs(v - ref) / abs(ref), "dtype": "fp32"}
+                                 "steps": steps, "result": v, "abs_err": e,
+                                 "rel_diff_vs_fp64": rd, "dtype": "fp32", "accum": "fp64-fold",
+                                 "verified": bool(rd <= 1e-9 and
+                                                  result_ok("pi4", args.rule, "fp32", n_total, e))}
         del f32
-    # (1) BASELINE config #1: the serial CPU sum at N = 1e6 (the reference's plumbing case),
+    # (7) BASELINE config #1: the serial CPU sum at N = 1e6 (the reference's plumbing case),
     #     on one host thread of the native host engine
-    if args.integrand == "pi4":
+    if pi4:
         from cuda_v_mpi_amd import native as _native
 
         mm = _native()
         c1 = Integrator("pi4", n=10**6, rule=args.rule, backend="host", threads=1)
         best1 = min(c1.run().seconds_device for _ in range(3))
         v1 = c1.run().value
+        e1 = abs(v1 - math.pi)
         out["baseline1_serial_cpu_1e6"] = {"N": 10**6, "value": 10**6 / best1,
-                                           "ms": best1 * 1e3, "result": v1,
-                                           "abs_err": abs(v1 - math.pi), "threads": 1,
-                                           "isa": mm.host_isa()}
-    # (5) the reference's own side of its CUDA-vs-MPI comparison: the same integral on this
+                                           "ms": best1 * 1e3, "result": v1, "abs_err": e1,
+                                           "threads": 1, "isa": mm.host_isa(),
+                                           "verified": result_ok("pi4", args.rule, "fp64",
+                                                                 10**6, e1)}
+    # (8) the reference's own side of its CUDA-vs-MPI comparison: the same integral on this
     #     node's host cores (native host engine, per-sample fp64 vector threads, each rank
     #     its slice with its share of the cores, best of 3, slowest rank)
     import torch
@@ -548,10 +643,12 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
     t = torch.tensor([best], dtype=torch.float64, device=dev)
     ctx.all_reduce_max(t)
     v = host.run().value
+    e = abs(v - host.spec.analytic())
     out["host_engine"] = {"value": n_total / float(t.item()), "ms": float(t.item()) * 1e3,
                           "ranks": ctx.world, "threads_per_rank": threads,
-                          "isa": m.host_isa(), "result": v,
-                          "abs_err": abs(v - host.spec.analytic())}
+                          "isa": m.host_isa(), "result": v, "abs_err": e,
+                          "verified": result_ok(args.integrand, args.rule, "fp64", n_total, e,
+                                                host.spec)}
     return out
 
 

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include "miint/common.hpp"
+#include "miint/fast_trig.hpp"
 
 namespace miint {
 
@@ -417,8 +418,71 @@ struct AngleSeries {
   }
 };
 
+// ------------------------------------------------------------------ per-sample trig tiles
+// kIeee tiles of Sin and TrainVel: every sample's own sin/cos by fast_trig.hpp (tile-shared
+// quadrant and Cody-Waite products, fdlibm kernels with the reduction tail), ocml per sample
+// for the tiles it declines. ANGLE maps the sample coordinate to the angle (identity for
+// sin, t / ts for the train); SHIFT 0 sums sin, 1 sums cos. Returns the signed sum over the
+// tile's U samples x0 + u h.
+template <int U, int SHIFT, class ANGLE, class LIB>
+__device__ __forceinline__ double trig_tile_sum(double x0, double h, const ANGLE& angle,
+                                                const LIB& lib) {
+  TrigTile q;
+  if (trig_tile(angle(x0), angle(fma(static_cast<double>(U - 1), h, x0)), SHIFT, q)) {
+    double a0 = 0.0, a1 = 0.0;
+    if (q.use_cos) {
+#pragma unroll
+      for (int u = 0; u < U; u += 2) {
+        a0 += trig_sample<true>(angle(fma(static_cast<double>(u), h, x0)), q);
+        a1 += trig_sample<true>(angle(fma(static_cast<double>(u + 1), h, x0)), q);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; u += 2) {
+        a0 += trig_sample<false>(angle(fma(static_cast<double>(u), h, x0)), q);
+        a1 += trig_sample<false>(angle(fma(static_cast<double>(u + 1), h, x0)), q);
+      }
+    }
+    const double t = a0 + a1;
+    return q.neg ? -t : t;
+  }
+  double acc0 = 0.0, acc1 = 0.0;  // library per sample (two chains keep 8 waves/SIMD)
+#pragma unroll 1
+  for (int u = 0; u < U; u += 2) {
+    acc0 += lib(angle(fma(static_cast<double>(u), h, x0)));
+    acc1 += lib(angle(fma(static_cast<double>(u + 1), h, x0)));
+  }
+  return acc0 + acc1;
+}
+// Sample u of a kIeee trig tile by exactly trig_tile_sum's operations (validation kernel).
+template <int U, int SHIFT, class ANGLE, class LIB>
+__device__ __forceinline__ double trig_tile_point(double x0, double h, int u, const ANGLE& angle,
+                                                  const LIB& lib) {
+  TrigTile q;
+  const double th = angle(fma(static_cast<double>(u), h, x0));
+  if (!trig_tile(angle(x0), angle(fma(static_cast<double>(U - 1), h, x0)), SHIFT, q))
+    return lib(th);
+  const double v = q.use_cos ? trig_sample<true>(th, q) : trig_sample<false>(th, q);
+  return q.neg ? -v : v;
+}
+struct IdentityAngle {
+  __device__ __forceinline__ double operator()(double x) const { return x; }
+};
+struct ScaledAngle {
+  double k;
+  __device__ __forceinline__ double operator()(double x) const { return x * k; }
+};
+struct OcmlSin {
+  __device__ __forceinline__ double operator()(double x) const { return sin(x); }
+};
+struct OcmlCos {
+  __device__ __forceinline__ double operator()(double x) const { return cos(x); }
+};
+
 // ------------------------------------------------------------------ sin(x), fp64
-// kIeee: ocml sin per sample (~53 VALU per sample measured, with its range reduction).
+// kIeee: every sample's own sin (trig_tile_sum: fast_trig.hpp per sample, ocml for tiles
+// it declines); SinLib keeps ocml sin for every sample (~56 VALU, with its range reduction:
+// the validation reference).
 // kSeries (default): AngleSeries<12> with w = 1 (192-sample tiles). Per point: absolute
 // error vs ocml sin <= 7.2e-16 measured (tests allow 4 ulp(1)); the sum agrees with the kIeee
 // path to 2e-15 relative. N = 1e9 on [0, pi]: 81.2 us per integration (1.23e13 subint/s,
@@ -449,6 +513,17 @@ struct Sin : TileDefaults<Sin>, AngleSeries<12> {
   }
   template <int U, DivMode>
   __device__ __forceinline__ double tile(double x0, double h) const {
+    return trig_tile_sum<U, 0>(x0, h, IdentityAngle{}, OcmlSin{});
+  }
+  template <int U>
+  __device__ __forceinline__ double ieee_point(double x0, double h, int u) const {
+    return trig_tile_point<U, 0>(x0, h, u, IdentityAngle{}, OcmlSin{});
+  }
+};
+// ocml sin for every sample (validation reference of the kIeee tile; set_trig_library).
+struct SinLib : Sin {
+  template <int U, DivMode>
+  __device__ __forceinline__ double tile(double x0, double h) const {
     // ocml sin is ~40 VALU ops with its own range reduction; unrolling it fully blows the
     // register budget (256 VGPRs -> 1 wave/SIMD), two independent chains keep 8 waves/SIMD.
     double acc0 = 0.0, acc1 = 0.0;
@@ -458,6 +533,15 @@ struct Sin : TileDefaults<Sin>, AngleSeries<12> {
       acc1 += sin(fma(static_cast<double>(u + 1), h, x0));
     }
     return acc0 + acc1;
+  }
+  template <int U, DivMode M>
+  __device__ __forceinline__ double tile_acc(double xa, double h, double acc) const {
+    static_assert(M != DivMode::kSeries, "SinLib is the kIeee reference");
+    return acc + tile<U, M>(xa, h);
+  }
+  template <int U>
+  __device__ __forceinline__ double ieee_point(double x0, double h, int u) const {
+    return sin(fma(static_cast<double>(u), h, x0));
   }
 };
 
@@ -616,6 +700,20 @@ struct TrainVel : TileDefaults<TrainVel>, AngleSeries<8> {
   __device__ __forceinline__ double series_point(double tm, int u) const {
     return (1.0 - point_of<true>(tm * inv_ts, u)) * vs;
   }
+  // kIeee: every sample's own cos(t / ts) (trig_tile_sum, shift 1); the tile value is
+  // vs (U - sum cos).
+  template <int U, DivMode>
+  __device__ __forceinline__ double tile(double x0, double h) const {
+    const double c = trig_tile_sum<U, 1>(x0, h, ScaledAngle{inv_ts}, OcmlCos{});
+    return fma(-vs, c, vs * static_cast<double>(U));
+  }
+  template <int U>
+  __device__ __forceinline__ double ieee_point(double x0, double h, int u) const {
+    return (1.0 - trig_tile_point<U, 1>(x0, h, u, ScaledAngle{inv_ts}, OcmlCos{})) * vs;
+  }
+};
+// ocml cos for every sample (validation reference of the kIeee tile; set_trig_library).
+struct TrainVelLib : TrainVel {
   template <int U, DivMode>
   __device__ __forceinline__ double tile(double x0, double h) const {
     double acc0 = 0.0, acc1 = 0.0;
@@ -625,6 +723,15 @@ struct TrainVel : TileDefaults<TrainVel>, AngleSeries<8> {
       acc1 += point(fma(static_cast<double>(u + 1), h, x0));
     }
     return acc0 + acc1;
+  }
+  template <int U, DivMode M>
+  __device__ __forceinline__ double tile_acc(double xa, double h, double acc) const {
+    static_assert(M != DivMode::kSeries, "TrainVelLib is the kIeee reference");
+    return acc + tile<U, M>(xa, h);
+  }
+  template <int U>
+  __device__ __forceinline__ double ieee_point(double x0, double h, int u) const {
+    return point(fma(static_cast<double>(u), h, x0));
   }
 };
 

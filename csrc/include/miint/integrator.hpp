@@ -35,6 +35,13 @@
 
 namespace miint {
 
+// Default number of concurrent step streams in a chained graph batch. One integration's
+// kernel spends ~2-3 us ramping up, draining and flushing; with consecutive steps on
+// different streams (independent: own partials, own result) the next step fills the CUs
+// the previous one's tail leaves idle. 1/8 of N = 1e9 on one MI355X: 11.5 us per step on
+// one stream, 10.0 on four (profiles/r3/stream_overlap.jsonl).
+constexpr int kAutoStepStreams = 4;
+
 struct RiemannConfig {
   Integrand integrand = Integrand::kPi4;
   double a = 0.0, b = 1.0;
@@ -61,6 +68,12 @@ struct RiemannConfig {
                                // torch.distributed path reduces results itself)
   bool force_collective = false;  // run the RCCL stage even with a 1-rank communicator
                                   // (exercises the multi-GPU graph path on one GPU)
+  int step_streams = 0;         // chained graph batches: steps dealt round-robin to this many
+                                // streams (each its own chain, ramp and tail of one step
+                                // overlapping the next one's work); 0 = auto (kAutoStepStreams)
+  int slice_rank = 0, slice_world = 0;  // > 0: integrate rank slice_rank's share of [0, n) over
+                                        // slice_world ranks whatever the communicator is (one-
+                                        // GPU rehearsal of a strong-scaled run's per-GPU work)
   double timeout_s = 300.0;    // collective watchdog in sync(); <= 0 disables
 };
 
@@ -155,6 +168,11 @@ class RiemannPlan {
  private:
   void enqueue_batch(hipStream_t cs, hipStream_t rs, int nsteps, bool overlap);
   void enqueue_chain(hipStream_t s, int nsteps) const;
+  void enqueue_chain_streams(hipStream_t cs, int nsteps);
+ public:
+  // Streams a chained batch of `nsteps` steps runs on (1 = the compute stream only).
+  int step_streams(int nsteps) const;
+ private:
   const Graph* batch_graph(int nsteps);  // captured lazily; null if capture failed
   bool use_graphs(bool requested, int steps);
   double* result_ptr(int j) const { return direct_ ? host_.device_ptr() + j : result_.get() + j; }
@@ -175,6 +193,8 @@ class RiemannPlan {
   PinnedBuffer<double> host_;
   Stream compute_;
   Stream comm_stream_;
+  std::vector<Stream> step_streams_;  // concurrent chains of a batch (step_streams() of them)
+  std::vector<std::unique_ptr<Event>> ev_step_join_;
   std::vector<std::unique_ptr<Event>> ev_computed_, ev_drained_;
   Event ev_fork_, ev_join_;
   Event ev_t0_, ev_t1_;

@@ -127,6 +127,9 @@ void launch_pi4_recip_narrow_f32(const float* d, uint64_t n, float* out, hipStre
 // Validation: when on, kIeee Pi4 launches run the library division everywhere (Pi4Wide,
 // Pi4F32Wide), so tests can check that the two give bitwise the same sums.
 void set_pi4_library_division(bool on);
+// Validation switch: kIeee sin (Sin) and cos (TrainVel) by ocml per sample instead of the
+// fast per-sample path (fast_trig.hpp). Process-wide; tests only.
+void set_trig_library(bool on);
 
 // Samples per lane tile of the kernel that launch_riemann_* would run for these arguments
 // (32; 64 or 128 on the series paths): host-side grid sizing.

@@ -274,6 +274,10 @@ template <> struct Maker<Sin> {
     return f;
   }
 };
+template <> struct Maker<SinLib> {
+  static constexpr int kLds = 1;
+  __device__ static SinLib make(const RiemannParams&, const double*, int, double*) { return {}; }
+};
 template <int NC> struct Maker<Poly<NC>> {
   static constexpr int kLds = 1;
   __device__ static Poly<NC> make(const RiemannParams& p, const double*, int, double*) {
@@ -287,6 +291,15 @@ template <> struct Maker<TrainVel> {
   __device__ static TrainVel make(const RiemannParams& p, const double*, int, double*) {
     TrainVel f;
     f.init_trig(p.trig);
+    f.inv_ts = 1.0 / p.p0;
+    f.vs = p.p1;
+    return f;
+  }
+};
+template <> struct Maker<TrainVelLib> {
+  static constexpr int kLds = 1;
+  __device__ static TrainVelLib make(const RiemannParams& p, const double*, int, double*) {
+    TrainVelLib f;
     f.inv_ts = 1.0 / p.p0;
     f.vs = p.p1;
     return f;
@@ -392,6 +405,7 @@ template <DivMode M, class F>
 constexpr bool occupancy_hint() {
   if constexpr (__is_same(F, Pi4)) return M == DivMode::kSeriesDirect;
   else if constexpr (__is_same(F, Pi4F32) || __is_same(F, Pi4F32Wide)) return M == DivMode::kIeee;
+  else if constexpr (__is_same(F, SinLib) || __is_same(F, TrainVelLib)) return true;
   else if constexpr (__is_same(F, Sin)) return M == DivMode::kIeee;
   else if constexpr (__is_same(F, PolyF32<16>)) return true;
   else if constexpr (IsPoly<F>::value) return M == DivMode::kSeries;
@@ -543,6 +557,10 @@ __global__ __launch_bounds__(B) void point_values_kernel(RiemannParams p, const 
       v = fma(sd.s, e + e * e, sd.s);
     } else if constexpr (M == DivMode::kIeee && __is_same(F, Pi4)) {
       v = full ? Pi4::recip_narrow(fma(x, x, 1.0)) : f.point(x);  // as Pi4::tile<U, kIeee>
+    } else if constexpr (M == DivMode::kIeee &&
+                         (__is_same(F, Sin) || __is_same(F, SinLib) ||
+                          __is_same(F, TrainVel) || __is_same(F, TrainVelLib))) {
+      v = full ? f.template ieee_point<T>(x0, p.h, u) : f.point(x);  // as F::tile<T, kIeee>
     } else {
       v = f.point(x);
     }
@@ -600,6 +618,8 @@ void launch_chained_t(const RiemannParams& p, LaunchShape shape, const double* t
 // kIeee Pi4 launches take Pi4::recip_narrow when both end coordinates (the extremes: x is
 // linear in the sample index) stay below kPi4NarrowMaxX in magnitude; NaN ends do not.
 std::atomic<bool> g_pi4_library_division{false};  // validation switch: always Pi4Wide
+std::atomic<bool> g_trig_library{false};  // validation switch: kIeee sin/cos by ocml per sample
+inline bool trig_library() { return g_trig_library.load(std::memory_order_relaxed); }
 inline bool pi4_narrow(const RiemannParams& p, double max_x = kPi4NarrowMaxX) {
   if (g_pi4_library_division.load(std::memory_order_relaxed)) return false;
   const double first = static_cast<double>(p.i_begin) + p.off;
@@ -654,6 +674,7 @@ void dispatch(const RiemannParams& p, DType dtype, DivMode m, A&&... a) {
       return;
     case Integrand::kSin:
       if (m == DivMode::kSeries) Op<DivMode::kSeries, Sin>::run(a...);
+      else if (trig_library()) Op<DivMode::kIeee, SinLib>::run(a...);
       else Op<DivMode::kIeee, Sin>::run(a...);
       return;
     case Integrand::kPoly:  // coefficient bucket (zero-padded): series 4, 6, 7, 8; Horner 4, 8, 16
@@ -668,6 +689,7 @@ void dispatch(const RiemannParams& p, DType dtype, DivMode m, A&&... a) {
       return;
     case Integrand::kTrainVel:
       if (m == DivMode::kSeries) Op<DivMode::kSeries, TrainVel>::run(a...);
+      else if (trig_library()) Op<DivMode::kIeee, TrainVelLib>::run(a...);
       else Op<DivMode::kIeee, TrainVel>::run(a...);
       return;
     case Integrand::kTable:
@@ -826,6 +848,7 @@ void launch_riemann_point_values(const RiemannParams& p, DivMode div, const doub
 }
 
 void set_pi4_library_division(bool on) { g_pi4_library_division.store(on); }
+void set_trig_library(bool on) { g_trig_library.store(on); }
 
 void launch_pi4_recip_narrow(const double* d, uint64_t n, double* out, hipStream_t stream) {
   if (n == 0) return;

@@ -6,11 +6,13 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <cmath>
 #include <cstdint>
 #include <string>
 
 #include "miint/comm.hpp"
 #include "miint/expr.hpp"
+#include "miint/fast_trig.hpp"
 #include "miint/host.hpp"
 #include "miint/integrator.hpp"
 #include "miint/kernels.hpp"
@@ -213,6 +215,9 @@ PYBIND11_MODULE(_miint, m) {
       .def_readwrite("rank", &RiemannConfig::rank)
       .def_readwrite("world", &RiemannConfig::world)
       .def_readwrite("force_collective", &RiemannConfig::force_collective)
+      .def_readwrite("step_streams", &RiemannConfig::step_streams)
+      .def_readwrite("slice_rank", &RiemannConfig::slice_rank)
+      .def_readwrite("slice_world", &RiemannConfig::slice_world)
       .def_readwrite("timeout_s", &RiemannConfig::timeout_s)
       .def_readwrite("host_direct", &RiemannConfig::host_direct)
       .def_readwrite("chain", &RiemannConfig::chain);
@@ -223,6 +228,7 @@ PYBIND11_MODULE(_miint, m) {
       .def_property_readonly("device", &RiemannPlan::device)
       .def_property_readonly("rank", &RiemannPlan::rank)
       .def_property_readonly("world", &RiemannPlan::world)
+      .def("step_streams", &RiemannPlan::step_streams, py::arg("nsteps"))
       .def_property_readonly("begin", &RiemannPlan::begin)
       .def_property_readonly("count", &RiemannPlan::count)
       .def_property_readonly("h", &RiemannPlan::h)
@@ -299,6 +305,28 @@ PYBIND11_MODULE(_miint, m) {
   });
   m.def("launch_pi4_recip_narrow_f32", [](uintptr_t d, uint64_t n, uintptr_t out, uintptr_t s) {
     launch_pi4_recip_narrow_f32(ptr<const float>(d), n, ptr<float>(out), stream(s));
+  });
+  m.def("set_trig_library", &set_trig_library, py::arg("on"),
+        "validation: kIeee sin/cos by ocml per sample (SinLib / TrainVelLib)");
+  m.def("fast_trig_host", [](uintptr_t x, uint64_t n, int shift, uintptr_t val, uintptr_t ulp) {
+    // the device's per-sample sin/cos (fast_trig.hpp, compiled for the host) and its error in
+    // ulps against long double sinl/cosl; NaN value/ulp where the tile path declines
+    const double* xs = reinterpret_cast<const double*>(x);
+    double* v = reinterpret_cast<double*>(val);
+    double* e = reinterpret_cast<double*>(ulp);
+    for (uint64_t i = 0; i < n; ++i) {
+      double out;
+      if (!fast_trig_point(xs[i], shift, out)) {
+        v[i] = e[i] = std::nan("");
+        continue;
+      }
+      const long double ref = shift ? cosl(static_cast<long double>(xs[i]))
+                                    : sinl(static_cast<long double>(xs[i]));
+      const double rd = static_cast<double>(ref);
+      const double sp = std::nextafter(std::fabs(rd), INFINITY) - std::fabs(rd);
+      v[i] = out;
+      e[i] = static_cast<double>((static_cast<long double>(out) - ref) / sp);
+    }
   });
   m.def("set_pi4_library_division", &set_pi4_library_division,
         "validation: kIeee Pi4 launches use the full library division (bitwise the same sums)");

@@ -33,7 +33,12 @@ RiemannPlan::RiemannPlan(const RiemannConfig& cfg, int device, const Comm* comm)
   params_.a = cfg.a;
   params_.h = (cfg.b - cfg.a) / static_cast<double>(cfg.n);
   params_.off = rule_offset(cfg.rule);
-  rank_slice(cfg.n, rank_, world_, &params_.i_begin, &params_.n);
+  if (cfg.slice_world > 0) {
+    MIINT_CHECK(cfg.slice_rank >= 0 && cfg.slice_rank < cfg.slice_world, "bad slice rank");
+    rank_slice(cfg.n, cfg.slice_rank, cfg.slice_world, &params_.i_begin, &params_.n);
+  } else {
+    rank_slice(cfg.n, rank_, world_, &params_.i_begin, &params_.n);
+  }
   params_.integrand = static_cast<int>(cfg.integrand);
   params_.ncoef = static_cast<int>(cfg.coef.size());
   MIINT_CHECK(cfg.coef.size() <= static_cast<size_t>(kMaxPolyCoeffs), "too many coefficients");
@@ -67,7 +72,14 @@ RiemannPlan::RiemannPlan(const RiemannConfig& cfg, int device, const Comm* comm)
     shape_.grid = static_cast<int>(g);
   }
 
-  partials_ = DeviceBuffer<double>(2 * static_cast<size_t>(shape_.grid));
+  // chained batches: two partial halves per step stream
+  const int lanes = step_streams(cfg.slots);
+  partials_ = DeviceBuffer<double>(2 * static_cast<size_t>(std::max(1, lanes)) *
+                                   static_cast<size_t>(shape_.grid));
+  for (int l = 1; l < lanes; ++l) {
+    step_streams_.emplace_back();
+    ev_step_join_.emplace_back(new Event(false));
+  }
   slots_ = DeviceBuffer<double>(static_cast<size_t>(shape_.grid));
   fill_unset_slots(slots_.get(), slots_.size(), nullptr);
   result_ = DeviceBuffer<double>(static_cast<size_t>(cfg.slots));
@@ -91,6 +103,7 @@ RiemannPlan::~RiemannPlan() {
   (void)hipSetDevice(device_);
   (void)hipStreamSynchronize(compute_.get());
   (void)hipStreamSynchronize(comm_stream_.get());
+  for (const auto& s : step_streams_) (void)hipStreamSynchronize(s.get());
 }
 
 DivMode RiemannPlan::effective_div() const {
@@ -160,9 +173,50 @@ void RiemannPlan::enqueue_chain(hipStream_t s, int nsteps) const {
                   result_ptr(nsteps - 1), s);
 }
 
+int RiemannPlan::step_streams(int nsteps) const {
+  if (!chained()) return 1;
+  const int want = cfg_.step_streams > 0 ? cfg_.step_streams : kAutoStepStreams;
+  return std::max(1, std::min(want, nsteps));
+}
+
+// Chained batch over L streams: step j runs on stream j % L (the compute stream is stream 0)
+// as step j / L of that stream's own chain, with its own two partial halves; every chain
+// closes with a finalize, and the compute stream joins all of them. The steps are
+// independent integrations, so kernels on different streams may overlap (one's ramp and
+// tail under another's work); each result is computed exactly as on one stream.
+void RiemannPlan::enqueue_chain_streams(hipStream_t cs, int nsteps) {
+  const int L = std::min(step_streams(nsteps), 1 + static_cast<int>(step_streams_.size()));
+  if (L <= 1) {
+    enqueue_chain(cs, nsteps);
+    return;
+  }
+  const int g = shape_.grid;
+  const int tn = static_cast<int>(cfg_.table.size());
+  auto lane = [&](int l) { return l == 0 ? cs : step_streams_[static_cast<size_t>(l - 1)].get(); };
+  auto half = [&](int l, int jj) {
+    return partials_.get() + (2 * static_cast<size_t>(l) + static_cast<size_t>(jj & 1)) * g;
+  };
+  ev_fork_.record(cs);
+  for (int l = 1; l < L; ++l) MIINT_HIP(hipStreamWaitEvent(lane(l), ev_fork_.get(), 0));
+  for (int j = 0; j < nsteps; ++j) {
+    const int l = j % L, jj = j / L;
+    launch_riemann_chained(params_, cfg_.dtype, cfg_.div, shape_, table_.get(), tn, half(l, jj),
+                           jj ? half(l, jj - 1) : nullptr, g, scale_,
+                           jj ? result_ptr(j - L) : nullptr, lane(l));
+  }
+  for (int l = 0; l < L && l < nsteps; ++l) {
+    const int last = l + ((nsteps - 1 - l) / L) * L;  // the chain's last step
+    launch_finalize(half(l, last / L), g, scale_, result_ptr(last), lane(l));
+    if (l > 0) {
+      ev_step_join_[static_cast<size_t>(l - 1)]->record(lane(l));
+      MIINT_HIP(hipStreamWaitEvent(cs, ev_step_join_[static_cast<size_t>(l - 1)]->get(), 0));
+    }
+  }
+}
+
 void RiemannPlan::enqueue_batch(hipStream_t cs, hipStream_t rs, int nsteps, bool overlap) {
   if (chained()) {
-    enqueue_chain(cs, nsteps);
+    enqueue_chain_streams(cs, nsteps);
     if (bucketed()) {  // one all-reduce + one copy of all the batch's results
       comm_->allreduce_sum(result_.get(), result_.get(), static_cast<size_t>(nsteps), cs);
       MIINT_HIP(hipMemcpyAsync(host_.get(), result_.get(), sizeof(double) * nsteps,

@@ -69,7 +69,8 @@ class Integrator:
                  backend: str = "hip", ctx: DistContext | None = None, comm: str = "native",
                  fused: bool = True, grid: int = 0, slots: int = 16, a: float | None = None,
                  b: float | None = None, force_collective: bool = False, bucket: bool = True,
-                 chain: bool = True, comm_obj=None, threads: int = 0, **spec_kw):
+                 chain: bool = True, comm_obj=None, threads: int = 0,
+                 slice_of: tuple[int, int] | None = None, step_streams: int = 0, **spec_kw):
         spec = integrands.get(integrand, **spec_kw) if isinstance(integrand, str) else integrand
         if a is not None or b is not None:
             spec = dataclasses.replace(spec, a=spec.a if a is None else a,
@@ -110,6 +111,9 @@ class Integrator:
             cfg.force_collective = force_collective
             cfg.bucket = bucket
             cfg.chain = chain
+            cfg.step_streams = step_streams
+            if slice_of is not None:  # (rank, world): that rank's share, on this device
+                cfg.slice_rank, cfg.slice_world = int(slice_of[0]), int(slice_of[1])
             self._m = m
             if backend == "host":
                 self._cfg = cfg

@@ -6,6 +6,12 @@ communicator come out of it:
   * a native RCCL communicator owned by the C++ runtime (``_miint.Comm``), bootstrapped with
     a unique id that rank 0 publishes through the torch.distributed store. The native one is
     what the Riemann plans capture into hipGraphs together with their kernels.
+
+A rank whose data plane is the native communicator keeps ONE RCCL communicator: its torch
+process group is gloo (``control_backend``), which carries only the control plane (flags,
+scalar gathers, barriers) on host tensors. A torch RCCL group is created only on demand
+(``DistContext.nccl_group``: the torch.distributed step path) and counted in
+``DistContext.nccl_groups`` so a run record can show how many the rank built.
 """
 from __future__ import annotations
 
@@ -25,10 +31,30 @@ class DistContext:
     device: int = 0
     backend: str = "none"
     initialized_here: bool = False
+    nccl_groups: int = 0  # torch RCCL process groups this rank created (default one included)
+    _nccl: object = None
 
     @property
     def is_root(self) -> bool:
         return self.rank == 0
+
+    @property
+    def host_collectives(self) -> bool:
+        """Control-plane collectives take host tensors (gloo) rather than device ones."""
+        return self.backend != "nccl"
+
+    def control_device(self) -> str:
+        return "cpu" if self.host_collectives else "cuda"
+
+    def nccl_group(self):
+        """The torch RCCL group for device-tensor collectives: the default group when it is
+        nccl, else one created here on first use (every rank must call this together)."""
+        if self.world == 1 or self.backend == "nccl":
+            return None  # default group
+        if self._nccl is None:
+            self._nccl = dist.new_group(backend="nccl")
+            self.nccl_groups += 1
+        return self._nccl
 
     def barrier(self) -> None:
         if self.world > 1 and dist.is_initialized():
@@ -94,9 +120,21 @@ def init(backend: str | None = None, timeout_s: float = 300.0, force: bool = Fal
             dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                     timeout=datetime.timedelta(seconds=timeout_s), **kw)
             ctx.initialized_here = True
+            ctx.nccl_groups = int(backend == "nccl")
     else:
         ctx.backend = backend if dist.is_initialized() else "none"
     return ctx
+
+
+def control_backend(data_plane: str, device: str = "gpu") -> str:
+    """Process-group backend for a rank whose collectives go through ``data_plane``.
+
+    ``native``: the C++ RCCL communicator carries every device collective, so the torch group
+    is gloo (control plane only: one RCCL communicator per rank, not two). ``torch``: the
+    torch group itself is the data plane, nccl on a GPU. CPU runs are gloo either way."""
+    if device == "cpu":
+        return "gloo"
+    return "gloo" if data_plane == "native" else "nccl"
 
 
 _uid_counter = [0]

@@ -5,9 +5,11 @@ The reference measures its decomposition by re-running ``mpirun -np P`` by hand
 every GPU count the node has,
 
   * ``bench.py --gpus N`` (one process per GPU, spawned by bench.py itself; RCCL over xGMI):
-    the weak-scaling headline (1e9 samples per GPU) and, from the same run, BASELINE #3's
-    strong-scaling point (N = 1e10 in total over the N GPUs) and BASELINE #5's 2-D field
-    (4096^2 samples in total, rows split over the N GPUs);
+    the weak-scaling headline (1e9 samples per GPU) and, from the same run, the metric's own
+    fixed-N point (``strong_1e9``: N = 1e9 in total over the N GPUs, as the reference splits
+    its fixed STEPS over its workers, riemann.cpp:10,71-73), BASELINE #3's strong-scaling
+    point (N = 1e10 in total) and BASELINE #5's 2-D field (4096^2 samples in total, rows
+    split over the N GPUs);
   * ``miint comm --gpus N`` (one process driving N GPUs, ncclCommInitAll): all-reduce and
     all-gather latency at 8 B (the Riemann payload, riemann.cpp:76) and 144 MB (4main.c:157's
     broadcast table),
@@ -101,6 +103,11 @@ def sweep(counts: list[int], steps: int = 200, warmup: int = 10, comm: bool = Tr
             "graphs": b["config"]["graphs"],
             "verified": b["verified"],
         }
+        s1 = b.get("strong_1e9")
+        if s1:
+            row["strong_1e9_value"] = s1["value"]
+            row["strong_1e9_ms"] = s1["ms_per_step"]
+            row["strong_1e9_verified"] = s1.get("verified")
         s = b.get("baseline3_strong_1e10")
         if s:
             row["strong_1e10_value"] = s["value"]
@@ -117,6 +124,8 @@ def sweep(counts: list[int], steps: int = 200, warmup: int = 10, comm: bool = Tr
             continue
         n = r["n_gpus"]
         r["weak_eff"] = r["value"] / (n * base["value"])
+        if "strong_1e9_value" in r and "strong_1e9_value" in base:  # the metric's own N
+            r["strong_1e9_eff"] = r["strong_1e9_value"] / (n * base["strong_1e9_value"])
         if "strong_1e10_value" in r and "strong_1e10_value" in base:
             r["strong_eff"] = r["strong_1e10_value"] / (n * base["strong_1e10_value"])
         if "t2d_4096_us" in r and "t2d_4096_us" in base:  # fixed total work: strong
@@ -125,7 +134,8 @@ def sweep(counts: list[int], steps: int = 200, warmup: int = 10, comm: bool = Tr
 
 
 def markdown(rows: list[dict]) -> str:
-    cols = ["n_gpus", "value", "ms_per_step", "weak_eff", "strong_1e10_value", "strong_eff",
+    cols = ["n_gpus", "value", "ms_per_step", "weak_eff", "strong_1e9_value", "strong_1e9_ms",
+            "strong_1e9_eff", "strong_1e10_value", "strong_eff",
             "t2d_4096_us", "t2d_strong_eff", "per_rank_spread_ms", "rccl_world", "allreduce_8B_us", "allgather_8B_us",
             "allreduce_144MB_us", "allgather_144MB_us"]
     out = ["| " + " | ".join(cols) + " |", "|" + "---|" * len(cols)]

@@ -23,7 +23,7 @@ from .dist import DistContext
 class TorchStepper:
     def __init__(self, spec: IntegrandSpec, n_total: int, ctx: DistContext, rule: str = "left",
                  dtype: str = "fp64", div: str = "series", grid: int | None = None,
-                 capacity: int = 4096):
+                 capacity: int = 4096, group=None):
         self.spec, self.n, self.ctx = spec, int(n_total), ctx
         self.rule, self.dtype, self.div = rule, dtype, div
         self.begin, self.count = rank_slice(self.n, ctx.rank, ctx.world)
@@ -31,6 +31,9 @@ class TorchStepper:
         self.ws = kernels.FusedWorkspace(grid or kernels.default_grid(), dev)
         self.out = torch.zeros(capacity, dtype=torch.float64, device=dev)
         self._works = []
+        # None = the default process group (nccl, or gloo on CUDA tensors for ranks that
+        # share a device); a gloo control-plane rank passes ctx.nccl_group()
+        self.group = group
 
     def launch_steps(self, steps: int) -> None:
         self._works = []
@@ -44,7 +47,7 @@ class TorchStepper:
             kernels.riemann(self.spec, self.n, rule=self.rule, dtype=self.dtype, div=self.div,
                             i_begin=self.begin, n_local=self.count, out=row, workspace=self.ws)
             if self.ctx.world > 1:
-                self._works.append(dist.all_reduce(row, async_op=True))
+                self._works.append(dist.all_reduce(row, group=self.group, async_op=True))
 
     def sync(self) -> None:
         for w in self._works:

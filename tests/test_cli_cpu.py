@@ -113,6 +113,7 @@ def test_scale_sweep_rows_and_efficiency(monkeypatch):
         "value": fake[n], "ms_per_step": 0.075, "per_rank_spread_ms": 0.001,
         "rccl_world": n if n > 1 else None, "config": {"graphs": True}, "verified": True,
         "baseline3_strong_1e10": {"value": fake[n] * 1.05, "ms_per_step": 0.7},
+        "strong_1e9": {"value": fake[n] * 0.9, "ms_per_step": 0.08, "verified": True},
         "baseline5_table2d_4096": {"ms_per_integration": 0.009 / n ** 0.8}})
     monkeypatch.setattr(scaling, "run_comm", lambda n: {"allreduce_8B_us": 10.0 * n})
     rows = scaling.sweep([1, 2, 4, 8])
@@ -120,6 +121,7 @@ def test_scale_sweep_rows_and_efficiency(monkeypatch):
     assert rows[2]["skipped"] == "only 2 devices" and rows[3]["skipped"] == "only 2 devices"
     assert rows[0]["weak_eff"] == 1.0 and abs(rows[1]["weak_eff"] - 0.95) < 1e-12
     assert abs(rows[1]["strong_eff"] - 0.95) < 1e-12
+    assert rows[0]["strong_1e9_eff"] == 1.0 and abs(rows[1]["strong_1e9_eff"] - 0.95) < 1e-12
     assert abs(rows[1]["t2d_4096_us"] - 9.0 / 2 ** 0.8) < 1e-9
     assert abs(rows[1]["t2d_strong_eff"] - 2 ** 0.8 / 2) < 1e-12
     md = scaling.markdown(rows)
@@ -158,3 +160,41 @@ def test_bench_driver_launch_form_json_contract():
     assert js["metric"].startswith("Riemann subintervals/sec at N=1e9 fp64")
     assert js["ms_per_step"] == pytest.approx(max(js["per_rank_ms"]))
     assert js["value"] == pytest.approx(js["config"]["N"] * 3 / (js["ms_per_step"] * 3e-3))
+
+
+def test_bench_native_ranks_build_no_torch_rccl_group():
+    """One RCCL communicator per rank: with --comm native (the default) the torch process
+    group is the gloo control plane and no torch nccl group is ever created; the native
+    communicator is the rank's only RCCL one. CPU form, 3 ranks (gloo everywhere; the record
+    states the control plane and counts torch RCCL groups)."""
+    from cuda_v_mpi_amd.parallel import dist as mdist
+
+    assert mdist.control_backend("native", "gpu") == "gloo"
+    assert mdist.control_backend("torch", "gpu") == "nccl"
+    assert mdist.control_backend("native", "cpu") == "gloo"
+    p = _bench("--gpus", "3", "--device", "cpu", "--samples", "3e4", "--steps", "2",
+               "--warmup", "1", "--settle-ms", "0")
+    assert p.returncode == 0, p.stderr[-3000:]
+    js = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert js["n_gpus"] == 3 and js["control_plane"] == "gloo"
+    assert js["torch_nccl_groups"] == 0
+    assert js["verified"] and js["headline_verified"]
+
+
+def test_bench_verification_bounds():
+    """The record's pass/fail rules: 4/(1+x^2) truncation per rule in closed form, fp32 at
+    2h, and a wrong value fails."""
+    sys.path.insert(0, REPO)
+    import bench
+
+    h = 1e-9
+    assert bench.result_ok("pi4", "left", "fp64", 10**9, 1.000000082740371e-09)
+    assert bench.result_ok("pi4", "left", "fp64", 10**10, 1.000000082740371e-10)
+    assert bench.result_ok("pi4", "left", "fp64", 10**6, 9.999998336063243e-07)  # h - h^2/6
+    assert not bench.result_ok("pi4", "left", "fp64", 10**9, 1.2e-9)
+    assert not bench.result_ok("pi4", "left", "fp64", 10**9, 0.0)
+    assert bench.result_ok("pi4", "mid", "fp64", 10**9, 4e-16)
+    assert not bench.result_ok("pi4", "mid", "fp64", 10**9, 1e-12)
+    assert bench.result_ok("pi4", "left", "fp32", 10**9, 1.0195799760026603e-09)
+    assert not bench.result_ok("pi4", "left", "fp32", 10**9, 3 * h)
+    assert not bench.result_ok("pi4", "left", "fp64", 10**9, float("nan"))

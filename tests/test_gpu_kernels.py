@@ -646,3 +646,67 @@ def test_pi4_fp32_ieee_tiles_equal_library_division(native, cuda, n):
     far = integrands.IntegrandSpec("pi4", 1e16, 2e16)
     got = float(kernels.riemann(far, 4097, rule="mid", dtype="fp32", div="ieee").item())
     assert got == pytest.approx(far.analytic(), rel=1e-5)
+
+
+# ------------------------------------------------------------------ per-sample sin / cos
+def _ulp_diff(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    sp = torch.nextafter(b.abs(), torch.full_like(b, math.inf)) - b.abs()
+    return ((a - b) / sp).abs()
+
+
+def _trig_windows(spec, n):
+    w = 1 << 16
+    return [0, n // 4 - w // 2, n // 2, 3 * n // 4 - w // 2, n - w]
+
+
+@pytest.mark.parametrize("a,b", [(0.0, math.pi), (1e5 - 1.0, 1e5), (-3.0, 40.0)])
+def test_sin_ieee_fast_within_one_ulp_of_ocml(native, cuda, a, b):
+    """kIeee sin per sample (fast_trig.hpp: tile-shared quadrant, Cody-Waite with tail,
+    fdlibm kernels) against ocml sin (SinLib, the set_trig_library reference) on dense 64 K
+    windows at N = 1e9: within 1 ulp everywhere, and the sums agree."""
+    spec = integrands.IntegrandSpec("sin", a, b)
+    n = 10**9
+    fast = [kernels.point_values(spec, n, div="ieee", i_begin=i, n_local=1 << 16)
+            for i in _trig_windows(spec, n)]
+    s_fast = float(kernels.riemann(spec, 10**8, rule="mid", div="ieee").item())
+    native.set_trig_library(True)
+    try:
+        lib = [kernels.point_values(spec, n, div="ieee", i_begin=i, n_local=1 << 16)
+               for i in _trig_windows(spec, n)]
+        s_lib = float(kernels.riemann(spec, 10**8, rule="mid", div="ieee").item())
+    finally:
+        native.set_trig_library(False)
+    for f, l in zip(fast, lib):
+        assert float(_ulp_diff(f, l).max()) <= 1.0
+    assert s_fast == pytest.approx(s_lib, rel=1e-14, abs=1e-15)
+    assert s_fast == pytest.approx(math.cos(a) - math.cos(b), abs=1e-9)
+
+
+def test_train_ieee_fast_matches_ocml(native, cuda):
+    """kIeee train velocity (1 - cos(t / ts)) vs per sample (shift-1 fast cos vs ocml cos):
+    every point within 2 ulp(1) * vs, the sums to 1e-14."""
+    spec = integrands.train()
+    n = 10**9
+    fast = [kernels.point_values(spec, n, div="ieee", i_begin=i, n_local=1 << 16)
+            for i in _trig_windows(spec, n)]
+    s_fast = float(kernels.riemann(spec, 10**8, rule="mid", div="ieee").item())
+    native.set_trig_library(True)
+    try:
+        lib = [kernels.point_values(spec, n, div="ieee", i_begin=i, n_local=1 << 16)
+               for i in _trig_windows(spec, n)]
+        s_lib = float(kernels.riemann(spec, 10**8, rule="mid", div="ieee").item())
+    finally:
+        native.set_trig_library(False)
+    for f, l in zip(fast, lib):
+        assert float((f - l).abs().max()) <= 2 * 2.0**-52 * spec.p1
+    assert s_fast == pytest.approx(s_lib, rel=1e-14)
+    assert s_fast == pytest.approx(spec.analytic(), rel=1e-9)
+
+
+def test_sin_ieee_fallback_tiles(cuda):
+    """Tiles the fast path declines (|x| beyond ~1.03e5, quadrant edges inside a tile) run
+    ocml per sample: the sum over a domain that needs both is still the torch fp64 sum."""
+    for a, b in ((2e5, 2e5 + 50.0), (1e5 - 30.0, 1e5 + 30.0)):
+        spec = integrands.IntegrandSpec("sin", a, b)
+        got = float(kernels.riemann(spec, 1_000_003, rule="mid", div="ieee").item())
+        assert got == pytest.approx(_ref_sum(spec, 1_000_003, rule="mid"), rel=1e-12, abs=1e-12)

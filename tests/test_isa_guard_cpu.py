@@ -1,0 +1,59 @@
+"""ISA / resource regression guard (tools/isa_guard.py) on the CPU box: the hot gfx950
+kernels are compiled device-only to assembly and compared with tools/isa_baseline.json —
+hot-loop VALU (+3 % fails), scratch, waves per SIMD. The per-sample loop these kernels
+replace is riemann.cpp:34-41; their speed rests on the exact allocation pinned here."""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tools"))
+
+import isa_guard  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def measured():
+    if not os.path.exists(isa_guard.HIPCC):
+        pytest.skip("hipcc not available")
+    return isa_guard.measure()
+
+
+def test_baseline_covers_every_guarded_kernel():
+    with open(isa_guard.BASELINE) as f:
+        base = json.load(f)
+    assert set(base) == set(isa_guard.GUARDED)
+    for k, v in base.items():
+        assert "missing" not in v, k
+        assert v["occupancy"] >= 4 and v["hot_loop_valu"] > 0, k
+
+
+def test_no_isa_regression(measured):
+    with open(isa_guard.BASELINE) as f:
+        base = json.load(f)
+    assert isa_guard.compare(base, measured) == []
+
+
+def test_headline_kernel_shape(measured):
+    """The headline kernel itself: 8 waves/SIMD, no scratch, one 192-sample series tile in
+    <= 2.7 VALU per sample (integrands.hpp Pi4: 508 per tile)."""
+    k = measured["pi4_series"]
+    assert k["occupancy"] == 8 and k["scratch"] == 0
+    assert k["vgpr"] <= 64 and k["sgpr"] <= 96
+    assert k["valu_per_sample"] <= 2.7
+
+
+def test_guard_flags_a_regression():
+    base = {"k": {"occupancy": 8, "scratch": 0, "hot_loop_valu": 100,
+                  "hot_loop_scratch_ops": 0, "max_block_valu": 50}}
+    ok = {"k": {"occupancy": 8, "scratch": 0, "hot_loop_valu": 103, "hot_loop_scratch_ops": 0,
+                "max_block_valu": 51}}
+    assert isa_guard.compare(base, ok) == []
+    for bad in ({"hot_loop_valu": 104}, {"occupancy": 7}, {"scratch": 16},
+                {"hot_loop_scratch_ops": 2}, {"max_block_valu": 52}):
+        now = {"k": dict(ok["k"], **bad)}
+        assert len(isa_guard.compare(base, now)) == 1, bad

@@ -14,10 +14,22 @@ mkdir -p gpurun_out
 # the GPU and exec'ing make/sh from it is refused on this pool.
 # (build/obj is not shipped to the box, so `make -q` alone always reports stale objects: the
 # in-tree extension and CLIs count as current when no source or build file is newer.)
+# Every shipped artifact is checked on its own against the sources it is built from: `make
+# ext` refreshes the .so but not the CLIs, so a source newer than ANY of them means a rebuild
+# (miintrun is built from its one file only).
+newer_src() {  # artifact, sources... -> true if a source is newer than the artifact
+  local a="$1"; shift
+  [ -n "$(find "$@" -newer "$a" -type f -print -quit)" ]
+}
 built_ok() {
-  local so; so=$(ls cuda_v_mpi_amd/_miint*.so 2>/dev/null | head -n 1)
-  [ -n "$so" ] && [ -x build/bin/miint ] && [ -x build/bin/miintrun ] || return 1
-  [ -z "$(find csrc Makefile -newer "$so" -type f -print -quit)" ]
+  local so a; so=$(ls cuda_v_mpi_amd/_miint*.so 2>/dev/null | head -n 1)
+  [ -n "$so" ] && [ -x build/bin/miintrun ] || return 1
+  for a in "$so" build/bin/riemann build/bin/cintegrate build/bin/trainscan build/bin/miint; do
+    [ -e "$a" ] || return 1
+    newer_src "$a" csrc/include csrc/kernels csrc/runtime csrc/python csrc/cli Makefile && return 1
+  done
+  newer_src build/bin/miintrun csrc/cli/miintrun.cpp && return 1
+  return 0
 }
 if ! built_ok && ! make -q all >/dev/null 2>&1; then
   echo "=== build out of date: make -j16 all" | tee -a gpurun_out/session.txt

@@ -93,7 +93,8 @@ def parse(argv=None) -> argparse.Namespace:
     p.add_argument("--slots", type=int, default=48,
                    help="steps per captured graph batch (= steps per bucketed all-reduce)")
     p.add_argument("--step-streams", type=int, default=0,
-                   help="streams a chained graph batch deals its steps over (0 = auto: 4)")
+                   help="streams a chained graph batch deals its steps over (0 = auto: 4 below "
+                        "6e8 samples per GPU per step, else 1)")
     p.add_argument("--no-bucket", action="store_true",
                    help="one all-reduce per step instead of one per graph batch of steps")
     p.add_argument("--force-collective", action="store_true",

@@ -35,6 +35,7 @@ struct BenchRow {
   std::string integrand, dtype, rule;
   double n = 0, result = 0, exact = 0, ms = 0;
   int gpus = 1;
+  int block = 0, grid = 0;  // launch shape of rank 0's plan
 };
 
 Integrand integrand_of(const std::string& s) { return cli::parse_integrand(s); }
@@ -74,7 +75,11 @@ BenchRow bench_one(const cli::Topology& topo, RiemannConfig cfg, int iters, bool
     std::lock_guard<std::mutex> g(mu);
     const double ms = t.wall_s * 1e3 / iters;
     if (ms > row.ms) row.ms = ms;  // slowest rank
-    if (rank == topo.rank0) row.result = plan.host_result(plan.host_index_of(iters - 1, graphs));
+    if (rank == topo.rank0) {
+      row.result = plan.host_result(plan.host_index_of(iters - 1, graphs));
+      row.block = plan.shape().block;
+      row.grid = plan.shape().grid;
+    }
   });
   return row;
 }
@@ -87,6 +92,8 @@ void print_row(const cli::Args& a, const BenchRow& r, const char* integ, const c
                    .add("rule", rule)
                    .add("n", r.n)
                    .add("gpus", r.gpus)
+                   .add("block", r.block)
+                   .add("grid", r.grid)
                    .add("ms_per_integration", r.ms)
                    .add("subintervals_per_s", r.n / (r.ms * 1e-3))
                    .add("result", r.result)
@@ -224,6 +231,9 @@ int main(int argc, char** argv) {
                                  a.str("rule", "left"), a.str("div", "series"));
       c.fused = !a.flag("unfused");
       c.grid = static_cast<int>(a.integer("grid", 0));
+      c.block = static_cast<int>(a.integer("block", kRiemannBlock));
+      c.step_streams = static_cast<int>(a.integer("step-streams", 0));
+      MIINT_CHECK(riemann_block_ok(c.block), "--block must be 64, 128, 256, 512 or 1024");
       c.waves_per_cu = static_cast<int>(a.integer("waves-per-cu", 32));
       const BenchRow r = bench_one(topo, c, iters, graphs);
       if (topo.rank0 == 0)

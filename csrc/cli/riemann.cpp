@@ -20,7 +20,8 @@
 // host cores instead (HostExpr). --analytic V adds the error vs V.
 //
 //   ./riemann [--n 1e9] [--gpus G] [--integrand sin|pi4|poly|train] [--rule left|mid]
-//             [--dtype fp64|fp32] [--iters K] [--parity] [--json] [--jsonl FILE]
+//             [--dtype fp64|fp32] [--iters K] [--block 64..1024] [--grid G] [--parity]
+//             [--json] [--jsonl FILE]
 //             [--device cpu [--threads T] [--ranks P]] [--expr EXPR --a A --b B [--analytic V]]
 #include <algorithm>
 #include <cmath>
@@ -221,6 +222,11 @@ int main(int argc, char** argv) {
     cfg.dtype = a.str("dtype", "fp64") == "fp32" ? DType::kF32 : DType::kF64;
     cfg.div = a.str("div", "series") == "ieee" ? DivMode::kIeee : DivMode::kSeries;
     cfg.fused = !a.flag("unfused");
+    // --block: threads per workgroup (the reference's SP, cintegrate.cu:17-18); --grid:
+    // workgroups (its SM), 0 = auto
+    cfg.block = static_cast<int>(a.integer("block", kRiemannBlock));
+    cfg.grid = static_cast<int>(a.integer("grid", 0));
+    MIINT_CHECK(riemann_block_ok(cfg.block), "--block must be 64, 128, 256, 512 or 1024");
     if (f == Integrand::kTrainVel) { cfg.p0 = oracle::kTrainTs; cfg.p1 = oracle::kTrainVs; }
     if (f == Integrand::kTable) cfg.table = prof;
     if (f == Integrand::kPoly) cfg.coef = {1.0, -0.5, 0.25, 0.125};
@@ -230,6 +236,7 @@ int main(int argc, char** argv) {
     const cli::Topology topo = cli::topology(a);
 
     double result = 0.0, dev_ms = 0.0;
+    LaunchShape launch_shape{0, cfg.block};
     if (a.flag("parity")) {
       // riemann.cpp:65-86 numerics on the GPU: P = world ranks -> W = P-1 workers.
       const int P = topo.world;
@@ -250,6 +257,10 @@ int main(int argc, char** argv) {
       std::mutex mu;
       cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
         RiemannPlan plan(cfg, dev, comm);
+        {
+          std::lock_guard<std::mutex> g(mu);
+          if (rank == topo.rank0) launch_shape = plan.shape();
+        }
         if (a.has("prepare")) plan.prepare_steps(static_cast<int>(a.integer("prepare", iters)));
         plan.run_steps(1, comm != nullptr, false);  // cold: code-object load, first launch
         StepTiming t = plan.run_steps(iters, comm != nullptr, iters > 1);
@@ -277,6 +288,8 @@ int main(int argc, char** argv) {
                      .add("analytic", exact)
                      .add("abs_err", std::fabs(result - exact))
                      .add("rel_err", std::fabs(result - exact) / std::fabs(exact))
+                     .add("block", launch_shape.block)
+                     .add("grid", launch_shape.grid)
                      .add("device_ms", dev_ms)
                      .add("seconds_device", dev_ms * 1e-3)
                      .add("subintervals_per_s", dev_ms > 0 ? nd / (dev_ms * 1e-3) : 0.0)

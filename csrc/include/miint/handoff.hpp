@@ -75,14 +75,16 @@ __device__ __forceinline__ double slot_wait(const double* p, double first,
 // batch are all issued before the first add (a plain loop waited for every load).
 // SLOTS = true: the partials are write-once slots of this launch (waited for, see above);
 // false: plain loads of partials a previous launch wrote (the kernel boundary orders them).
+// BLOCK = 0: the launch's own block size (blockDim.x), for kernels launched at several sizes.
 template <int BLOCK, bool SLOTS>
 __device__ __forceinline__ double ordered_partials(const double* partials, int n) {
+  const int bs = BLOCK > 0 ? BLOCK : static_cast<int>(blockDim.x);
   double v = 0.0;
-  for (int base = 0; base < n; base += kFinalBatch * BLOCK) {
+  for (int base = 0; base < n; base += kFinalBatch * bs) {
     double r[kFinalBatch];
 #pragma unroll
     for (int k = 0; k < kFinalBatch; ++k) {
-      const int i = base + k * BLOCK + static_cast<int>(threadIdx.x);
+      const int i = base + k * bs + static_cast<int>(threadIdx.x);
       if constexpr (SLOTS)
         r[k] = i < n ? slot_load(&partials[i]) : 0.0;
       else
@@ -91,7 +93,7 @@ __device__ __forceinline__ double ordered_partials(const double* partials, int n
 #pragma unroll
     for (int k = 0; k < kFinalBatch; ++k) {
       if constexpr (SLOTS) {
-        const int i = base + k * BLOCK + static_cast<int>(threadIdx.x);
+        const int i = base + k * bs + static_cast<int>(threadIdx.x);
         if (slot_unset(r[k])) r[k] = slot_wait(&partials[i], r[k]);
       }
       v += r[k];
@@ -104,7 +106,8 @@ __device__ __forceinline__ double ordered_partials(const double* partials, int n
 // thread re-arms exactly the slots it read).
 template <int BLOCK>
 __device__ __forceinline__ void rearm_slots(double* partials, int n) {
-  for (int i = static_cast<int>(threadIdx.x); i < n; i += BLOCK)
+  const int bs = BLOCK > 0 ? BLOCK : static_cast<int>(blockDim.x);
+  for (int i = static_cast<int>(threadIdx.x); i < n; i += bs)
     slot_store(&partials[i], slot_unset_value());
 }
 

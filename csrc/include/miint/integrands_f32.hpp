@@ -187,9 +187,10 @@ struct TableF32 : TileDefaults<TableF32> {
   __device__ static constexpr double anchor() {
     return M == DivMode::kSeries ? 0.5 * (U - 1) : 0.0;
   }
+  // Clamped in fp64 BEFORE the conversion: a double beyond the int range has no defined
+  // static_cast<int> (the hardware saturates, the language does not promise it); NaN -> 0.
   __device__ __forceinline__ int segment(double t) const {
-    const int i = static_cast<int>(t);
-    return i < 0 ? 0 : (i >= nseg ? nseg - 1 : i);
+    return static_cast<int>(fmin(fmax(t, 0.0), static_cast<double>(nseg - 1)));
   }
   // fp64 coordinate and segment, fp32 interpolation
   __device__ __forceinline__ float pointf(double t) const {

@@ -38,9 +38,13 @@ namespace miint {
 // Default number of concurrent step streams in a chained graph batch. One integration's
 // kernel spends ~2-3 us ramping up, draining and flushing; with consecutive steps on
 // different streams (independent: own partials, own result) the next step fills the CUs
-// the previous one's tail leaves idle. 1/8 of N = 1e9 on one MI355X: 11.5 us per step on
-// one stream, 10.0 on four (profiles/r3/stream_overlap.jsonl).
+// the previous one's tail leaves idle. 1/8 of N = 1e9 on one MI355X: 12.2 -> 11.2 us per
+// step (20-step graphs), 11.5 -> 9.8-10.3 (48-step); 1/4: 20.5 -> 18.7; 1/2: 38.4 -> 36.8
+// (profiles/r3/strong_slices_streams.jsonl, ss20.jsonl). A step that fills the whole GPU for
+// ~70 us (>= kStepStreamsMaxCount samples: N = 1e9 on one GPU) gains nothing and replays
+// less evenly (20-step graphs: 74.3 us on one stream, 74.2-88 on 2-4), so it keeps one.
 constexpr int kAutoStepStreams = 4;
+constexpr uint64_t kStepStreamsMaxCount = 600000000ull;
 
 struct RiemannConfig {
   Integrand integrand = Integrand::kPi4;
@@ -53,6 +57,7 @@ struct RiemannConfig {
   double p0 = 0.0, p1 = 0.0;   // Integrand::kTrainVel (ts, vs)
   std::vector<double> table;   // Integrand::kTable (host copy, uploaded once)
   int grid = 0;                // workgroups; 0 = auto (waves_per_cu per CU)
+  int block = kRiemannBlock;   // threads per workgroup: 64, 128, 256, 512 or 1024 (--block)
   int waves_per_cu = 32;       // 8 x 256-thread workgroups per CU (every Riemann kernel fits 8
                                // waves/SIMD): the default grid is one full wave
   bool fused = true;           // one launch (ticket reduction) vs partials + finalize
@@ -70,7 +75,8 @@ struct RiemannConfig {
                                   // (exercises the multi-GPU graph path on one GPU)
   int step_streams = 0;         // chained graph batches: steps dealt round-robin to this many
                                 // streams (each its own chain, ramp and tail of one step
-                                // overlapping the next one's work); 0 = auto (kAutoStepStreams)
+                                // overlapping the next one's work); 0 = auto (kAutoStepStreams
+                                // below kStepStreamsMaxCount samples per step, else 1)
   int slice_rank = 0, slice_world = 0;  // > 0: integrate rank slice_rank's share of [0, n) over
                                         // slice_world ranks whatever the communicator is (one-
                                         // GPU rehearsal of a strong-scaled run's per-GPU work)

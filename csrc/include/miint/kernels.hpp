@@ -71,8 +71,10 @@ struct LaunchShape {
   int block;  // threads per workgroup
 };
 
-// Default grid: enough workgroups to hold `waves_per_cu` waves on every CU.
-LaunchShape default_riemann_shape(int num_cus, int waves_per_cu = 32);
+// Block sizes the Riemann kernels run (--block): 64, 128, 256 (default), 512, 1024.
+bool riemann_block_ok(int block);
+// Default grid: enough workgroups of `block` threads to hold `waves_per_cu` waves on every CU.
+LaunchShape default_riemann_shape(int num_cus, int waves_per_cu = 32, int block = kRiemannBlock);
 
 // Riemann partial sums: writes one fp64 partial per workgroup into partials[0..grid).
 // Partials are *unscaled* sums of f; multiply by h * integrand scale at finalize.
@@ -81,9 +83,10 @@ void launch_riemann_partials(const RiemannParams& p, DType dtype, DivMode div,
                              LaunchShape shape, const double* table, int table_n,
                              double* partials, hipStream_t stream);
 
-// out[0] = scale * sum(partials[0..n)) in a fixed order (bitwise reproducible).
+// out[0] = scale * sum(partials[0..n)) in a fixed order (bitwise reproducible): one
+// workgroup of `block` threads, the same order as a fused launch at that block size.
 void launch_finalize(const double* partials, int n, double scale, double* out,
-                     hipStream_t stream);
+                     hipStream_t stream, int block = kRiemannBlock);
 
 // Fill `count` doubles with the write-once slots' unset pattern (handoff.hpp).
 constexpr unsigned kUnsetSlotWord = 0xFFFAFFFAu;
@@ -130,6 +133,14 @@ void set_pi4_library_division(bool on);
 // Validation switch: kIeee sin (Sin) and cos (TrainVel) by ocml per sample instead of the
 // fast per-sample path (fast_trig.hpp). Process-wide; tests only.
 void set_trig_library(bool on);
+// Validation switch: every kernel that stages a WINDOW of a table in LDS (train-scan samplers,
+// interp_fill chunks, the 2-D row stream's footprint tile) first fills its LDS buffer with
+// NaN (the 2-D stream: every tile slot outside the computed footprint), so a read past the
+// staged window yields NaN instead of a stale-but-finite word. Per device (the current one),
+// process-wide; tests only.
+void set_lds_poison(bool on);
+void set_lds_poison_trainscan(bool on);  // (per kernel file; set_lds_poison sets all)
+void set_lds_poison_table(bool on);
 
 // Samples per lane tile of the kernel that launch_riemann_* would run for these arguments
 // (32; 64 or 128 on the series paths): host-side grid sizing.

@@ -91,6 +91,9 @@ void launch_trainscan_onepass(const TrainScanKernelParams& p, void* ws, double* 
                               double* totals, hipStream_t s);
 // Nonzero if a one-pass look-back spin gave up (reads the workspace header; synchronises).
 unsigned trainscan_onepass_timeout(const void* ws, hipStream_t s);
+// Nonzero if the closed-form K1 + K2 launch's block-aggregate hand-off gave up waiting (its
+// totals are then NaN); 0 for the 3-kernel path. Synchronises.
+unsigned trainscan_local_timeout(const TrainScanKernelParams& p, const void* ws, hipStream_t s);
 
 class TrainScan {
  public:

@@ -110,6 +110,26 @@ __device__ __forceinline__ T block_sum(T v, T* lds) {
   }
 }
 
+// block_sum for a block size chosen at launch (blockDim.x: whole waves, <= 1024; `lds` holds
+// at least blockDim.x / kWave elements). For blockDim.x == BLOCK it performs exactly
+// block_sum<BLOCK>'s additions, so results are bitwise the same.
+template <typename T>
+__device__ __forceinline__ T block_sum_dyn(T v, T* lds) {
+  const int nw = static_cast<int>(blockDim.x) / kWave;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+  v = wave_sum_to_last(v);
+  if (nw == 1) return wave_broadcast_last(v);
+  if (lane == kWave - 1) lds[wid] = v;
+  __syncthreads();
+  T r = T(0);
+  if (wid == 0) {
+    r = lane < nw ? lds[lane] : T(0);
+    r = wave_sum(r);
+  }
+  return r;  // meaningful in wave 0
+}
+
 // Block-wide inclusive scan; also returns the block total through *total.
 template <int BLOCK, typename T>
 __device__ __forceinline__ T block_inclusive_scan(T v, T* lds, T* total) {

@@ -21,6 +21,7 @@
 
 #include <atomic>
 #include <cmath>
+#include <string>
 
 #include "miint/common.hpp"
 #include "miint/handoff.hpp"
@@ -32,7 +33,11 @@
 namespace miint {
 namespace {
 
-constexpr int B = kRiemannBlock;
+constexpr int B = kRiemannBlock;  // the default block; validation kernels run at it
+// The integration kernels take their block size at launch (--block, SP in the reference,
+// cintegrate.cu:17-18,124-127): 64, 128, 256, 512 or 1024 threads. Everything that depends
+// on it reads blockDim.x; the hot tile loop itself does not.
+constexpr int kMaxBlock = 1024;
 
 // Wave-uniform 64-bit value read from one lane (two 32-bit v_readlane).
 __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
@@ -50,8 +55,9 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
 template <DivMode M, class F>
 __device__ __forceinline__ double lane_sum(const RiemannParams& p, const F& f) {
   constexpr int T = F::template tile_len<M>();
-  const uint64_t lanes = static_cast<uint64_t>(gridDim.x) * B;
-  const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * B + threadIdx.x;
+  const uint64_t bs = blockDim.x;
+  const uint64_t lanes = static_cast<uint64_t>(gridDim.x) * bs;
+  const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * bs + threadIdx.x;
   const uint64_t ntile = p.n / T;
   const uint64_t rounds = gid < ntile ? (ntile - 1 - gid) / lanes + 1 : 0;
   const uint64_t r_all = readlane_u64(rounds, kWave - 1);  // lane 63 has the fewest rounds
@@ -63,11 +69,10 @@ __device__ __forceinline__ double lane_sum(const RiemannParams& p, const F& f) {
   uint64_t r = 0;
   for (; r < r_all; ++r, ib += istep) acc = f.template tile_acc<T, M>(fma(ib, p.h, p.a), p.h, acc);
   if (r < r_any && r < rounds) acc = f.template tile_acc<T, M>(fma(ib, p.h, p.a), p.h, acc);
-  // remainder (< T samples): one per lane of the launch, so T must not exceed the lanes of
-  // the smallest grid (one 256-thread workgroup); the longest tile is 192 samples
-  static_assert(T <= B, "the remainder loop gives each lane at most one sample");
+  // remainder (< T samples): one per lane (a grid of fewer lanes than T loops)
   const uint64_t done = ntile * T;
-  if (gid < p.n - done) acc += f.point(fma(base + static_cast<double>(done + gid), p.h, p.a));
+  for (uint64_t k = gid; k < p.n - done; k += lanes)
+    acc += f.point(fma(base + static_cast<double>(done + k), p.h, p.a));
   return acc;
 }
 
@@ -334,7 +339,7 @@ template <int NC> struct Maker<PolyF32<NC>> {
 template <> struct Maker<TableF32> {
   static constexpr int kLds = kMaxTable;
   __device__ static TableF32 make(const RiemannParams&, const double* table, int n, double* lds) {
-    for (int i = threadIdx.x; i < n; i += B) lds[i] = table[i];
+    for (int i = threadIdx.x; i < n; i += static_cast<int>(blockDim.x)) lds[i] = table[i];
     __syncthreads();
     TableF32 f;
     f.tab = lds;
@@ -345,7 +350,7 @@ template <> struct Maker<TableF32> {
 template <> struct Maker<Table> {
   static constexpr int kLds = kMaxTable;
   __device__ static Table make(const RiemannParams&, const double* table, int n, double* lds) {
-    for (int i = threadIdx.x; i < n; i += B) lds[i] = table[i];  // 14.4 KB, once per block
+    for (int i = threadIdx.x; i < n; i += static_cast<int>(blockDim.x)) lds[i] = table[i];
     __syncthreads();
     Table f{{}, lds, n - 1};
     f.init();
@@ -418,19 +423,19 @@ constexpr bool occupancy_hint() {
 template <DivMode M, class F>
 __device__ __forceinline__ void partials_body(const RiemannParams& p, const double* table,
                                               int table_n, double* partials) {
-  __shared__ double red[B / kWave];
+  __shared__ double red[kMaxBlock / kWave];
   __shared__ double lds[lds_words<M, F>()];
   const F f = make_functor<M, F>(p, table, table_n, lds);
-  const double s = block_sum<B>(lane_sum<M>(p, f), red);
+  const double s = block_sum_dyn(lane_sum<M>(p, f), red);
   if (threadIdx.x == 0) partials[blockIdx.x] = s;
 }
 template <DivMode M, class F>
-__global__ __launch_bounds__(B) void riemann_kernel(RiemannParams p, const double* table,
+__global__ __launch_bounds__(kMaxBlock) void riemann_kernel(RiemannParams p, const double* table,
                                                     int table_n, double* partials) {
   partials_body<M, F>(p, table, table_n, partials);
 }
 template <DivMode M, class F>
-__global__ __launch_bounds__(B) kFullOccupancy void riemann_kernel_o8(RiemannParams p,
+__global__ __launch_bounds__(kMaxBlock) kFullOccupancy void riemann_kernel_o8(RiemannParams p,
                                                                       const double* table,
                                                                       int table_n,
                                                                       double* partials) {
@@ -438,17 +443,16 @@ __global__ __launch_bounds__(B) kFullOccupancy void riemann_kernel_o8(RiemannPar
 }
 
 // ---------------------------------------------------------------------------- finalize
-// Same width and order as the fused kernel's last-workgroup sum (B threads, partial i
-// folded into thread i % B in increasing i), so both paths are bitwise identical.
-constexpr int kFinalBlock = B;
-
+// Same width and order as the fused kernel's last-workgroup sum (launched at the plan's
+// block size bs: partial i folded into thread i % bs in increasing i), so both paths are
+// bitwise identical.
 __device__ __forceinline__ double ordered_sum(const double* partials, int n, double* red) {
-  return block_sum<kFinalBlock>(ordered_partials<kFinalBlock, false>(partials, n), red);
+  return block_sum_dyn(ordered_partials<0, false>(partials, n), red);
 }
 
-__global__ __launch_bounds__(kFinalBlock) void finalize_kernel(const double* partials, int n,
-                                                               double scale, double* out) {
-  __shared__ double red[kFinalBlock / kWave];
+__global__ __launch_bounds__(kMaxBlock) void finalize_kernel(const double* partials, int n,
+                                                             double scale, double* out) {
+  __shared__ double red[kMaxBlock / kWave];
   const double s = ordered_sum(partials, n, red);
   if (threadIdx.x == 0) out[0] = s * scale;
 }
@@ -460,27 +464,27 @@ template <DivMode M, class F>
 __device__ __forceinline__ void fused_body(const RiemannParams& p, const double* table,
                                            int table_n, double* partials, unsigned int* ticket,
                                            double scale, double* out) {
-  __shared__ double red[B / kWave];
+  __shared__ double red[kMaxBlock / kWave];
   __shared__ double lds[lds_words<M, F>()];
   __shared__ int is_last;
   const F f = make_functor<M, F>(p, table, table_n, lds);
-  const double s = block_sum<B>(lane_sum<M>(p, f), red);
+  const double s = block_sum_dyn(lane_sum<M>(p, f), red);
   if (!publish_and_ticket(s, partials, ticket, blockIdx.x, gridDim.x, &is_last)) return;
-  const double v = ordered_partials<B, true>(partials, static_cast<int>(gridDim.x));
-  rearm_slots<B>(partials, static_cast<int>(gridDim.x));
-  const double tot = block_sum<B>(v, red);
+  const double v = ordered_partials<0, true>(partials, static_cast<int>(gridDim.x));
+  rearm_slots<0>(partials, static_cast<int>(gridDim.x));
+  const double tot = block_sum_dyn(v, red);
   if (threadIdx.x == 0) out[0] = tot * scale;
   rearm_ticket(ticket, gridDim.x);
 }
 template <DivMode M, class F>
-__global__ __launch_bounds__(B) void riemann_fused_kernel(RiemannParams p, const double* table,
+__global__ __launch_bounds__(kMaxBlock) void riemann_fused_kernel(RiemannParams p, const double* table,
                                                           int table_n, double* partials,
                                                           unsigned int* ticket, double scale,
                                                           double* out) {
   fused_body<M, F>(p, table, table_n, partials, ticket, scale, out);
 }
 template <DivMode M, class F>
-__global__ __launch_bounds__(B) kFullOccupancy void riemann_fused_kernel_o8(
+__global__ __launch_bounds__(kMaxBlock) kFullOccupancy void riemann_fused_kernel_o8(
     RiemannParams p, const double* table, int table_n, double* partials, unsigned int* ticket,
     double scale, double* out) {
   fused_body<M, F>(p, table, table_n, partials, ticket, scale, out);
@@ -499,26 +503,26 @@ template <DivMode M, class F>
 __device__ __forceinline__ void chained_body(const RiemannParams& p, const double* table,
                                              int table_n, double* partials, const double* prev,
                                              int nprev, double scale, double* out_prev) {
-  __shared__ double red[B / kWave];
+  __shared__ double red[kMaxBlock / kWave];
   __shared__ double lds[lds_words<M, F>()];
   if (prev != nullptr && blockIdx.x == gridDim.x - 1) {
-    const double tot = block_sum<B>(ordered_partials<B, false>(prev, nprev), red);
+    const double tot = block_sum_dyn(ordered_partials<0, false>(prev, nprev), red);
     if (threadIdx.x == 0) out_prev[0] = tot * scale;
     __syncthreads();  // red is reused below
   }
   const F f = make_functor<M, F>(p, table, table_n, lds);
-  const double s = block_sum<B>(lane_sum<M>(p, f), red);
+  const double s = block_sum_dyn(lane_sum<M>(p, f), red);
   if (threadIdx.x == 0) partials[blockIdx.x] = s;
 }
 template <DivMode M, class F>
-__global__ __launch_bounds__(B) void riemann_chained_kernel(RiemannParams p, const double* table,
+__global__ __launch_bounds__(kMaxBlock) void riemann_chained_kernel(RiemannParams p, const double* table,
                                                             int table_n, double* partials,
                                                             const double* prev, int nprev,
                                                             double scale, double* out_prev) {
   chained_body<M, F>(p, table, table_n, partials, prev, nprev, scale, out_prev);
 }
 template <DivMode M, class F>
-__global__ __launch_bounds__(B) kFullOccupancy void riemann_chained_kernel_o8(
+__global__ __launch_bounds__(kMaxBlock) kFullOccupancy void riemann_chained_kernel_o8(
     RiemannParams p, const double* table, int table_n, double* partials, const double* prev,
     int nprev, double scale, double* out_prev) {
   chained_body<M, F>(p, table, table_n, partials, prev, nprev, scale, out_prev);
@@ -587,9 +591,9 @@ template <DivMode M, class F>
 void launch_partials_t(const RiemannParams& p, LaunchShape shape, const double* table,
                        int table_n, double* partials, hipStream_t stream) {
   if constexpr (occupancy_hint<M, F>())
-    riemann_kernel_o8<M, F><<<shape.grid, B, 0, stream>>>(p, table, table_n, partials);
+    riemann_kernel_o8<M, F><<<shape.grid, shape.block, 0, stream>>>(p, table, table_n, partials);
   else
-    riemann_kernel<M, F><<<shape.grid, B, 0, stream>>>(p, table, table_n, partials);
+    riemann_kernel<M, F><<<shape.grid, shape.block, 0, stream>>>(p, table, table_n, partials);
 }
 template <DivMode M, class F>
 void launch_fused_t(const RiemannParams& p, LaunchShape shape, const double* table, int table_n,
@@ -597,10 +601,10 @@ void launch_fused_t(const RiemannParams& p, LaunchShape shape, const double* tab
                     hipStream_t stream) {
   if constexpr (occupancy_hint<M, F>())
     riemann_fused_kernel_o8<M, F>
-        <<<shape.grid, B, 0, stream>>>(p, table, table_n, partials, ticket, scale, out);
+        <<<shape.grid, shape.block, 0, stream>>>(p, table, table_n, partials, ticket, scale, out);
   else
     riemann_fused_kernel<M, F>
-        <<<shape.grid, B, 0, stream>>>(p, table, table_n, partials, ticket, scale, out);
+        <<<shape.grid, shape.block, 0, stream>>>(p, table, table_n, partials, ticket, scale, out);
 }
 
 template <DivMode M, class F>
@@ -608,10 +612,10 @@ void launch_chained_t(const RiemannParams& p, LaunchShape shape, const double* t
                       int table_n, double* partials, const double* prev, int nprev, double scale,
                       double* out_prev, hipStream_t stream) {
   if constexpr (occupancy_hint<M, F>())
-    riemann_chained_kernel_o8<M, F><<<shape.grid, B, 0, stream>>>(p, table, table_n, partials,
+    riemann_chained_kernel_o8<M, F><<<shape.grid, shape.block, 0, stream>>>(p, table, table_n, partials,
                                                                   prev, nprev, scale, out_prev);
   else
-    riemann_chained_kernel<M, F><<<shape.grid, B, 0, stream>>>(p, table, table_n, partials,
+    riemann_chained_kernel<M, F><<<shape.grid, shape.block, 0, stream>>>(p, table, table_n, partials,
                                                                prev, nprev, scale, out_prev);
 }
 
@@ -725,17 +729,24 @@ template <DivMode M, class F> struct PointsOp {
 }  // namespace
 
 // ============================================================================ host side
-LaunchShape default_riemann_shape(int num_cus, int waves_per_cu) {
-  const int waves_per_block = B / kWave;
+bool riemann_block_ok(int block) {
+  return block == 64 || block == 128 || block == 256 || block == 512 || block == 1024;
+}
+
+LaunchShape default_riemann_shape(int num_cus, int waves_per_cu, int block) {
+  MIINT_CHECK(riemann_block_ok(block), "unsupported Riemann block size");
+  const int waves_per_block = block / kWave;
   int blocks = (num_cus * waves_per_cu) / waves_per_block;
   if (blocks < 1) blocks = 1;
-  return {blocks, B};
+  return {blocks, block};
 }
 
 double integrand_scale(Integrand f) { return f == Integrand::kPi4 ? Pi4::kScale : 1.0; }
 
 static void check_shape(LaunchShape s) {
-  MIINT_CHECK(s.block == B, "riemann kernels are compiled for 256-thread workgroups");
+  MIINT_CHECK(riemann_block_ok(s.block),
+              "riemann kernels run 64-, 128-, 256-, 512- or 1024-thread workgroups (got " +
+                  std::to_string(s.block) + ")");
   MIINT_CHECK(s.grid >= 1 && s.grid <= (1 << 20), "grid out of range");
 }
 
@@ -807,9 +818,10 @@ void launch_riemann_partials(const RiemannParams& p, DType dtype, DivMode div, L
 }
 
 void launch_finalize(const double* partials, int n, double scale, double* out,
-                     hipStream_t stream) {
+                     hipStream_t stream, int block) {
   MIINT_CHECK(n >= 1, "finalize needs at least one partial");
-  finalize_kernel<<<1, kFinalBlock, 0, stream>>>(partials, n, scale, out);
+  MIINT_CHECK(riemann_block_ok(block), "unsupported finalize block size");
+  finalize_kernel<<<1, block, 0, stream>>>(partials, n, scale, out);
   MIINT_HIP(hipGetLastError());
 }
 

@@ -15,6 +15,8 @@
 // down the rows.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include <algorithm>
 #include <cmath>
 #include <type_traits>
@@ -63,6 +65,11 @@ __device__ __forceinline__ int seg_of(double t, int nseg) {
   return t >= static_cast<double>(nseg) ? nseg - 1 : (t < 1.0 ? 0 : static_cast<int>(t));
 }
 
+// set_lds_poison: NaN in every LDS word a window does not stage (validation only); the 2-D
+// stream kernel gets it as a template instantiation instead (no branch in the hot kernel)
+__constant__ int g_lds_poison;
+std::atomic<bool> g_table2d_poison{false};
+
 __device__ __forceinline__ double interp_lds(const double* tab, int nseg, double t) {
   const int i = seg_of(t, nseg);
   const double v0 = tab[i];
@@ -91,6 +98,10 @@ __global__ __launch_bounds__(kB) void interp_fill_kernel(const double* __restric
   if (vb < ve) {
     const int ka = seg(i0 + 2 * vb), kb = seg(i0 + 2 * ve - 1);
     const int k0 = ka < kb ? ka : kb, k1 = ka < kb ? kb : ka;
+    if (g_lds_poison) {
+      for (int k = static_cast<int>(threadIdx.x); k < kMaxTable; k += kB) tab[k] = __builtin_nan("");
+      __syncthreads();
+    }
     for (int k = k0 + static_cast<int>(threadIdx.x); k <= k1 + 1; k += kB) tab[k - k0] = table[k];
     __syncthreads();
     auto at = [&](uint64_t i) {  // interp_lds on the staged window (tab[j] = table[k0 + j])
@@ -271,7 +282,9 @@ __device__ __forceinline__ double fma_sv(double a, double s, double c) {
   return r;
 }
 
-template <int MODE, int SH>
+// POISON (validation instantiation, set_lds_poison): tile slots outside the computed footprint
+// hold NaN instead of the corner value, so a read outside the footprint shows.
+template <int MODE, int SH, bool POISON>
 __global__ __launch_bounds__(kB) void table2d_stream_kernel(Table2DParams p, int rows_per_wave,
                                                             double* partials, unsigned* ticket,
                                                             double* out, Table2DChain chain) {
@@ -312,6 +325,7 @@ __global__ __launch_bounds__(kB) void table2d_stream_kernel(Table2DParams p, int
       const unsigned off = (lx < w && rr < hgt) ? static_cast<unsigned>(rr * p.nx + lx) * 8u : 0u;
       v[j] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(tb) + off);
     }
+
     // chained: workgroup 0 closes the previous integration while its staging loads fly
     // (the loads above hold 32 VGPRs; the kernel is LDS-limited to 4 waves per SIMD, whose
     // 128-VGPR budget the close's 16 loads in flight fit beside them)
@@ -321,6 +335,12 @@ __global__ __launch_bounds__(kB) void table2d_stream_kernel(Table2DParams p, int
     }
 #pragma unroll
     for (int j = 0; j < kPasses; ++j) tile[(ly + kRowsPer * j) * kSW + lx] = v[j];
+    if constexpr (POISON) {  // validation: NaN in the tile slots outside the footprint
+#pragma unroll
+      for (int j = 0; j < kPasses; ++j)
+        if (!(lx < w && ly + kRowsPer * j < hgt))
+          tile[(ly + kRowsPer * j) * kSW + lx] = __builtin_nan("");
+    }
   }
   // per-lane columns: LDS column and x fraction, computed once
   int col[kSCols];
@@ -414,6 +434,17 @@ void launch_sum_array(const double* x, uint64_t n, double scale, double* partial
   launch_finalize(partials, grid, scale, out, stream);
 }
 
+void set_lds_poison_table(bool on) {
+  const int v = on ? 1 : 0;
+  MIINT_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_lds_poison), &v, sizeof(v)));
+  g_table2d_poison.store(on);
+}
+
+void set_lds_poison(bool on) {
+  set_lds_poison_table(on);
+  set_lds_poison_trainscan(on);
+}
+
 void launch_interp_fill(const double* table, int table_n, double dt, uint64_t i0, uint64_t n,
                         double* y, hipStream_t stream) {
   MIINT_CHECK(table_n >= 2 && table_n <= kMaxTable, "table size must be in [2, 2048]");
@@ -498,12 +529,19 @@ static void launch_table2d(const Table2DParams& p, double* partials, unsigned* t
                            double* out, Table2DChain chain, hipStream_t stream) {
   check_table2d(p);
   const Table2DShape sh = table2d_shape(p);
-  if (sh.stream && sh.short_tile)
-    table2d_stream_kernel<MODE, kSHShort><<<sh.grid, kB, 0, stream>>>(
+  const bool poison = g_table2d_poison.load(std::memory_order_relaxed);
+  if (sh.stream && sh.short_tile && poison)
+    table2d_stream_kernel<MODE, kSHShort, true><<<sh.grid, kB, 0, stream>>>(
+        p, sh.rows_per_wave, partials, ticket, out, chain);
+  else if (sh.stream && sh.short_tile)
+    table2d_stream_kernel<MODE, kSHShort, false><<<sh.grid, kB, 0, stream>>>(
+        p, sh.rows_per_wave, partials, ticket, out, chain);
+  else if (sh.stream && poison)
+    table2d_stream_kernel<MODE, kSH, true><<<sh.grid, kB, 0, stream>>>(
         p, sh.rows_per_wave, partials, ticket, out, chain);
   else if (sh.stream)
-    table2d_stream_kernel<MODE, kSH><<<sh.grid, kB, 0, stream>>>(p, sh.rows_per_wave, partials,
-                                                                 ticket, out, chain);
+    table2d_stream_kernel<MODE, kSH, false><<<sh.grid, kB, 0, stream>>>(
+        p, sh.rows_per_wave, partials, ticket, out, chain);
   else if (sh.tile == 128)
     table2d_kernel<128, MODE><<<sh.grid, kB, 0, stream>>>(p, partials, ticket, out, chain);
   else

@@ -45,6 +45,9 @@ constexpr int kSpan = 64;  // table entries staged per tile (LDS)
 typedef double f64x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) const double lds_f64;
 
+// set_lds_poison: fill a tile's LDS window with NaN before staging (validation only)
+__constant__ int g_lds_poison;
+
 struct Sampler {
   const double* tab;  // LDS copy of table entries [s0, s0 + count), or the global table
   bool staged;        // tab points into LDS
@@ -112,6 +115,10 @@ __device__ __forceinline__ Sampler make_sampler(const TrainScanKernelParams& p, 
   const int s1 = min(seg_of(p.dt * static_cast<double>(p.i0 + last), nseg) + 2, nseg);
   if (s1 - s0 + 1 > kSpan)  // coarse sampling: read the (L2-resident) table directly
     return {p.table, false, 0, nseg, p.dt, p.i0, p.n, p.win_lo, p.win_hi};
+  if (g_lds_poison) {  // validation: what the window does not stage reads as NaN
+    for (int k = threadIdx.x; k < kSpan; k += kB) tab[k] = __builtin_nan("");
+    __syncthreads();
+  }
   for (int k = threadIdx.x; k <= s1 - s0; k += kB) tab[k] = p.table[s0 + k];
   __syncthreads();
   return {tab, true, s0, nseg, p.dt, p.i0, p.n, p.win_lo, p.win_hi};
@@ -237,6 +244,7 @@ struct ClosedScan {
   f64x2* blockpre;   // per block, exclusive {PB, QB}
   double* agg;       // per block {A, B, N} (stride 4 doubles)
   unsigned* ticket;
+  unsigned* timeout;  // raised by a block-aggregate slot wait that gave up (ticket + 1)
 };
 
 // kHandoff = false (one GPU, <= kMaxFoldBlocks blocks): stop after the per-block aggregates;
@@ -291,9 +299,9 @@ __global__ __launch_bounds__(kB) void ts_tile_scan_closed(TrainScanKernelParams 
     const uint32_t b = b0 + threadIdx.x;
     const bool vb = b < gridDim.x;
     const double* g = cs.agg + 4 * b;
-    const double a = vb ? slot_wait(g, slot_load(g)) : 0.0;
-    const double bb = vb ? slot_wait(g + 1, slot_load(g + 1)) : 0.0;
-    const double nb = vb ? slot_wait(g + 2, slot_load(g + 2)) : 0.0;
+    const double a = vb ? slot_wait(g, slot_load(g), cs.timeout) : 0.0;
+    const double bb = vb ? slot_wait(g + 1, slot_load(g + 1), cs.timeout) : 0.0;
+    const double nb = vb ? slot_wait(g + 2, slot_load(g + 2), cs.timeout) : 0.0;
     double ta, tq;
     const double pb = cp + (block_inclusive_scan<kB>(a, red, &ta) - a);
     __syncthreads();
@@ -318,6 +326,7 @@ ClosedScan closed_carve(void* ws, uint64_t nt) {
   cs.blockpre = cs.local + nt;
   cs.agg = reinterpret_cast<double*>(cs.blockpre + nb);
   cs.ticket = reinterpret_cast<unsigned*>(cs.agg + 4 * nb);
+  cs.timeout = cs.ticket + 1;
   return cs;
 }
 
@@ -645,6 +654,11 @@ __global__ __launch_bounds__(256) void ts_parity_serial(TrainScanKernelParams p,
 
 }  // namespace
 
+void set_lds_poison_trainscan(bool on) {
+  const int v = on ? 1 : 0;
+  MIINT_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_lds_poison), &v, sizeof(v)));
+}
+
 size_t trainscan_workspace_bytes(uint64_t n) {
   const uint64_t nt = (n + kTile - 1) / kTile;
   // 3-kernel path: {sums, prefix} f64x2 per tile + per-block {prefix, aggregates, ticket};
@@ -674,6 +688,17 @@ unsigned trainscan_onepass_timeout(const void* ws, hipStream_t s) {
   unsigned v = 0;
   MIINT_HIP(hipMemcpyAsync(&v, static_cast<const char*>(ws) + 4, sizeof(v), hipMemcpyDeviceToHost,
                            s));
+  MIINT_HIP(hipStreamSynchronize(s));
+  return v;
+}
+
+unsigned trainscan_local_timeout(const TrainScanKernelParams& p, const void* ws,
+                                 hipStream_t s) {
+  uint64_t sps = 0;
+  if (!closed_form_sps(p.dt, &sps)) return 0;  // the 3-kernel path hands nothing over
+  const ClosedScan cs = closed_carve(const_cast<void*>(ws), (p.n + kTile - 1) / kTile);
+  unsigned v = 0;
+  MIINT_HIP(hipMemcpyAsync(&v, cs.timeout, sizeof(v), hipMemcpyDeviceToHost, s));
   MIINT_HIP(hipStreamSynchronize(s));
   return v;
 }

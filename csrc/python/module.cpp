@@ -208,6 +208,7 @@ PYBIND11_MODULE(_miint, m) {
       .def_readwrite("p1", &RiemannConfig::p1)
       .def_readwrite("table", &RiemannConfig::table)
       .def_readwrite("grid", &RiemannConfig::grid)
+      .def_readwrite("block", &RiemannConfig::block)
       .def_readwrite("waves_per_cu", &RiemannConfig::waves_per_cu)
       .def_readwrite("fused", &RiemannConfig::fused)
       .def_readwrite("slots", &RiemannConfig::slots)
@@ -306,6 +307,8 @@ PYBIND11_MODULE(_miint, m) {
   m.def("launch_pi4_recip_narrow_f32", [](uintptr_t d, uint64_t n, uintptr_t out, uintptr_t s) {
     launch_pi4_recip_narrow_f32(ptr<const float>(d), n, ptr<float>(out), stream(s));
   });
+  m.def("set_lds_poison", &set_lds_poison, py::arg("on"),
+        "validation: staged-window kernels fill their LDS with NaN first (current device)");
   m.def("set_trig_library", &set_trig_library, py::arg("on"),
         "validation: kIeee sin/cos by ocml per sample (SinLib / TrainVelLib)");
   m.def("fast_trig_host", [](uintptr_t x, uint64_t n, int shift, uintptr_t val, uintptr_t ulp) {
@@ -330,9 +333,12 @@ PYBIND11_MODULE(_miint, m) {
   });
   m.def("set_pi4_library_division", &set_pi4_library_division,
         "validation: kIeee Pi4 launches use the full library division (bitwise the same sums)");
-  m.def("launch_finalize", [](uintptr_t partials, int n, double scale, uintptr_t out, uintptr_t s) {
-    launch_finalize(ptr<const double>(partials), n, scale, ptr<double>(out), stream(s));
-  });
+  m.def("riemann_block_ok", &riemann_block_ok);
+  m.def("launch_finalize", [](uintptr_t partials, int n, double scale, uintptr_t out, uintptr_t s,
+                              int block) {
+    launch_finalize(ptr<const double>(partials), n, scale, ptr<double>(out), stream(s), block);
+  }, py::arg("partials"), py::arg("n"), py::arg("scale"), py::arg("out"), py::arg("stream"),
+     py::arg("block") = kRiemannBlock);
   m.def("default_riemann_grid", [](int cus, int waves) { return default_riemann_shape(cus, waves).grid; });
   m.def("default_reduce_grid", &default_reduce_grid);
   m.def("launch_sum_array", [](uintptr_t x, uint64_t n, double scale, uintptr_t partials, int grid,

@@ -22,6 +22,11 @@ void expr_check(const std::string& e) {
     MIINT_CHECK(ok, std::string("expression: character '") + c + "' not allowed (one C++ "
                     "expression over x: no ; { } [ ] # quotes or backslashes)");
   }
+  // digraphs spell the characters refused above: <% %> <: :> %: are { } [ ] #
+  for (const char* dg : {"<%", "%>", "<:", ":>", "%:"})
+    MIINT_CHECK(e.find(dg) == std::string::npos,
+                std::string("expression: digraph '") + dg + "' not allowed (it spells a brace, "
+                "bracket or #)");
   // identifiers that are not math: asm / volatile / goto / the preprocessor are out
   std::string word;
   auto bad = [](const std::string& w) {

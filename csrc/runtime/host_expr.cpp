@@ -7,6 +7,7 @@
 // The system compiler builds it into a shared object (-O3 -march=native -fPIC -shared; no
 // fast-math), which is dlopen'ed and run on the HostPool's threads.
 #include <dlfcn.h>
+#include <fcntl.h>
 #include <spawn.h>
 #include <sys/stat.h>
 #include <sys/wait.h>
@@ -67,17 +68,36 @@ std::string host_compiler() {
   return "c++";
 }
 
-// Run argv[0] with argv as a child (posix_spawn: no fork of this possibly GPU-initialised
-// process image) and wait; returns its exit status.
-int run_child(const std::vector<std::string>& args) {
+// Run argv[0] with argv as a child and wait; returns its exit status. posix_spawn, no fork
+// of this possibly GPU-initialised process image, and no shell in between: the compiler is
+// the child itself, its stdout and stderr redirected to `log` by spawn file actions.
+int run_child(const std::vector<std::string>& args, const std::string& log) {
   std::vector<char*> argv;
   for (const auto& s : args) argv.push_back(const_cast<char*>(s.c_str()));
   argv.push_back(nullptr);
+  posix_spawn_file_actions_t fa;
+  if (::posix_spawn_file_actions_init(&fa) != 0) return -1;
+  ::posix_spawn_file_actions_addopen(&fa, 1, log.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0600);
+  ::posix_spawn_file_actions_adddup2(&fa, 1, 2);
   pid_t pid = 0;
-  if (::posix_spawnp(&pid, argv[0], nullptr, nullptr, argv.data(), environ) != 0) return -1;
+  const int err = ::posix_spawnp(&pid, argv[0], &fa, nullptr, argv.data(), environ);
+  ::posix_spawn_file_actions_destroy(&fa);
+  if (err != 0) return -1;
   int st = 0;
   if (::waitpid(pid, &st, 0) < 0) return -1;
   return WIFEXITED(st) ? WEXITSTATUS(st) : 128 + WTERMSIG(st);
+}
+
+// Under rocprofv3 every child process inherits the profiler's preloaded library, which
+// initialises the GPU before the compiler's own code runs; a compiler that then execs its
+// driver stages is the exec-after-GPU-init this pool refuses. Refuse up front, with the
+// reason, as cuda_v_mpi_amd/_native.py does for its build.
+void check_not_profiled() {
+  const char* pre = std::getenv("LD_PRELOAD");
+  MIINT_CHECK(!(pre && std::string(pre).find("rocprofiler") != std::string::npos),
+              "host expression: cannot run the host compiler under rocprofv3 (its preload "
+              "initialises the GPU in the compiler); compile the expression outside the "
+              "profiled process first");
 }
 
 struct Compiled {
@@ -100,10 +120,9 @@ Compiled compile_host(const std::string& expr) {
     std::ofstream f(src);
     f << host_source(expr);
   }
-  const int rc = run_child({"sh", "-c",
-                            "\"$0\" -std=c++17 -O3 -march=native -fPIC -shared -o \"$1\" \"$2\" "
-                            "> \"$3\" 2>&1",
-                            host_compiler(), so, src, log});
+  check_not_profiled();
+  const int rc = run_child({host_compiler(), "-std=c++17", "-O3", "-march=native", "-fPIC",
+                            "-shared", "-o", so, src}, log);
   auto cleanup = [&] {  // the loaded object stays mapped; the files can go
     std::remove(src.c_str());
     std::remove(so.c_str());

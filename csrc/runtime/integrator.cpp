@@ -2,6 +2,7 @@
 #include "miint/integrator.hpp"
 
 #include <algorithm>
+#include <string>
 
 #include "miint/trace.hpp"
 
@@ -48,14 +49,18 @@ RiemannPlan::RiemannPlan(const RiemannConfig& cfg, int device, const Comm* comm)
   scale_ = params_.h * integrand_scale(cfg.integrand);
 
   const DeviceInfo info = device_info(device);
-  shape_ = default_riemann_shape(info.num_cus, cfg.waves_per_cu);
+  MIINT_CHECK(riemann_block_ok(cfg.block),
+              "block must be 64, 128, 256, 512 or 1024 threads (got " + std::to_string(cfg.block) +
+                  ")");
+  const uint64_t bs = static_cast<uint64_t>(cfg.block);
+  shape_ = default_riemann_shape(info.num_cus, cfg.waves_per_cu, cfg.block);
   if (cfg.grid > 0) shape_.grid = cfg.grid;
   // Never launch more workgroups than there are tiles to deal out, counted at the tile
   // length of the kernel that will run (32, 64 or 128 samples): idle workgroups still
   // launch, publish a partial and widen the final reduction.
   const uint64_t tl = static_cast<uint64_t>(riemann_tile_len(params_, cfg.dtype, cfg.div));
   const uint64_t tiles = (params_.n + tl - 1) / tl;
-  const uint64_t need = std::max<uint64_t>(1, (tiles + kRiemannBlock - 1) / kRiemannBlock);
+  const uint64_t need = std::max<uint64_t>(1, (tiles + bs - 1) / bs);
   shape_.grid = static_cast<int>(std::min<uint64_t>(static_cast<uint64_t>(shape_.grid), need));
   // Small N (latency-bound): give lanes ~4 tiles each, but keep >= 1 workgroup per CU. At
   // one tile per lane the launch, the partial stores and the final reduction over every
@@ -66,7 +71,7 @@ RiemannPlan::RiemannPlan(const RiemannConfig& cfg, int device, const Comm* comm)
   if (cfg.grid <= 0) {
     const uint64_t cus = static_cast<uint64_t>(info.num_cus);
     const uint64_t four =
-        std::max<uint64_t>(cus, (tiles + 4 * kRiemannBlock - 1) / (4 * kRiemannBlock));
+        std::max<uint64_t>(cus, (tiles + 4 * bs - 1) / (4 * bs));
     uint64_t g = std::min<uint64_t>(static_cast<uint64_t>(shape_.grid), four);
     if (g > cus) g -= g % cus;
     shape_.grid = static_cast<int>(g);
@@ -125,7 +130,7 @@ void RiemannPlan::enqueue_compute(hipStream_t s, int slot, int host_index) const
   } else {
     launch_riemann_partials(params_, cfg_.dtype, cfg_.div, shape_, table_.get(), tn,
                             partials_.get(), s);
-    launch_finalize(partials_.get(), shape_.grid, scale_, out, s);
+    launch_finalize(partials_.get(), shape_.grid, scale_, out, s, shape_.block);
   }
 }
 
@@ -170,12 +175,14 @@ void RiemannPlan::enqueue_chain(hipStream_t s, int nsteps) const {
                            scale_, j ? result_ptr(j - 1) : nullptr, s);
   }
   launch_finalize(partials_.get() + static_cast<size_t>((nsteps - 1) & 1) * g, g, scale_,
-                  result_ptr(nsteps - 1), s);
+                  result_ptr(nsteps - 1), s, shape_.block);
 }
 
 int RiemannPlan::step_streams(int nsteps) const {
   if (!chained()) return 1;
-  const int want = cfg_.step_streams > 0 ? cfg_.step_streams : kAutoStepStreams;
+  const int want = cfg_.step_streams > 0            ? cfg_.step_streams
+                   : params_.n >= kStepStreamsMaxCount ? 1
+                                                       : kAutoStepStreams;
   return std::max(1, std::min(want, nsteps));
 }
 
@@ -206,7 +213,7 @@ void RiemannPlan::enqueue_chain_streams(hipStream_t cs, int nsteps) {
   }
   for (int l = 0; l < L && l < nsteps; ++l) {
     const int last = l + ((nsteps - 1 - l) / L) * L;  // the chain's last step
-    launch_finalize(half(l, last / L), g, scale_, result_ptr(last), lane(l));
+    launch_finalize(half(l, last / L), g, scale_, result_ptr(last), lane(l), shape_.block);
     if (l > 0) {
       ev_step_join_[static_cast<size_t>(l - 1)]->record(lane(l));
       MIINT_HIP(hipStreamWaitEvent(cs, ev_step_join_[static_cast<size_t>(l - 1)]->get(), 0));

@@ -188,9 +188,14 @@ TrainScanResult TrainScan::run() {
   r.device_ms = Event::elapsed_ms(e0_, e1_);
   if (cfg_.algo == ScanAlgo::kLookback) r.timeout = scan_timeout_flag(state_.get(), s);
   if (cfg_.algo == ScanAlgo::kOnePass) r.timeout = trainscan_onepass_timeout(state_.get(), s);
+  if (cfg_.algo == ScanAlgo::kFused) {
+    const TrainScanKernelParams p{table_.get(), tn_, 1.0 / cfg_.steps_per_sec, begin_, count_,
+                                  win_lo_, win_hi_};
+    r.timeout = trainscan_local_timeout(p, state_.get(), s);
+  }
   // a look-back that gave up has poisoned its outputs with NaN: never hand them back
-  MIINT_CHECK(r.timeout == 0, "trainscan: a look-back spin hit its limit (a predecessor tile "
-                              "never published); results are invalid");
+  MIINT_CHECK(r.timeout == 0, "trainscan: a hand-off spin hit its limit (a predecessor tile or "
+                              "block never published); results are invalid");
   // 4main.c:241 prints default_sum[tablelen-2]; the complete integral is element T-1.
   const uint64_t gi = cfg_.parity ? total_ - 2 : total_ - 1;
   r.distance = pick_global(vel_.get(), gi, s) / cfg_.steps_per_sec;

@@ -70,7 +70,8 @@ class Integrator:
                  fused: bool = True, grid: int = 0, slots: int = 16, a: float | None = None,
                  b: float | None = None, force_collective: bool = False, bucket: bool = True,
                  chain: bool = True, comm_obj=None, threads: int = 0,
-                 slice_of: tuple[int, int] | None = None, step_streams: int = 0, **spec_kw):
+                 slice_of: tuple[int, int] | None = None, step_streams: int = 0,
+                 block: int = 256, **spec_kw):
         spec = integrands.get(integrand, **spec_kw) if isinstance(integrand, str) else integrand
         if a is not None or b is not None:
             spec = dataclasses.replace(spec, a=spec.a if a is None else a,
@@ -108,6 +109,7 @@ class Integrator:
             cfg.p0, cfg.p1 = spec.p0, spec.p1
             cfg.table = spec.native_table()
             cfg.grid, cfg.fused, cfg.slots = grid, fused, slots
+            cfg.block = block  # threads per workgroup (the reference's SP): 64 .. 1024
             cfg.force_collective = force_collective
             cfg.bucket = bucket
             cfg.chain = chain

@@ -21,7 +21,10 @@ def test_expr_compiles_for_gfx950_without_a_device(native):
 
 @pytest.mark.parametrize("bad", ["x; x", "x) { return 0", "asm(\"s_nop 0\")", "asm (x)",
                                  "__builtin_amdgcn_s_sleep(1)", "x\\", "#define y", "'a'",
-                                 "", "x" * 5000])
+                                 "", "x" * 5000,
+                                 # digraphs: { } [ ] # spelled with allowed characters
+                                 "x <% return 0; %>", "x <: 0 :>", "%:define y", "x%>",
+                                 "(<%%>)"])
 def test_expr_rejected_before_compiling(native, bad):
     with pytest.raises(RuntimeError, match="expression"):
         native.expr_source(bad)
@@ -76,6 +79,18 @@ def test_host_expr_rejections(native):
         native.HostExpr("x; system(0)")
     with pytest.raises(RuntimeError, match="does not compile"):
         native.HostExpr("1.0 / (1.0 + y)")
+    with pytest.raises(RuntimeError, match="digraph"):  # a block smuggled past the filter
+        native.HostExpr("x + (<%%>)")
+
+
+def test_expr_modulo_and_comparisons_still_allowed(native):
+    """The digraph rule leaves the operators it shares characters with: %, <, >, ?: ."""
+    src = native.expr_source("x < 0.5 ? fmod(x, 0.25) : (x > 0.75 ? 1.0 : x * x)")
+    assert "fmod(x, 0.25)" in src
+    v = native.HostExpr("(x < 0.5) ? 2.0 : 0.0").integrate(0.0, 1.0, 1000,
+                                                          native.Rule.mid, 0, 1000,
+                                                          native.HostPool(1))
+    assert v == pytest.approx(1.0, rel=1e-12)
 
 
 def test_cli_and_compare_host_expr():

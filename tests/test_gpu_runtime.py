@@ -406,3 +406,23 @@ def test_compare_gpu_vs_host(native, cuda):
         assert abs(r["value"] - 2.0) < 1e-12, r
     assert by["reference-program"]["value"] == native.oracle.riemann_mpi_parity(8, 1e8)
     assert rows[-1]["speedup_gpu_vs_host"] > 1.0
+
+
+@pytest.mark.parametrize("block", [64, 128, 512, 1024])
+def test_block_sizes(native, cuda, block):
+    """--block (the reference's SP, cintegrate.cu:17-18,124-127): every supported workgroup
+    size integrates correctly, the chained graph batch equals the one-launch fused form
+    bitwise at that size, and unsupported sizes are refused with the list of valid ones."""
+    from cuda_v_mpi_amd import Integrator
+
+    n = 10**8 + 17
+    it = Integrator("pi4", n=n, rule="mid", block=block)
+    assert it.plan.block == block
+    one = it.run().value
+    assert one == pytest.approx(math.pi, abs=1e-13)
+    it.plan.run_steps(5, False, True)  # chained graph batch
+    assert it.plan.host_result(it.plan.host_index_of(4, True)) == one
+    s = Integrator("sin", n=10**7 + 3, rule="mid", block=block, div="ieee").run().value
+    assert s == pytest.approx(2.0, abs=1e-12)
+    with pytest.raises(RuntimeError, match="64, 128, 256, 512 or 1024"):
+        Integrator("pi4", n=n, block=192)

@@ -47,12 +47,12 @@ GUARDED = {
     "pi4f32_series": ("riemann", CH + r"0ENS0_6Pi4F32EE", 192),
     "pi4f32_ieee": ("riemann", CH + r"1ENS0_6Pi4F32EE", 32),
     "poly7_series": ("riemann", CH + r"0ENS_4PolyILi7EEE", 64),
-    "table2d_stream_0_16": ("table", r"table2d_stream_kernelILi0ELi16EE", 0),
-    "table2d_stream_0_32": ("table", r"table2d_stream_kernelILi0ELi32EE", 0),
-    "table2d_stream_1_16": ("table", r"table2d_stream_kernelILi1ELi16EE", 0),
-    "table2d_stream_1_32": ("table", r"table2d_stream_kernelILi1ELi32EE", 0),
-    "table2d_stream_2_16": ("table", r"table2d_stream_kernelILi2ELi16EE", 0),
-    "table2d_stream_2_32": ("table", r"table2d_stream_kernelILi2ELi32EE", 0),
+    "table2d_stream_0_16": ("table", r"table2d_stream_kernelILi0ELi16ELb0EE", 0),
+    "table2d_stream_0_32": ("table", r"table2d_stream_kernelILi0ELi32ELb0EE", 0),
+    "table2d_stream_1_16": ("table", r"table2d_stream_kernelILi1ELi16ELb0EE", 0),
+    "table2d_stream_1_32": ("table", r"table2d_stream_kernelILi1ELi32ELb0EE", 0),
+    "table2d_stream_2_16": ("table", r"table2d_stream_kernelILi2ELi16ELb0EE", 0),
+    "table2d_stream_2_32": ("table", r"table2d_stream_kernelILi2ELi32ELb0EE", 0),
 }
 
 

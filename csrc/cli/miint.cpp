@@ -246,6 +246,7 @@ int main(int argc, char** argv) {
       c.grid = static_cast<int>(a.integer("grid", 4096));
       c.bucket = !a.flag("no-bucket");  // one all-reduce per graph replay of kGraphSteps
       c.chain = !a.flag("no-chain");    // graph replays: chained launches, no per-launch tail
+      c.step_streams = static_cast<int>(a.integer("step-streams", 0));  // chains per replay
       // --slice R/W: time only rank R's rows of a W-GPU split, on this GPU (no collective)
       const std::string sl = a.str("slice", "");
       if (!sl.empty()) {
@@ -256,6 +257,7 @@ int main(int argc, char** argv) {
       }
       double value = 0.0, timed = 0.0, ms = 0.0;
       bool bucketed = false, chained = false;
+      int streams = 1;
       std::mutex mu;
       cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
         Table2DPlan plan(c, dev, comm);
@@ -267,12 +269,14 @@ int main(int argc, char** argv) {
           timed = plan.last_result();
           bucketed = plan.bucketed() && graphs;
           chained = plan.chained() && graphs;
+          streams = chained ? plan.step_streams() : 1;
         }
         if (t > ms) ms = t;
       });
       if (topo.rank0 == 0) {
         cli::JsonRecord r;
         r.add("program", "table2d").add("grid", c.grid);
+        r.add("step_streams", streams);
         if (c.world > 1) {
           r.add("slice", std::to_string(c.rank) + "/" + std::to_string(c.world))
               .add("partial", value);

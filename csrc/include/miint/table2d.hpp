@@ -16,6 +16,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <memory>
+#include <vector>
+
 #include "miint/comm.hpp"
 #include "miint/kernels.hpp"
 #include "miint/runtime.hpp"
@@ -36,7 +39,16 @@ struct Table2DConfig {
   // Graph timing: chained launches (launch j's workgroup 0 closes launch j-1's partials,
   // one finalize closes the replay) instead of the fused hand-off tail in every launch.
   bool chain = true;
+  // Chained graph timing: the kGraphSteps integrations of a replay are dealt round-robin to
+  // this many streams, each its own chain (integrations are independent: own partials, own
+  // result), so one launch's staging latency and tail overlap the next one's work. 0 = auto
+  // (kAutoT2Streams); 1 = one chain on the plan's stream.
+  int step_streams = 0;
 };
+// 4096^2 on one MI355X, us per integration by chains 1/2/3/4/8 (two runs each, settled
+// clocks; profiles/r3/t2d_streams.jsonl): whole field 8.51 / 6.7-6.9 / 7.1 / 7.5-7.6 / 7.3-7.5;
+// a 1/8 row slice (the per-GPU share at 8 GPUs) 4.2 / 3.1-4.7 / 3.9-6.7 / 4.1-4.3 / 4.5-4.8.
+constexpr int kAutoT2Streams = 2;
 
 class Table2DPlan {
  public:
@@ -53,6 +65,8 @@ class Table2DPlan {
   bool bucketed() const { return bucketed_; }
   bool chained() const { return cfg_.chain && (!comm_ || world_ == 1 || bucketed_); }
   static constexpr int kGraphSteps = 32;
+  static constexpr double kSettleMs = 30.0;  // graph time(): warm-up replays before timing
+  int step_streams() const;  // chains a chained replay runs (1 when not chained)
   int row0() const { return row0_; }
   int row1() const { return row1_; }
 
@@ -67,6 +81,9 @@ class Table2DPlan {
   bool bucketed_ = false;
   bool last_batched_ = false;  // the last time() left kGraphSteps results in host_
   Stream stream_;
+  std::vector<Stream> lanes_;  // streams 1.. of a multi-stream chained replay
+  std::vector<std::unique_ptr<Event>> ev_join_;
+  Event ev_fork_{false};
   DeviceBuffer<double> v_, table_, partials_, chain_, result_;
   DeviceBuffer<unsigned int> ticket_;
   PinnedBuffer<double> host_;

@@ -32,7 +32,13 @@ Table2DPlan::Table2DPlan(const Table2DConfig& cfg, int device, const Comm* comm)
   const Table2DParams p{table_.get(), n, n, cfg.extent, cfg.extent, cfg.grid, cfg.grid,
                         row0_, std::max(row1_, row0_ + 1)};
   partials_ = DeviceBuffer<double>(static_cast<size_t>(table2d_grid(p)));
-  chain_ = DeviceBuffer<double>(2 * partials_.size());  // chained launches' double buffer
+  const int L = step_streams();
+  // chained launches: a double buffer per chain
+  chain_ = DeviceBuffer<double>(2 * static_cast<size_t>(L) * partials_.size());
+  for (int l = 1; l < L; ++l) {
+    lanes_.emplace_back();
+    ev_join_.emplace_back(new Event(false));
+  }
   fill_unset_slots(partials_.get(), partials_.size(), stream_.get());  // fused kernel's slots
   bucketed_ = cfg.bucket && comm_ && world_ > 1;
   result_ = DeviceBuffer<double>(kGraphSteps);
@@ -40,6 +46,12 @@ Table2DPlan::Table2DPlan(const Table2DConfig& cfg, int device, const Comm* comm)
   MIINT_HIP(hipMemset(ticket_.get(), 0, ticket_.bytes()));
   host_ = PinnedBuffer<double>(kGraphSteps);
   stream_.sync();
+}
+
+int Table2DPlan::step_streams() const {
+  if (!chained()) return 1;
+  return std::max(1, std::min(kGraphSteps, cfg_.step_streams > 0 ? cfg_.step_streams
+                                                                  : kAutoT2Streams));
 }
 
 void Table2DPlan::launch_local(double* out, hipStream_t s) {
@@ -96,16 +108,35 @@ double Table2DPlan::time(int iters, bool graphs) {
       if (row1_ <= row0_) {  // more ranks than rows
         MIINT_HIP(hipMemsetAsync(outs, 0, kGraphSteps * sizeof(double), cs));
       } else if (chained()) {
+        // integration i runs on chain i % L as that chain's step i / L: launch j of a chain
+        // closes the chain's launch j - 1 (its workgroup 0), a finalize closes each chain,
+        // and the plan's stream joins them all
         const int n = static_cast<int>(oracle::profile_table().size());
         const Table2DParams p{table_.get(), n, n, cfg_.extent, cfg_.extent, cfg_.grid,
                               cfg_.grid, row0_, row1_};
         const size_t nb = partials_.size();
-        for (int i = 0; i < kGraphSteps; ++i)
-          launch_table2d_chained(p, chain_.get() + (i & 1) * nb,
-                                 i ? chain_.get() + ((i - 1) & 1) * nb : nullptr,
-                                 i ? outs + i - 1 : nullptr, cs);
-        launch_table2d_finalize(chain_.get() + ((kGraphSteps - 1) & 1) * nb,
-                                static_cast<int>(nb), outs + kGraphSteps - 1, cs);
+        const int L = 1 + static_cast<int>(lanes_.size());
+        auto lane = [&](int l) { return l == 0 ? cs : lanes_[static_cast<size_t>(l - 1)].get(); };
+        auto half = [&](int l, int j) {
+          return chain_.get() + (2 * static_cast<size_t>(l) + static_cast<size_t>(j & 1)) * nb;
+        };
+        if (L > 1) {
+          ev_fork_.record(cs);
+          for (int l = 1; l < L; ++l) MIINT_HIP(hipStreamWaitEvent(lane(l), ev_fork_.get(), 0));
+        }
+        for (int i = 0; i < kGraphSteps; ++i) {
+          const int l = i % L, j = i / L;
+          launch_table2d_chained(p, half(l, j), j ? half(l, j - 1) : nullptr,
+                                 j ? outs + i - L : nullptr, lane(l));
+        }
+        for (int l = 0; l < L; ++l) {
+          const int last = l + ((kGraphSteps - 1 - l) / L) * L;
+          launch_table2d_finalize(half(l, last / L), static_cast<int>(nb), outs + last, lane(l));
+          if (l > 0) {
+            ev_join_[static_cast<size_t>(l - 1)]->record(lane(l));
+            MIINT_HIP(hipStreamWaitEvent(cs, ev_join_[static_cast<size_t>(l - 1)]->get(), 0));
+          }
+        }
       } else {
         for (int i = 0; i < kGraphSteps; ++i) launch_local(outs + i, cs);
       }
@@ -116,7 +147,15 @@ double Table2DPlan::time(int iters, bool graphs) {
       }
     });
   const int launches = std::max(1, (iters + kGraphSteps - 1) / kGraphSteps);
-  launch_with(gc, graph_, s);  // warm
+  // Warm-up: from idle the GPU needs ~25 ms of continuous work to reach steady clocks
+  // (profiles/r1/clock_ramp.jsonl) and one replay here is 0.1-0.3 ms, so replay for about
+  // kSettleMs first. Every replay of a collective plan holds collectives, so the count must
+  // be the same on every rank: it comes from the plan's size (an estimate of the replay
+  // time: ~0.5 ps per sample, >= 3 us per integration), not from a measurement.
+  const double samples = static_cast<double>(cfg_.grid) * cfg_.grid / world_;
+  const double est_replay_ms = kGraphSteps * std::max(3e-3, samples * 5e-10);
+  const int warm = std::max(1, static_cast<int>(kSettleMs / est_replay_ms));
+  for (int i = 0; i < warm; ++i) launch_with(gc, graph_, s);
   e0_.record(s);
   for (int i = 0; i < launches; ++i) launch_with(gc, graph_, s);
   e1_.record(s);

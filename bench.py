@@ -601,6 +601,18 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
                                  "verified": bool(rd <= 1e-9 and
                                                   result_ok("pi4", args.rule, "fp32", n_total, e))}
         del f32
+        # ... and with fp32 accumulation down to the workgroup partial (fp32 lane sums,
+        # v_add_f32_dpp wave reduction, fp32 LDS step): the all-fp32 reduction the config
+        # names, kept as the measured alternative (bound: fp32-level agreement, 1e-6)
+        fa = Integrator("pi4", n=n_total, div=args.div, **dict(kw, dtype="fp32acc"))
+        ms = _timed_steps(ctx, fa.plan, steps, pipeline, dev)
+        v = fa.plan.host_result(fa.plan.host_index_of(steps - 1, True))
+        e, rd = abs(v - math.pi), abs(v - ref) / abs(ref)
+        out["baseline4_fp32_accum32"] = {"value": n_total / (ms * 1e-3), "ms_per_step": ms,
+                                         "steps": steps, "result": v, "abs_err": e,
+                                         "rel_diff_vs_fp64": rd, "dtype": "fp32",
+                                         "accum": "fp32", "verified": bool(rd <= 1e-6)}
+        del fa
     # (7) BASELINE config #1: the serial CPU sum at N = 1e6 (the reference's plumbing case),
     #     on one host thread of the native host engine
     if pi4:

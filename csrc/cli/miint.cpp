@@ -48,7 +48,7 @@ RiemannConfig make_cfg(const std::string& integ, double n, const std::string& dt
   c.b = c.integrand == Integrand::kPi4 || c.integrand == Integrand::kPoly ? 1.0
       : c.integrand == Integrand::kSin ? 3.14159265358979323846 : 1800.0;
   c.n = static_cast<uint64_t>(n);
-  c.dtype = dtype == "fp32" ? DType::kF32 : DType::kF64;
+  c.dtype = dtype == "fp32" ? DType::kF32 : (dtype == "fp32acc" ? DType::kF32Acc32 : DType::kF64);
   c.rule = rule == "mid" ? Rule::kMid : (rule == "right" ? Rule::kRight : Rule::kLeft);
   c.div = div == "ieee" ? DivMode::kIeee : DivMode::kSeries;
   if (c.integrand == Integrand::kTrainVel) { c.p0 = oracle::kTrainTs; c.p1 = oracle::kTrainVs; }
@@ -57,7 +57,8 @@ RiemannConfig make_cfg(const std::string& integ, double n, const std::string& dt
   return c;
 }
 
-BenchRow bench_one(const cli::Topology& topo, RiemannConfig cfg, int iters, bool graphs) {
+BenchRow bench_one(const cli::Topology& topo, RiemannConfig cfg, int iters, bool graphs,
+                   int settle_steps = -1) {
   BenchRow row;
   row.n = static_cast<double>(cfg.n);
   row.gpus = topo.world;
@@ -69,7 +70,8 @@ BenchRow bench_one(const cli::Topology& topo, RiemannConfig cfg, int iters, bool
     // Clock settle (see bench.py): ~60 ms of back-to-back steps before timing. The count is
     // a function of the rank's sample count only, so every rank issues the same collectives.
     const double est_s = static_cast<double>(plan.count()) / 1.3e13;
-    const int settle = static_cast<int>(std::min(20000.0, std::max(3.0, 0.06 / est_s)));
+    const int settle = settle_steps >= 0 ? settle_steps
+                       : static_cast<int>(std::min(20000.0, std::max(3.0, 0.06 / est_s)));
     plan.run_steps(settle, comm != nullptr, graphs);
     StepTiming t = plan.run_steps(iters, comm != nullptr, graphs);
     std::lock_guard<std::mutex> g(mu);
@@ -233,9 +235,14 @@ int main(int argc, char** argv) {
       c.grid = static_cast<int>(a.integer("grid", 0));
       c.block = static_cast<int>(a.integer("block", kRiemannBlock));
       c.step_streams = static_cast<int>(a.integer("step-streams", 0));
+      // validation / A-B: kIeee sin and cos by ocml per sample instead of fast_trig.hpp
+      if (a.flag("trig-library")) set_trig_library(true);
       MIINT_CHECK(riemann_block_ok(c.block), "--block must be 64, 128, 256, 512 or 1024");
       c.waves_per_cu = static_cast<int>(a.integer("waves-per-cu", 32));
-      const BenchRow r = bench_one(topo, c, iters, graphs);
+      // --settle N: untimed steps before the timed ones (default: ~60 ms worth; profiler
+      // runs pass a few, so the trace holds little more than the timed dispatches)
+      const BenchRow r = bench_one(topo, c, iters, graphs,
+                                   static_cast<int>(a.integer("settle", -1)));
       if (topo.rank0 == 0)
         print_row(a, r, a.str("integrand", "pi4").c_str(), a.str("dtype", "fp64").c_str(),
                   a.str("rule", "left").c_str());
@@ -247,6 +254,8 @@ int main(int argc, char** argv) {
       c.bucket = !a.flag("no-bucket");  // one all-reduce per graph replay of kGraphSteps
       c.chain = !a.flag("no-chain");    // graph replays: chained launches, no per-launch tail
       c.step_streams = static_cast<int>(a.integer("step-streams", 0));  // chains per replay
+      c.min_wg = static_cast<int>(a.integer("min-wg", 0));
+      c.settle_ms = a.num("settle-ms", c.settle_ms);
       // --slice R/W: time only rank R's rows of a W-GPU split, on this GPU (no collective)
       const std::string sl = a.str("slice", "");
       if (!sl.empty()) {

@@ -219,7 +219,10 @@ int main(int argc, char** argv) {
     cfg.b = hi;
     cfg.n = n;
     cfg.rule = parse_rule(a.str("rule", "left"));
-    cfg.dtype = a.str("dtype", "fp64") == "fp32" ? DType::kF32 : DType::kF64;
+    const std::string dts = a.str("dtype", "fp64");
+    MIINT_CHECK(dts == "fp64" || dts == "fp32" || dts == "fp32acc",
+                "--dtype must be fp64|fp32|fp32acc");
+    cfg.dtype = dts == "fp32" ? DType::kF32 : (dts == "fp32acc" ? DType::kF32Acc32 : DType::kF64);
     cfg.div = a.str("div", "series") == "ieee" ? DivMode::kIeee : DivMode::kSeries;
     cfg.fused = !a.flag("unfused");
     // --block: threads per workgroup (the reference's SP, cintegrate.cu:17-18); --grid:

@@ -14,7 +14,12 @@
 
 namespace miint {
 
-enum class DType : int { kF64 = 0, kF32 = 1 };
+// kF32Acc32: the fp32 sample path with fp32 accumulation down to the workgroup partial
+// (lane sums, v_add_f32_dpp wave reduction, LDS block step; the partials meet in fp64) —
+// the all-fp32 reduction BASELINE #4 names, measured against kF32's fp64 fold. 4/(1+x^2)
+// only.
+enum class DType : int { kF64 = 0, kF32 = 1, kF32Acc32 = 2 };
+inline bool is_fp32(DType t) { return t == DType::kF32 || t == DType::kF32Acc32; }
 
 // Tile (unroll) size of the Riemann kernels: U consecutive samples per lane per step.
 constexpr int kRiemannTile = 32;     // default samples per lane tile (Pi4 series: 64)
@@ -52,7 +57,7 @@ constexpr int kPolySeriesMaxCoeffs = 8;  // polynomials up to degree 7 have a se
 // coefficient count (Taylor-pair tiles for up
 // to kPolySeriesMaxCoeffs coefficients, exact for any h; Horner per sample otherwise).
 inline DivMode effective_div(DivMode d, double h, Integrand f, DType t, int ncoef = 0) {
-  if (t == DType::kF32) {  // fp32: one series form per integrand (integrands_f32.hpp)
+  if (is_fp32(t)) {  // fp32: one series form per integrand (integrands_f32.hpp)
     if (d == DivMode::kIeee) return DivMode::kIeee;
     if (f == Integrand::kPi4) return series_ok(h) ? DivMode::kSeries : DivMode::kIeee;
     if (f == Integrand::kPoly)
@@ -192,6 +197,7 @@ struct Table2DParams {
   double X, Y;       // physical extents
   int gx, gy;        // sample grid
   int row0, row1;    // sample rows owned by this launch
+  int min_wg = 0;    // row stream: fewest workgroups to aim for (0 = 512)
 };
 int table2d_grid(const Table2DParams& p);
 // Which kernel a launch runs: "stream" (LDS footprint + row streaming, fine grids) or

@@ -44,6 +44,8 @@ struct Table2DConfig {
   // result), so one launch's staging latency and tail overlap the next one's work. 0 = auto
   // (kAutoT2Streams); 1 = one chain on the plan's stream.
   int step_streams = 0;
+  int min_wg = 0;  // row stream: fewest workgroups its shape aims for (0 = kernel default)
+  double settle_ms = 30.0;  // graph time(): untimed warm-up replays first (steady clocks)
 };
 // 4096^2 on one MI355X, us per integration by chains 1/2/3/4/8 (two runs each, settled
 // clocks; profiles/r3/t2d_streams.jsonl): whole field 8.51 / 6.7-6.9 / 7.1 / 7.5-7.6 / 7.3-7.5;
@@ -65,7 +67,6 @@ class Table2DPlan {
   bool bucketed() const { return bucketed_; }
   bool chained() const { return cfg_.chain && (!comm_ || world_ == 1 || bucketed_); }
   static constexpr int kGraphSteps = 32;
-  static constexpr double kSettleMs = 30.0;  // graph time(): warm-up replays before timing
   int step_streams() const;  // chains a chained replay runs (1 when not chained)
   int row0() const { return row0_; }
   int row1() const { return row1_; }

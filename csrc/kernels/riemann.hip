@@ -52,8 +52,13 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
 //    counter, no per-tile VALU compare) and only one extra round is exec-masked.
 //  * The tile's anchor index is carried as an exact double (integers < 2^53 are exact), so
 //    a round costs one v_add_f64 + one v_fma_f64 for its coordinate.
+// Accumulator type of a functor's lane sums and block reduction: fp64 everywhere except the
+// all-fp32 variant (Pi4F32Acc32: fp32 lanes, v_add_f32_dpp wave sums, fp32 LDS step).
+template <class F> struct AccOf { using type = double; };
+
 template <DivMode M, class F>
-__device__ __forceinline__ double lane_sum(const RiemannParams& p, const F& f) {
+__device__ __forceinline__ typename AccOf<F>::type lane_sum(const RiemannParams& p, const F& f) {
+  using Acc = typename AccOf<F>::type;
   constexpr int T = F::template tile_len<M>();
   const uint64_t bs = blockDim.x;
   const uint64_t lanes = static_cast<uint64_t>(gridDim.x) * bs;
@@ -65,14 +70,14 @@ __device__ __forceinline__ double lane_sum(const RiemannParams& p, const F& f) {
   const double base = static_cast<double>(p.i_begin) + p.off;
   const double istep = static_cast<double>(lanes * T);
   double ib = base + static_cast<double>(gid * T) + F::template anchor<T, M>();
-  double acc = 0.0;
+  Acc acc = 0;
   uint64_t r = 0;
   for (; r < r_all; ++r, ib += istep) acc = f.template tile_acc<T, M>(fma(ib, p.h, p.a), p.h, acc);
   if (r < r_any && r < rounds) acc = f.template tile_acc<T, M>(fma(ib, p.h, p.a), p.h, acc);
   // remainder (< T samples): one per lane (a grid of fewer lanes than T loops)
   const uint64_t done = ntile * T;
   for (uint64_t k = gid; k < p.n - done; k += lanes)
-    acc += f.point(fma(base + static_cast<double>(done + k), p.h, p.a));
+    acc += static_cast<Acc>(f.point(fma(base + static_cast<double>(done + k), p.h, p.a)));
   return acc;
 }
 
@@ -238,6 +243,70 @@ struct Pi4F32Wide : Pi4F32 {
 };
 constexpr double kPi4F32NarrowMaxX = 0x1p49;
 
+// The same samples as Pi4F32, accumulated in fp32 all the way to the workgroup partial
+// (DType::kF32Acc32): the tile value s (U + sum e) is formed and added in fp32, lanes reduce
+// with v_add_f32_dpp and the block step runs in fp32. What this drops is the fp64 fold
+// Pi4F32 keeps (see Pi4F32::tile_acc): measured against it in profiles/r3/fp32_accum.jsonl.
+struct Pi4F32Acc32 : Pi4F32 {
+  template <int UU, DivMode M>
+  __device__ __forceinline__ float tile_acc(double xmd, double h, float acc) const {
+    if constexpr (M == DivMode::kSeries) {
+      static_assert(UU == kSubs * kSubLen, "fp32 series tiles are kSubs 32-sample sub-tiles");
+      const float xm = static_cast<float>(xmd);
+      const float hf = static_cast<float>(h);
+      const float dm = fmaf(xm, xm, 1.0f);
+      float s = __builtin_amdgcn_rcpf(dm);
+      s = fmaf(s, fmaf(-dm, s, 1.0f), s);
+      const float em = fmaf(-dm, s, 1.0f);
+      const float a = (-2.0f * hf) * xm * s;
+      const float b = -(hf * hf) * s;
+      const f32x2 bb = {b, b};
+      const f32x2 aa = {a, a};
+      const f32x2 emv = {em, em};
+      f32x2 ecs[kSubs / 2], aqs[kSubs / 2];
+#pragma unroll
+      for (int p2 = 0; p2 < kSubs / 2; ++p2) {
+        const f32x2 c0v = {(2 * p2 - 0.5f * (kSubs - 1)) * kSubLen,
+                           (2 * p2 + 1 - 0.5f * (kSubs - 1)) * kSubLen};
+        ecs[p2] = pk_fma(c0v, pk_fma(c0v, bb, aa), emv);
+        aqs[p2] = pk_fma(c0v + c0v, bb, aa);
+      }
+      f32x2 t;
+#pragma unroll
+      for (int q = 0; q < kSubs; ++q) {
+        const float ec = (q & 1) ? ecs[q / 2].y : ecs[q / 2].x;
+        const float aq = (q & 1) ? aqs[q / 2].y : aqs[q / 2].x;
+        const f32x2 av = {aq, aq};
+        f32x2 cc = pk_fma(f32x2{0.25f, 2.25f}, bb, f32x2{ec, ec});
+#pragma unroll
+        for (int j = 0; j < kSubLen / 2; j += 2) {
+          const f32x2 k0 = {j + 0.5f, -(j + 0.5f)};
+          const f32x2 k1 = {j + 1.5f, -(j + 1.5f)};
+          const f32x2 e0 = pk_fma(k0, av, f32x2{cc.x, cc.x});
+          t = (q == 0 && j == 0) ? e0 : t + e0;
+          t += pk_fma(k1, av, f32x2{cc.y, cc.y});
+          if (j + 2 < kSubLen / 2)
+            cc = pk_fma(f32x2{4.0f * j + 6.0f, 4.0f * j + 10.0f}, bb, cc);
+        }
+      }
+      return fmaf(s, static_cast<float>(UU) + (t.x + t.y), acc);  // all fp32
+    } else {
+      const float x0 = static_cast<float>(xmd);
+      const float hf = static_cast<float>(h);
+      const f32x2 xb = {x0, x0}, hh = {hf, hf}, one = {1.0f, 1.0f};
+      f32x2 a2 = {0.0f, 0.0f};
+#pragma unroll
+      for (int u = 0; u < UU; u += 2) {
+        const f32x2 uu = {static_cast<float>(u), static_cast<float>(u + 1)};
+        const f32x2 x = pk_fma(uu, hh, xb);
+        a2 += recip_narrow(pk_fma(x, x, one));
+      }
+      return acc + (a2.x + a2.y);
+    }
+  }
+};
+template <> struct AccOf<Pi4F32Acc32> { using type = float; };
+
 // The host's series validity check (series_ok: kSeriesHalfSpan * h <= 2e-6) must bound the
 // farthest sample offset of both Pi4 series tiles.
 static_assert(2 * AngleSeries<12>::kPairs + 12 == kSinTrig, "trig table sized for Sin");
@@ -264,6 +333,12 @@ template <> struct Maker<Pi4Wide> {
 template <> struct Maker<Pi4F32Wide> {
   static constexpr int kLds = 1;
   __device__ static Pi4F32Wide make(const RiemannParams&, const double*, int, double*) {
+    return {};
+  }
+};
+template <> struct Maker<Pi4F32Acc32> {
+  static constexpr int kLds = 1;
+  __device__ static Pi4F32Acc32 make(const RiemannParams&, const double*, int, double*) {
     return {};
   }
 };
@@ -409,7 +484,9 @@ __device__ __forceinline__ F make_functor(const RiemannParams& p, const double* 
 template <DivMode M, class F>
 constexpr bool occupancy_hint() {
   if constexpr (__is_same(F, Pi4)) return M == DivMode::kSeriesDirect;
-  else if constexpr (__is_same(F, Pi4F32) || __is_same(F, Pi4F32Wide)) return M == DivMode::kIeee;
+  else if constexpr (__is_same(F, Pi4F32) || __is_same(F, Pi4F32Wide) ||
+                     __is_same(F, Pi4F32Acc32))
+    return M == DivMode::kIeee;
   else if constexpr (__is_same(F, SinLib) || __is_same(F, TrainVelLib)) return true;
   else if constexpr (__is_same(F, Sin)) return M == DivMode::kIeee;
   else if constexpr (__is_same(F, PolyF32<16>)) return true;
@@ -423,10 +500,11 @@ constexpr bool occupancy_hint() {
 template <DivMode M, class F>
 __device__ __forceinline__ void partials_body(const RiemannParams& p, const double* table,
                                               int table_n, double* partials) {
-  __shared__ double red[kMaxBlock / kWave];
+  using Acc = typename AccOf<F>::type;
+  __shared__ Acc red[kMaxBlock / kWave];
   __shared__ double lds[lds_words<M, F>()];
   const F f = make_functor<M, F>(p, table, table_n, lds);
-  const double s = block_sum_dyn(lane_sum<M>(p, f), red);
+  const double s = static_cast<double>(block_sum_dyn(lane_sum<M>(p, f), red));
   if (threadIdx.x == 0) partials[blockIdx.x] = s;
 }
 template <DivMode M, class F>
@@ -464,11 +542,15 @@ template <DivMode M, class F>
 __device__ __forceinline__ void fused_body(const RiemannParams& p, const double* table,
                                            int table_n, double* partials, unsigned int* ticket,
                                            double scale, double* out) {
+  using Acc = typename AccOf<F>::type;
   __shared__ double red[kMaxBlock / kWave];
+  __shared__ Acc red_acc[__is_same(Acc, double) ? 1 : kMaxBlock / kWave];
   __shared__ double lds[lds_words<M, F>()];
   __shared__ int is_last;
   const F f = make_functor<M, F>(p, table, table_n, lds);
-  const double s = block_sum_dyn(lane_sum<M>(p, f), red);
+  double s;
+  if constexpr (__is_same(Acc, double)) s = block_sum_dyn(lane_sum<M>(p, f), red);
+  else s = static_cast<double>(block_sum_dyn(lane_sum<M>(p, f), red_acc));
   if (!publish_and_ticket(s, partials, ticket, blockIdx.x, gridDim.x, &is_last)) return;
   const double v = ordered_partials<0, true>(partials, static_cast<int>(gridDim.x));
   rearm_slots<0>(partials, static_cast<int>(gridDim.x));
@@ -511,7 +593,13 @@ __device__ __forceinline__ void chained_body(const RiemannParams& p, const doubl
     __syncthreads();  // red is reused below
   }
   const F f = make_functor<M, F>(p, table, table_n, lds);
-  const double s = block_sum_dyn(lane_sum<M>(p, f), red);
+  double s;
+  if constexpr (__is_same(typename AccOf<F>::type, double)) {
+    s = block_sum_dyn(lane_sum<M>(p, f), red);
+  } else {
+    __shared__ typename AccOf<F>::type red_acc[kMaxBlock / kWave];
+    s = static_cast<double>(block_sum_dyn(lane_sum<M>(p, f), red_acc));
+  }
   if (threadIdx.x == 0) partials[blockIdx.x] = s;
 }
 template <DivMode M, class F>
@@ -637,6 +725,14 @@ inline bool pi4_narrow(const RiemannParams& p, double max_x = kPi4NarrowMaxX) {
 template <template <DivMode, class> class Op, class... A>
 void dispatch(const RiemannParams& p, DType dtype, DivMode m, A&&... a) {
   const Integrand f = static_cast<Integrand>(p.integrand);
+  if (dtype == DType::kF32Acc32) {
+    MIINT_CHECK(f == Integrand::kPi4, "fp32 accumulation (fp32acc) is implemented for pi4 only");
+    if (m == DivMode::kSeries) Op<DivMode::kSeries, Pi4F32Acc32>::run(a...);
+    else if (pi4_narrow(p, kPi4F32NarrowMaxX)) Op<DivMode::kIeee, Pi4F32Acc32>::run(a...);
+    else fail("fp32acc: coordinates beyond 2^49 need the wide division (use fp32)", __FILE__,
+              __LINE__);
+    return;
+  }
   if (dtype == DType::kF32) {
     const bool ser = m == DivMode::kSeries;
     switch (f) {

@@ -498,7 +498,7 @@ Table2DShape table2d_shape(const Table2DParams& p) {
       sh.rows_per_wave = r;
       sh.short_tile = span(4 * r, step_y) <= kSHShort;
       sh.grid = dim3(gxs, (rows + 4 * r - 1) / (4 * r));
-      if (nwg >= 512) break;
+      if (nwg >= (p.min_wg > 0 ? p.min_wg : 512)) break;
     }
     if (sh.stream) return sh;
   }

@@ -73,7 +73,10 @@ PYBIND11_MODULE(_miint, m) {
       .value("train", Integrand::kTrainVel)
       .value("table", Integrand::kTable);
   py::enum_<Rule>(m, "Rule").value("left", Rule::kLeft).value("mid", Rule::kMid).value("right", Rule::kRight);
-  py::enum_<DType>(m, "DType").value("fp64", DType::kF64).value("fp32", DType::kF32);
+  py::enum_<DType>(m, "DType")
+      .value("fp64", DType::kF64)
+      .value("fp32", DType::kF32)
+      .value("fp32acc", DType::kF32Acc32);
   py::enum_<DivMode>(m, "DivMode")
       .value("series", DivMode::kSeries)
       .value("ieee", DivMode::kIeee)

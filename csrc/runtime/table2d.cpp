@@ -30,7 +30,7 @@ Table2DPlan::Table2DPlan(const Table2DConfig& cfg, int device, const Comm* comm)
   MIINT_HIP(hipMemcpy(v_.get(), prof.data(), v_.bytes(), hipMemcpyHostToDevice));
   launch_outer_product(v_.get(), n, table_.get(), stream_.get());
   const Table2DParams p{table_.get(), n, n, cfg.extent, cfg.extent, cfg.grid, cfg.grid,
-                        row0_, std::max(row1_, row0_ + 1)};
+                        row0_, std::max(row1_, row0_ + 1), cfg.min_wg};
   partials_ = DeviceBuffer<double>(static_cast<size_t>(table2d_grid(p)));
   const int L = step_streams();
   // chained launches: a double buffer per chain
@@ -58,7 +58,7 @@ void Table2DPlan::launch_local(double* out, hipStream_t s) {
   const int n = static_cast<int>(oracle::profile_table().size());
   if (row1_ > row0_) {
     const Table2DParams p{table_.get(), n, n, cfg_.extent, cfg_.extent, cfg_.grid, cfg_.grid,
-                          row0_, row1_};
+                          row0_, row1_, cfg_.min_wg};
     launch_table2d_fused(p, partials_.get(), ticket_.get(), out, s);
   } else {
     MIINT_HIP(hipMemsetAsync(out, 0, sizeof(double), s));  // more ranks than rows
@@ -113,7 +113,7 @@ double Table2DPlan::time(int iters, bool graphs) {
         // and the plan's stream joins them all
         const int n = static_cast<int>(oracle::profile_table().size());
         const Table2DParams p{table_.get(), n, n, cfg_.extent, cfg_.extent, cfg_.grid,
-                              cfg_.grid, row0_, row1_};
+                              cfg_.grid, row0_, row1_, cfg_.min_wg};
         const size_t nb = partials_.size();
         const int L = 1 + static_cast<int>(lanes_.size());
         auto lane = [&](int l) { return l == 0 ? cs : lanes_[static_cast<size_t>(l - 1)].get(); };
@@ -149,12 +149,12 @@ double Table2DPlan::time(int iters, bool graphs) {
   const int launches = std::max(1, (iters + kGraphSteps - 1) / kGraphSteps);
   // Warm-up: from idle the GPU needs ~25 ms of continuous work to reach steady clocks
   // (profiles/r1/clock_ramp.jsonl) and one replay here is 0.1-0.3 ms, so replay for about
-  // kSettleMs first. Every replay of a collective plan holds collectives, so the count must
+  // cfg_.settle_ms first. Every replay of a collective plan holds collectives, so the count must
   // be the same on every rank: it comes from the plan's size (an estimate of the replay
   // time: ~0.5 ps per sample, >= 3 us per integration), not from a measurement.
   const double samples = static_cast<double>(cfg_.grid) * cfg_.grid / world_;
   const double est_replay_ms = kGraphSteps * std::max(3e-3, samples * 5e-10);
-  const int warm = std::max(1, static_cast<int>(kSettleMs / est_replay_ms));
+  const int warm = std::max(1, static_cast<int>(cfg_.settle_ms / est_replay_ms));
   for (int i = 0; i < warm; ++i) launch_with(gc, graph_, s);
   e0_.record(s);
   for (int i = 0; i < launches; ++i) launch_with(gc, graph_, s);

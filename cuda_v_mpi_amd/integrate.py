@@ -80,8 +80,8 @@ class Integrator:
             raise ValueError("n must be >= 1")
         if rule not in ("left", "mid", "right"):
             raise ValueError("rule must be left|mid|right")
-        if dtype not in ("fp64", "fp32"):
-            raise ValueError("dtype must be fp64|fp32")
+        if dtype not in ("fp64", "fp32", "fp32acc"):
+            raise ValueError("dtype must be fp64|fp32|fp32acc")
         self.spec, self.n, self.rule, self.dtype, self.div = spec, int(n), rule, dtype, div
         self.backend, self.comm_kind = backend, comm
         if comm_obj is not None:  # an existing native communicator (e.g. a loopback rank)

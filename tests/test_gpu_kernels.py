@@ -741,3 +741,19 @@ def test_table_far_domain_beyond_int_range(cuda, a, dtype, div):
     want = _ref_sum(spec, n, rule="mid")
     assert math.isfinite(got)
     assert got == pytest.approx(want, rel=1e-9 if dtype == "fp64" else 1e-5)
+
+
+@pytest.mark.parametrize("rule", ["left", "mid"])
+def test_fp32_accumulation_policy(cuda, rule):
+    """fp32 samples folded into fp64 lane sums (dtype fp32, the default) against fp32 lane
+    sums + v_add_f32_dpp wave reduction + fp32 block step (fp32acc): both agree with the fp64
+    value to fp32 level, and the fp64 fold is the more accurate of the two (why it is the
+    default; profiles/r3/fp32_accum.jsonl has the times)."""
+    spec = integrands.pi4()
+    n = 10**9
+    ref = float(kernels.riemann(spec, n, rule=rule).item())
+    fold = float(kernels.riemann(spec, n, rule=rule, dtype="fp32").item())
+    acc32 = float(kernels.riemann(spec, n, rule=rule, dtype="fp32acc").item())
+    assert abs(fold - ref) / ref <= 1e-9
+    assert abs(acc32 - ref) / ref <= 1e-6
+    assert abs(fold - ref) < abs(acc32 - ref)

@@ -14,22 +14,30 @@ G2="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_LDS_
 G3="FETCH_SIZE GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"
 G4="WRITE_SIZE GRBM_GUI_ACTIVE SQ_LDS_UNALIGNED_STALL SQ_INSTS_FLAT"
 
+# ONLY="name1 name2": run just those workloads (default: all)
+want() { [ -z "${ONLY:-}" ] || [[ " $ONLY " == *" $1 "* ]]; }
 run() {  # name, group-name, counters, command...
   local name=$1 gname=$2 ctrs=$3; shift 3
+  want "$name" || return 0
   timeout -k 10 300 rocprofv3 --pmc $ctrs --kernel-trace --output-format csv \
     -d "$OUT/${name}_${gname}" -o run -- "$@" > "$OUT/${name}_${gname}.log" 2>&1
 }
 
 for g in G1 G2; do
-  run pi4_series $g "${!g}" "$REPO/build/bin/miint" bench --iters 20
-  run pi4_ieee $g "${!g}" "$REPO/build/bin/miint" bench --iters 10 --div ieee
-  run pi4_fp32 $g "${!g}" "$REPO/build/bin/miint" bench --iters 20 --dtype fp32
-  run sin $g "${!g}" "$REPO/build/bin/miint" bench --iters 20 --integrand sin
-  run sin_ocml $g "${!g}" "$REPO/build/bin/miint" bench --iters 4 --integrand sin --div ieee
-  run train $g "${!g}" "$REPO/build/bin/miint" bench --iters 20 --integrand train
-  run poly $g "${!g}" "$REPO/build/bin/miint" bench --iters 10 --integrand poly
-  run table $g "${!g}" "$REPO/build/bin/miint" bench --iters 10 --integrand table
-  run table2d $g "${!g}" "$REPO/build/bin/miint" table2d
+  run pi4_series $g "${!g}" "$REPO/build/bin/miint" bench --iters 200 --settle 300
+  run pi4_fp32acc $g "${!g}" "$REPO/build/bin/miint" bench --iters 200 --settle 300 --dtype fp32acc
+  run sin_fast $g "${!g}" "$REPO/build/bin/miint" bench --iters 40 --settle 40 --integrand sin --div ieee
+  run train_fast $g "${!g}" "$REPO/build/bin/miint" bench --iters 40 --settle 40 --integrand train --div ieee
+  run table2d_slice8 $g "${!g}" "$REPO/build/bin/miint" table2d --slice 0/8 --iters 320 --settle-ms 20
+  run pi4_ieee $g "${!g}" "$REPO/build/bin/miint" bench --iters 20 --settle 60 --div ieee
+  run pi4_fp32 $g "${!g}" "$REPO/build/bin/miint" bench --iters 200 --settle 300 --dtype fp32
+  run sin $g "${!g}" "$REPO/build/bin/miint" bench --iters 200 --settle 300 --integrand sin
+  run sin_ocml $g "${!g}" "$REPO/build/bin/miint" bench --iters 4 --integrand sin --div ieee \
+    --trig-library --settle 16
+  run train $g "${!g}" "$REPO/build/bin/miint" bench --iters 200 --settle 300 --integrand train
+  run poly $g "${!g}" "$REPO/build/bin/miint" bench --iters 100 --settle 200 --integrand poly
+  run table $g "${!g}" "$REPO/build/bin/miint" bench --iters 200 --settle 300 --integrand table
+  run table2d $g "${!g}" "$REPO/build/bin/miint" table2d --iters 320 --settle-ms 20
   run dpp_selftest $g "${!g}" python3 "$REPO/tools/dpp_probe.py"
 done
 for g in G1 G2 G3 G4; do

@@ -40,9 +40,12 @@ def _elapsed() -> float:
 
 
 def _ctx(backend=None):
+    """Process group for the ranks (torchrun env). GPU runs reduce through the native RCCL
+    communicator, so their torch group is the gloo control plane (one RCCL communicator per
+    rank); host/cpu backends reduce over gloo itself."""
     from .parallel import dist as mdist
 
-    return mdist.init(backend=backend)
+    return mdist.init(backend=backend or mdist.control_backend("native"))
 
 
 def cmd_riemann(a) -> int:
@@ -50,8 +53,8 @@ def cmd_riemann(a) -> int:
 
     ctx = _ctx("gloo" if a.backend in ("cpu", "host") else None)
     spec_b = {"sin": math.pi, "pi4": 1.0}.get(a.integrand, None)
-    it = Integrator(a.integrand, n=int(a.n), rule=a.rule, dtype=a.dtype, ctx=ctx,
-                    backend=a.backend)
+    it = Integrator(a.integrand, n=int(a.n), rule=a.rule, dtype=a.dtype, div=a.div, ctx=ctx,
+                    backend=a.backend, block=a.block)
     r = it.run()
     if ctx.is_root:
         print(output.fmt_seconds(_elapsed()))
@@ -285,8 +288,10 @@ def main(argv=None) -> int:
         sp.add_argument("--integrand", default=integrand)
         sp.add_argument("--n", type=float, default=1e9)
         sp.add_argument("--rule", default="left", choices=["left", "mid", "right"])
-        sp.add_argument("--dtype", default="fp64", choices=["fp64", "fp32"])
+        sp.add_argument("--dtype", default="fp64", choices=["fp64", "fp32", "fp32acc"])
         sp.add_argument("--div", default="series", choices=["series", "ieee", "series_direct"])
+        sp.add_argument("--block", type=int, default=256, choices=[64, 128, 256, 512, 1024],
+                        help="threads per workgroup (the reference's SP)")
         sp.add_argument("--backend", default="hip", choices=["hip", "host", "cpu"])
         sp.add_argument("--json", action="store_true")
 

@@ -27,16 +27,25 @@ Warmup: the W warmup steps, then untimed repeats of the timed K-step pattern for
 
 Weak scaling: every GPU integrates its own 1e9-sample slice of a global N = 1e9 x n_gpus
 (N = 8e9 on 8 GPUs). The results of the last batch of timed steps (every rank holds the
-global sums) are checked on the host against pi. After the timed region (outside it) the
-record also gets: the same config with IEEE division per sample ("ieee_div"), the series
-path's per-point error against IEEE division on a 64 K-sample window ("per_point_max_ulp"),
-and the other BASELINE configs: #1, the serial CPU sum at N = 1e6 on one host thread
-("baseline1_serial_cpu_1e6"); #3, N = 1e10 in total strong-scaled over the same GPUs
-("baseline3_strong_1e10"); #4, the same integral through the packed-fp32 path
-("baseline4_fp32", with its difference from the fp64 value); #5, the 4096^2 2-D velocity
-field with its rows split over the same GPUs ("baseline5_table2d_4096") — and the same
-integral on the node's host cores (the native host engine, the reference's own CPU/MPI side:
-"host_engine").
+global sums) are checked on the host against the rule's closed-form truncation error. After
+the timed region (outside it) the same ranks also measure, each with its own graphs, timing
+and pass/fail ("verified"): the metric's own config, N = 1e9 IN TOTAL split over the GPUs as
+the reference splits its fixed STEPS over its workers ("strong_1e9", riemann.cpp:10,71-73);
+the same config with IEEE division per sample ("ieee_div"); the series path's per-point
+error against IEEE division on a 64 K-sample window ("per_point"); and the other BASELINE
+configs: #1, the serial CPU sum at N = 1e6 on one host thread ("baseline1_serial_cpu_1e6");
+#3, N = 1e10 in total strong-scaled over the same GPUs ("baseline3_strong_1e10"); #4, the
+same integral through the packed-fp32 path ("baseline4_fp32", tile values folded in fp64,
+and "baseline4_fp32_accum32", fp32 accumulation to the workgroup partial); #5, the 4096^2
+2-D velocity field with its rows split over the same GPUs ("baseline5_table2d_4096") — and
+the same integral on the node's host cores (the native host engine, the reference's own
+CPU/MPI side: "host_engine"). The record's "verified" is the AND of the headline's and every
+extra's; the exit status follows the headline's.
+
+One RCCL communicator per rank: with --comm native (default) the torch process group is gloo
+and carries only the control plane (barriers, the settle-count MAX, the per-rank times); the
+native communicator is shared by every plan of the run. The record says which
+("control_plane", "torch_nccl_groups").
 """
 from __future__ import annotations
 
@@ -89,7 +98,9 @@ def parse(argv=None) -> argparse.Namespace:
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--no-pipeline", action="store_true")
     p.add_argument("--unfused", action="store_true", help="partials + finalize (2 launches)")
-    p.add_argument("--grid", type=int, default=0)
+    p.add_argument("--grid", type=int, default=0, help="workgroups (0 = auto; the reference's SM)")
+    p.add_argument("--block", type=int, default=256, choices=[64, 128, 256, 512, 1024],
+                   help="threads per workgroup (the reference's SP)")
     p.add_argument("--slots", type=int, default=48,
                    help="steps per captured graph batch (= steps per bucketed all-reduce)")
     p.add_argument("--step-streams", type=int, default=0,
@@ -216,7 +227,7 @@ def main(argv=None) -> int:
                           div=args.div, backend="cpu" if cpu else "hip", ctx=ctx, comm=comm,
                           fused=not args.unfused, grid=args.grid, slots=args.slots,
                           force_collective=args.force_collective, bucket=not args.no_bucket,
-                          step_streams=args.step_streams)
+                          step_streams=args.step_streams, block=args.block)
 
     # A native RCCL communicator that fails to come up on every rank (the failure is agreed
     # over the torch process group, so all ranks switch together) falls back to the
@@ -407,6 +418,7 @@ def main(argv=None) -> int:
                 "step_streams": plan.step_streams(min(args.steps, plan.slots))
                 if plan is not None else 1,
                 "grid": plan.grid if plan is not None else 0,
+                "block": plan.block if plan is not None else args.block,
                 "device": args.device,
             },
         }

@@ -198,3 +198,18 @@ def test_bench_verification_bounds():
     assert bench.result_ok("pi4", "left", "fp32", 10**9, 1.0195799760026603e-09)
     assert not bench.result_ok("pi4", "left", "fp32", 10**9, 3 * h)
     assert not bench.result_ok("pi4", "left", "fp64", 10**9, float("nan"))
+
+
+def test_bench_eight_rank_rehearsal():
+    """The driver's 8-GPU scaling run, rehearsed on the CPU: 8 spawned rank processes, the gloo
+    control plane (no torch RCCL group), one time per rank, MAX over ranks, weak N = 8 x
+    per-rank samples, every rank's result verified."""
+    p = _bench("--gpus", "8", "--device", "cpu", "--samples", "8e4", "--steps", "2",
+               "--warmup", "1", "--settle-ms", "0", timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    js = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert js["n_gpus"] == 8 and len(js["per_rank_ms"]) == 8
+    assert js["control_plane"] == "gloo" and js["torch_nccl_groups"] == 0
+    assert js["config"]["N"] == 8 * 80_000 and js["config"]["parallelism"] == "dp8"
+    assert js["ms_per_step"] == pytest.approx(max(js["per_rank_ms"]))
+    assert js["verified"]

@@ -12,7 +12,12 @@ run --div ieee
 run --dtype fp32
 run --dtype fp32 --rule mid
 run --samples 1e10 --steps 100
+run --dtype fp32acc
 run --integrand sin
+run --integrand sin --div ieee
 run --integrand train
+run --integrand train --div ieee
 run --integrand table
+run --integrand table --div ieee
 run --integrand poly
+run --integrand poly --div ieee

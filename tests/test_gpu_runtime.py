@@ -426,3 +426,45 @@ def test_block_sizes(native, cuda, block):
     assert s == pytest.approx(2.0, abs=1e-12)
     with pytest.raises(RuntimeError, match="64, 128, 256, 512 or 1024"):
         Integrator("pi4", n=n, block=192)
+
+
+@pytest.mark.parametrize("streams", [2, 3, 4])
+def test_step_streams_bitwise(native, cuda, streams):
+    """Chained graph batches dealt over several streams (each its own chain, own partials,
+    own finalize; the compute stream joins them) give every step exactly the one-stream
+    result, bitwise — including remainder batches whose step count the streams do not
+    divide."""
+    from cuda_v_mpi_amd import Integrator
+
+    n = 10**8 + 7
+    ref = Integrator("pi4", n=n, rule="mid", slots=48, step_streams=1)
+    assert ref.plan.step_streams(48) == 1
+    ref.plan.run_steps(48, False, True)
+    want = [ref.plan.host_result(ref.plan.host_index_of(k, True)) for k in range(48)]
+    assert len(set(want)) == 1
+    it = Integrator("pi4", n=n, rule="mid", slots=48, step_streams=streams)
+    assert it.plan.step_streams(48) == streams
+    for steps in (48, 29, 5):
+        it.plan.run_steps(steps, False, True)
+        got = [it.plan.host_result(it.plan.host_index_of(k, True)) for k in range(steps)]
+        assert got == want[:steps]
+
+
+def test_step_streams_auto_policy(native, cuda):
+    """Auto: four streams below 6e8 samples per step, one at or above (N = 1e9 on one GPU)."""
+    from cuda_v_mpi_amd import Integrator
+
+    assert Integrator("pi4", n=10**9, slots=48).plan.step_streams(48) == 1
+    assert Integrator("pi4", n=10**9, slots=48, slice_of=(0, 8)).plan.step_streams(48) == 4
+    assert Integrator("pi4", n=10**9, slots=48, slice_of=(0, 8)).plan.step_streams(3) == 3
+
+
+def test_table2d_step_streams_equal(native, cuda):
+    """The 2-D replay on 1, 2 and 4 chained streams: the same 32 results, bitwise."""
+    res = []
+    for ss in (1, 2, 4):
+        p = native.Table2DPlan(4096, 1800.0, 0, None, True, True, ss)
+        assert p.step_streams == ss
+        p.time(p.graph_steps, True)
+        res.append(p.last_result())
+    assert res[0] == res[1] == res[2] == native.table2d_oracle(4096)

@@ -42,13 +42,15 @@ def test_riemann_vs_torch(cuda, spec, n):
     assert got == pytest.approx(want, rel=1e-12, abs=1e-12)
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "fp32acc"])
 @pytest.mark.parametrize("n", [1, 63, 4097, 1_000_003, 40_000_001, 50_000_017])
-def test_riemann_fp32_small_and_odd_n(cuda, n):
-    """fp32 path at odd N and N below the grid size (remainder samples, partial tiles, the
-    IEEE fallback up to 4.8e7 and, at 50_000_017, the 192-sample series tiles with a
-    remainder of 17 samples) against the fp64 torch reference."""
+def test_riemann_fp32_small_and_odd_n(cuda, n, dtype):
+    """fp32 paths (fp64 fold, and fp32 accumulation) at odd N and N below the grid size
+    (remainder samples, partial tiles, the IEEE fallback up to 4.8e7 and, at 50_000_017, the
+    192-sample series tiles with a remainder of 17 samples) against the fp64 torch
+    reference."""
     spec = integrands.pi4()
-    got = float(kernels.riemann(spec, n, rule="mid", dtype="fp32").item())
+    got = float(kernels.riemann(spec, n, rule="mid", dtype=dtype).item())
     want = _ref_sum(spec, n, rule="mid")
     assert got == pytest.approx(want, rel=2e-6)
 

@@ -32,9 +32,16 @@
 
 using namespace miint;
 
+constexpr const char* kUsage =
+    "usage: cintegrate [--gpus G] [--loopback W] [--materialize] [--parity [--sp 32 --sm 2]]\n"
+    "                  [--kernel sin] [--profile FILE] [--steps-per-sec S] [--iters K]\n"
+    "                  [--json] [--jsonl FILE] [--device cpu [--threads T]]\n"
+    "Train distance: the interpolated velocity profile summed over 1800 s (h = 1e-4 s).\n";
+
 int main(int argc, char** argv) {
   try {
     cli::Args a(argc, argv);
+    if (cli::usage_requested(a, kUsage)) return 0;
     const bool cpu = cli::on_cpu(a);
     const cli::Topology topo = cpu ? cli::Topology{} : cli::topology(a);
     const int sps = static_cast<int>(a.integer("steps-per-sec", oracle::kStepsPerSec));

@@ -62,11 +62,41 @@ class Args {
     return it != kv_.end() && it->second != "0" && it->second != "false";
   }
   const std::vector<std::string>& positional() const { return pos_; }
+  // --help / -h: the caller prints its usage text and exits before touching any device
+  bool help() const {
+    return kv_.count("help") > 0 || std::find(pos_.begin(), pos_.end(), "-h") != pos_.end();
+  }
 
  private:
   std::map<std::string, std::string> kv_;
   std::vector<std::string> pos_;
 };
+
+// Strict spellings of the shared knobs: a typo fails instead of running the default.
+inline DType parse_dtype(const std::string& s) {
+  if (s == "fp64") return DType::kF64;
+  if (s == "fp32") return DType::kF32;
+  if (s == "fp32acc") return DType::kF32Acc32;
+  fail("--dtype must be fp64, fp32 or fp32acc (got " + s + ")", __FILE__, __LINE__);
+}
+inline Rule parse_rule(const std::string& s) {
+  if (s == "left") return Rule::kLeft;
+  if (s == "mid") return Rule::kMid;
+  if (s == "right") return Rule::kRight;
+  fail("--rule must be left, mid or right (got " + s + ")", __FILE__, __LINE__);
+}
+inline DivMode parse_div(const std::string& s) {
+  if (s == "series") return DivMode::kSeries;
+  if (s == "ieee") return DivMode::kIeee;
+  fail("--div must be series or ieee (got " + s + ")", __FILE__, __LINE__);
+}
+
+// Print `text` and return true when --help / -h was given (main returns 0 then).
+inline bool usage_requested(const Args& a, const char* text) {
+  if (!a.help()) return false;
+  std::fputs(text, stdout);
+  return true;
+}
 
 inline int env_int(const char* k, int d) {
   const char* v = std::getenv(k);

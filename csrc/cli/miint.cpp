@@ -48,9 +48,9 @@ RiemannConfig make_cfg(const std::string& integ, double n, const std::string& dt
   c.b = c.integrand == Integrand::kPi4 || c.integrand == Integrand::kPoly ? 1.0
       : c.integrand == Integrand::kSin ? 3.14159265358979323846 : 1800.0;
   c.n = static_cast<uint64_t>(n);
-  c.dtype = dtype == "fp32" ? DType::kF32 : (dtype == "fp32acc" ? DType::kF32Acc32 : DType::kF64);
-  c.rule = rule == "mid" ? Rule::kMid : (rule == "right" ? Rule::kRight : Rule::kLeft);
-  c.div = div == "ieee" ? DivMode::kIeee : DivMode::kSeries;
+  c.dtype = cli::parse_dtype(dtype);
+  c.rule = cli::parse_rule(rule);
+  c.div = cli::parse_div(div);
   if (c.integrand == Integrand::kTrainVel) { c.p0 = oracle::kTrainTs; c.p1 = oracle::kTrainVs; }
   if (c.integrand == Integrand::kTable) c.table = oracle::profile_table();
   if (c.integrand == Integrand::kPoly) c.coef = {0.3, -1.2, 0.7, 0.05, -0.4, 0.9, 0.1};
@@ -209,9 +209,22 @@ int comm_sweep(const cli::Args& a, const cli::Topology& topo, double max_bytes, 
 
 }  // namespace
 
+constexpr const char* kUsage =
+    "usage: miint info\n"
+    "       miint bench [--integrand pi4] [--n 1e9] [--dtype fp64|fp32|fp32acc] [--rule left]\n"
+    "                   [--iters 200] [--gpus G] [--div series|ieee] [--unfused] [--no-graph]\n"
+    "                   [--block B] [--grid G] [--step-streams S] [--trig-library] [--settle N]\n"
+    "       miint sweep [--gpus G]\n"
+    "       miint table2d [--grid 4096] [--gpus G] [--slice R/W] [--no-graph]\n"
+    "                     [--step-streams S] [--min-wg W] [--settle-ms MS]\n"
+    "       miint selfcheck\n"
+    "       miint comm [--gpus G] [--max-bytes 144e6] [--iters 20]\n"
+    "Every record is one JSON line on stdout; --jsonl FILE also appends it to FILE.\n";
+
 int main(int argc, char** argv) {
   try {
     cli::Args a(argc, argv);
+    if (cli::usage_requested(a, kUsage)) return 0;
     const std::string cmd = a.positional().empty() ? "info" : a.positional()[0];
     if (cmd == "info") {
       const int nd = device_count();

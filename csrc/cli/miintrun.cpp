@@ -48,10 +48,10 @@ int free_port() {
   return port;
 }
 
-int usage() {
-  std::fprintf(stderr,
+int usage(FILE* out = stderr) {
+  std::fprintf(out,
                "usage: miintrun -np P [--addr A] [--port N] [--grace S] [--] PROGRAM [ARGS...]\n");
-  return 2;
+  return out == stderr ? 2 : 0;
 }
 
 int status_code(int st) { return WIFEXITED(st) ? WEXITSTATUS(st) : 128 + WTERMSIG(st); }
@@ -72,6 +72,7 @@ int main(int argc, char** argv) {
       }
       return argv[++i];
     };
+    if (a == "-h" || a == "--help") return usage(stdout);
     if (a == "-np" || a == "-n" || a == "--np") np = std::atoi(val("-np"));
     else if (a == "--addr") addr = val("--addr");
     else if (a == "--port") port = std::atoi(val("--port"));

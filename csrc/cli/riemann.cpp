@@ -19,8 +19,8 @@
 // the reference edits riemann.cpp:37 and recompiles; with --device cpu, compiled for the
 // host cores instead (HostExpr). --analytic V adds the error vs V.
 //
-//   ./riemann [--n 1e9] [--gpus G] [--integrand sin|pi4|poly|train] [--rule left|mid]
-//             [--dtype fp64|fp32] [--iters K] [--block 64..1024] [--grid G] [--parity]
+//   ./riemann [--n 1e9] [--gpus G] [--integrand sin|pi4|poly|train] [--rule left|mid|right]
+//             [--dtype fp64|fp32|fp32acc] [--iters K] [--block 64..1024] [--grid G] [--parity]
 //             [--json] [--jsonl FILE]
 //             [--device cpu [--threads T] [--ranks P]] [--expr EXPR --a A --b B [--analytic V]]
 #include <algorithm>
@@ -39,13 +39,6 @@
 using namespace miint;
 
 namespace {
-
-Rule parse_rule(const std::string& s) {
-  if (s == "left") return Rule::kLeft;
-  if (s == "mid") return Rule::kMid;
-  if (s == "right") return Rule::kRight;
-  fail("unknown rule " + s, __FILE__, __LINE__);
-}
 
 void print_result(double secs, double hi, double nd, double result) {
   std::printf("%lf seconds\n", secs);
@@ -193,10 +186,21 @@ int run_expr(const cli::Args& a, const RiemannConfig& cfg, double nd, int iters)
 
 }  // namespace
 
+constexpr const char* kUsage =
+    "usage: riemann [--n 1e9] [--gpus G] [--loopback W] [--integrand sin|pi4|poly|train|table]\n"
+    "               [--rule left|mid|right] [--dtype fp64|fp32|fp32acc] [--div series|ieee]\n"
+    "               [--iters K] [--block 64..1024] [--grid G] [--a A --b B] [--parity]\n"
+    "               [--json] [--jsonl FILE] [--profile FILE]\n"
+    "               [--device cpu [--threads T] [--ranks P]]\n"
+    "               [--expr EXPR --a A --b B [--analytic V]]\n"
+    "Riemann sum of f on [a, b] (default sin on [0, pi], N = 1e9); prints the reference's\n"
+    "two lines, or one JSON record with --json. Multi-GPU: --gpus G, torchrun or miintrun.\n";
+
 int main(int argc, char** argv) {
   try {
     install_crash_handler_from_env();
     cli::Args a(argc, argv);
+    if (cli::usage_requested(a, kUsage)) return 0;
     const Integrand f = cli::parse_integrand(a.str("integrand", "sin"));
     const double pi = 3.14159265358979323846;
     double lo = 0.0, hi = pi;  // riemann.cpp:6 RANGE = M_PI
@@ -218,12 +222,9 @@ int main(int argc, char** argv) {
     cfg.a = lo;
     cfg.b = hi;
     cfg.n = n;
-    cfg.rule = parse_rule(a.str("rule", "left"));
-    const std::string dts = a.str("dtype", "fp64");
-    MIINT_CHECK(dts == "fp64" || dts == "fp32" || dts == "fp32acc",
-                "--dtype must be fp64|fp32|fp32acc");
-    cfg.dtype = dts == "fp32" ? DType::kF32 : (dts == "fp32acc" ? DType::kF32Acc32 : DType::kF64);
-    cfg.div = a.str("div", "series") == "ieee" ? DivMode::kIeee : DivMode::kSeries;
+    cfg.rule = cli::parse_rule(a.str("rule", "left"));
+    cfg.dtype = cli::parse_dtype(a.str("dtype", "fp64"));
+    cfg.div = cli::parse_div(a.str("div", "series"));
     cfg.fused = !a.flag("unfused");
     // --block: threads per workgroup (the reference's SP, cintegrate.cu:17-18); --grid:
     // workgroups (its SM), 0 = auto

@@ -88,9 +88,17 @@ int run_host(const cli::Args& a) {
 
 }  // namespace
 
+constexpr const char* kUsage =
+    "usage: trainscan [--gpus G] [--loopback W] [--algo fused|lookback|onepass] [--parity]\n"
+    "                 [--replicate] [--no-phase2] [--steps-per-sec S] [--iters K]\n"
+    "                 [--json] [--jsonl FILE] [--profile FILE]\n"
+    "                 [--device cpu [--threads T] [--ranks P] [--no-keep]]\n"
+    "Distributed two-phase prefix scan of the train profile (velocity, then position).\n";
+
 int main(int argc, char** argv) {
   try {
     cli::Args a(argc, argv);
+    if (cli::usage_requested(a, kUsage)) return 0;
     if (cli::on_cpu(a)) return run_host(a);
     const cli::Topology topo = cli::topology(a);
     TrainScanConfig cfg;

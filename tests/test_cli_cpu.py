@@ -65,6 +65,27 @@ def test_native_cli_refuses_without_gpu():
         assert p.returncode == 1 and "HIP devices" in p.stderr
 
 
+def _native(name):
+    exe = os.path.join(REPO, "build", "bin", name)
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", REPO, "-j8", "cli"], check=True, capture_output=True)
+    return exe
+
+
+@pytest.mark.parametrize("name", ["riemann", "cintegrate", "trainscan", "miint", "miintrun"])
+def test_native_cli_help_needs_no_device(name):
+    p = subprocess.run([_native(name), "--help"], capture_output=True, text=True, timeout=60)
+    assert p.returncode == 0 and p.stdout.startswith("usage: " + name), p.stderr
+
+
+@pytest.mark.parametrize("flag,value", [("rule", "midd"), ("dtype", "fp46"), ("div", "iee")])
+def test_native_cli_rejects_misspelt_knobs(flag, value):
+    # a typo must fail, not quietly run the default rule / dtype / division
+    p = subprocess.run([_native("riemann"), "--device", "cpu", "--n", "1e4", f"--{flag}", value],
+                       capture_output=True, text=True, timeout=60)
+    assert p.returncode == 1 and f"--{flag} must be" in p.stderr
+
+
 def _bench(*args, timeout=300):
     return subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args],
                           capture_output=True, text=True, timeout=timeout)

@@ -393,6 +393,9 @@ def main(argv=None) -> int:
             "control_plane": ctx.backend,
             "torch_nccl_groups": ctx.nccl_groups,
             "native_rccl_comms": int(comm is not None and getattr(comm, "kind", "") == "rccl"),
+            # MIINT_OVERSUBSCRIBE: ranks share GPUs and RCCL runs over loopback sockets — a
+            # correctness run of the multi-rank path, not a scaling number
+            "ranks_share_gpus": mdist.ranks_share_devices() and world > 1,
             "per_rank_ms": per_rank_ms,
             "per_rank_spread_ms": max(per_rank_ms) - min(per_rank_ms),
             "graph_replays_timed": graph_replays,

@@ -155,7 +155,7 @@ inline void run_ranks(const Topology& t,
     const char* addr = std::getenv("MASTER_ADDR");
     const int port = env_int("MASTER_PORT", 29500) + 17;
     const std::string id = rendezvous_unique_id(addr ? addr : "127.0.0.1", port, t.rank0, t.world);
-    const int dev = env_int("LOCAL_RANK", 0);
+    const int dev = rank_device(env_int("LOCAL_RANK", 0));
     comms.emplace_back(new RcclComm(id, t.rank0, t.world, dev));
     fn(t.rank0, dev, comms[0].get());
     return;

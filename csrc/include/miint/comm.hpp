@@ -110,6 +110,18 @@ inline void launch_with(const Comm* comm, const Graph& g, hipStream_t s) {
   else g.launch(s);
 }
 
+// Ranks that share a GPU (MIINT_OVERSUBSCRIBE=1: more ranks than devices, e.g. W ranks on
+// the one GPU of a test box). RCCL refuses two ranks of one host on one device ("Duplicate
+// GPU detected"), so each such rank presents itself as a host of its own (NCCL_HOSTID) and
+// the ranks meet over RCCL's socket transport on loopback (NCCL_SOCKET_IFNAME=lo unless set).
+// The multi-rank RCCL path runs for real — bootstrap, collectives, graph capture — at
+// loopback-socket speed: a correctness configuration, not a performance one.
+bool ranks_share_devices();
+// Device of a process-per-rank rank: LOCAL_RANK, modulo the visible devices when shared.
+int rank_device(int local_rank);
+// Sets the RCCL environment above for `rank` (rank < 0: only what bootstrap reads).
+void prepare_shared_device_rccl(int rank);
+
 class RcclComm final : public Comm {
  public:
   // 128-byte RCCL unique id (raw bytes), created by rank 0 and shared out of band.

@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
@@ -18,7 +19,27 @@
 
 namespace miint {
 
+bool ranks_share_devices() {
+  const char* v = std::getenv("MIINT_OVERSUBSCRIBE");
+  return v && std::strcmp(v, "0") != 0 && *v != '\0';
+}
+
+int rank_device(int local_rank) {
+  if (!ranks_share_devices()) return local_rank;
+  const int nd = device_count();
+  MIINT_CHECK(nd >= 1, "MIINT_OVERSUBSCRIBE: no HIP devices visible");
+  return local_rank % nd;
+}
+
+void prepare_shared_device_rccl(int rank) {
+  if (!ranks_share_devices()) return;
+  ::setenv("NCCL_SOCKET_IFNAME", "lo", 0);  // the ranks are on this host
+  ::setenv("NCCL_IB_DISABLE", "1", 0);
+  if (rank >= 0) ::setenv("NCCL_HOSTID", ("miint-shared-rank-" + std::to_string(rank)).c_str(), 1);
+}
+
 std::string RcclComm::unique_id() {
+  prepare_shared_device_rccl(-1);
   ncclUniqueId id;
   MIINT_RCCL(ncclGetUniqueId(&id));
   return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
@@ -30,6 +51,7 @@ RcclComm::RcclComm(const std::string& id, int rank, int world, int device)
   MIINT_CHECK(rank >= 0 && rank < world, "rank out of range");
   ncclUniqueId uid;
   std::memcpy(&uid, id.data(), sizeof(uid));
+  prepare_shared_device_rccl(rank);
   DeviceGuard g(device);
   MIINT_RCCL(ncclCommInitRank(&comm_, world, uid, rank));
 }

@@ -88,6 +88,24 @@ class DistContext:
             self.initialized_here = False
 
 
+def ranks_share_devices() -> bool:
+    """MIINT_OVERSUBSCRIBE=1: more ranks than GPUs (W ranks on a one-GPU box). The native
+    runtime reads the same variable (``miint::ranks_share_devices``, comm.hpp)."""
+    return os.environ.get("MIINT_OVERSUBSCRIBE", "") not in ("", "0")
+
+
+def prepare_shared_device_rccl(rank: int) -> None:
+    """RCCL refuses two ranks of one host on one GPU, so under ``ranks_share_devices`` each
+    rank names itself a host of its own and the ranks meet over RCCL's socket transport on
+    loopback: the multi-rank RCCL path runs for real, at socket speed (a correctness
+    configuration). Mirrors ``miint::prepare_shared_device_rccl`` for torch's RCCL groups."""
+    if not ranks_share_devices():
+        return
+    os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
+    os.environ.setdefault("NCCL_IB_DISABLE", "1")
+    os.environ["NCCL_HOSTID"] = f"miint-shared-rank-{rank}"
+
+
 def env_world() -> tuple[int, int, int]:
     return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
             int(os.environ.get("LOCAL_RANK", "0")))
@@ -103,9 +121,10 @@ def init(backend: str | None = None, timeout_s: float = 300.0, force: bool = Fal
     if backend is None:
         backend = "nccl" if torch.cuda.is_available() else "gloo"
     ctx = DistContext(rank=rank, world=world, local_rank=local, backend=backend)
+    prepare_shared_device_rccl(rank)
     if backend == "nccl":
-        ctx.device = local
-        torch.cuda.set_device(local)
+        ctx.device = local % torch.cuda.device_count() if ranks_share_devices() else local
+        torch.cuda.set_device(ctx.device)
     elif torch.cuda.is_available():
         # gloo process group with GPU compute: ranks may share devices (testing on 1 GPU)
         ctx.device = local % torch.cuda.device_count()
@@ -116,7 +135,7 @@ def init(backend: str | None = None, timeout_s: float = 300.0, force: bool = Fal
         if not dist.is_initialized():
             kw = {}
             if backend == "nccl":
-                kw["device_id"] = torch.device("cuda", local)
+                kw["device_id"] = torch.device("cuda", ctx.device)
             dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                     timeout=datetime.timedelta(seconds=timeout_s), **kw)
             ctx.initialized_here = True

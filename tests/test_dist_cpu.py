@@ -125,3 +125,20 @@ def test_torchrun_table2d_cpu_rows_split_over_ranks():
     rows = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
     assert len(rows) == 1 and rows[0]["gpus"] == 3  # rank 0 prints
     assert rows[0]["rel_err_vs_oracle"] < 1e-13
+
+
+def test_shared_device_rccl_env(monkeypatch):
+    """MIINT_OVERSUBSCRIBE=1 (ranks share a GPU): each rank a host of its own to RCCL, socket
+    transport on loopback; without it nothing is touched."""
+    from cuda_v_mpi_amd.parallel import dist as mdist
+
+    for k in ("MIINT_OVERSUBSCRIBE", "NCCL_HOSTID", "NCCL_SOCKET_IFNAME", "NCCL_IB_DISABLE"):
+        monkeypatch.delenv(k, raising=False)
+    mdist.prepare_shared_device_rccl(3)
+    assert not mdist.ranks_share_devices() and "NCCL_HOSTID" not in os.environ
+    monkeypatch.setenv("MIINT_OVERSUBSCRIBE", "1")
+    monkeypatch.setenv("NCCL_SOCKET_IFNAME", "eth9")  # a user's choice is kept
+    mdist.prepare_shared_device_rccl(3)
+    assert mdist.ranks_share_devices()
+    assert os.environ["NCCL_HOSTID"] == "miint-shared-rank-3"
+    assert os.environ["NCCL_SOCKET_IFNAME"] == "eth9" and os.environ["NCCL_IB_DISABLE"] == "1"

@@ -26,5 +26,9 @@ step bench_native_np2 300 python bench.py --gpus 2 --steps 20 --warmup 5 --no-ex
 step bench_torch_np2 300 python bench.py --gpus 2 --steps 20 --warmup 5 --no-extras --comm torch
 step bench_native_np4 300 python bench.py --gpus 4 --steps 20 --warmup 5 --no-extras
 step bench_strong_np2 300 python bench.py --gpus 2 --steps 20 --warmup 5 --no-extras --scaling strong
-grep -h 'NET/\|via NET\|Duplicate\|nRanks\|Init COMPLETE' "$out"/*.log | sort | uniq -c | sort -rn | head -40 > "$out/nccl_summary.txt" || true
+# RCCL prints its INFO lines on stdout: transport and topology of every communicator
+for f in "$out"/*.out; do
+  echo "== $(basename "$f" .out)"
+  grep -o 'nRanks [0-9]* nNodes [0-9]* localRanks [0-9]*\|via NET/Socket/[0-9]*\|Using \[0\]lo:[0-9.]*\|Init COMPLETE' "$f" | sort | uniq -c || true
+done > "$out/nccl_summary.txt"
 echo done

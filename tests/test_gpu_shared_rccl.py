@@ -64,3 +64,16 @@ def test_bench_two_ranks_native_rccl_one_gpu(cuda):
     assert r["rccl_world"] == 2 and r["native_rccl_comms"] == 1 and r["torch_nccl_groups"] == 0
     assert r["comm_fallback"] is None and r["graph_replays_timed"] == 1
     assert r["config"]["bucketed_allreduce"] and r["config"]["N"] == 2 * 10**9
+
+
+def test_bench_driver_launch_form_two_ranks(cuda):
+    """The driver's own launch line (torch.distributed.run, one rank per process) with the
+    two ranks on the one GPU: the record is rank 0's, with the max over ranks."""
+    rec = _records([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                    "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                    "29641", os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "10",
+                    "--warmup", "3", "--no-extras"], timeout=240)
+    assert len(rec) == 1
+    r = rec[0]
+    assert r["launcher"] == "torchrun" and r["verified"] and r["rccl_world"] == 2
+    assert abs(r["ms_per_step"] - max(r["per_rank_ms"])) <= 1e-9

@@ -86,10 +86,17 @@ def run_comm(n: int, timeout: float = 600.0) -> dict:
 
 
 def sweep(counts: list[int], steps: int = 200, warmup: int = 10, comm: bool = True) -> list[dict]:
+    """One row per GPU count. Under MIINT_OVERSUBSCRIBE=1 (``dist.ranks_share_devices``) a
+    count above the visible devices still runs, its ranks sharing GPUs over RCCL's loopback
+    sockets: a rehearsal of the sweep's multi-rank path, marked ``ranks_share_gpus`` and given
+    no efficiency (the GPUs are time-shared, so the numbers say nothing about scaling)."""
+    from .dist import ranks_share_devices
+
     have = visible_gpus()
+    shared = ranks_share_devices()
     rows: list[dict] = []
     for n in counts:
-        if n > have:
+        if n > have and not (shared and have >= 1):
             rows.append({"n_gpus": n, "skipped": f"only {have} devices"})
             continue
         b = run_bench(n, steps, warmup)
@@ -103,6 +110,8 @@ def sweep(counts: list[int], steps: int = 200, warmup: int = 10, comm: bool = Tr
             "graphs": b["config"]["graphs"],
             "verified": b["verified"],
         }
+        if n > have:
+            row["ranks_share_gpus"] = True
         s1 = b.get("strong_1e9")
         if s1:
             row["strong_1e9_value"] = s1["value"]
@@ -115,12 +124,12 @@ def sweep(counts: list[int], steps: int = 200, warmup: int = 10, comm: bool = Tr
         t2 = b.get("baseline5_table2d_4096")
         if t2:
             row["t2d_4096_us"] = t2["ms_per_integration"] * 1e3
-        if comm:
+        if comm and n <= have:  # miint comm drives n distinct devices from one process
             row.update(run_comm(n))
         rows.append(row)
     base = next((r for r in rows if r["n_gpus"] == 1 and "value" in r), None)
     for r in rows:
-        if base is None or "value" not in r:
+        if base is None or "value" not in r or r.get("ranks_share_gpus"):
             continue
         n = r["n_gpus"]
         r["weak_eff"] = r["value"] / (n * base["value"])

@@ -147,6 +147,15 @@ def test_scale_sweep_rows_and_efficiency(monkeypatch):
     assert abs(rows[1]["t2d_strong_eff"] - 2 ** 0.8 / 2) < 1e-12
     md = scaling.markdown(rows)
     assert "skipped: only 2 devices" in md and md.count("\n") == 5
+    # ranks sharing GPUs: every count runs, the shared rows carry no efficiency and no
+    # comm sweep (that one needs distinct devices)
+    monkeypatch.setenv("MIINT_OVERSUBSCRIBE", "1")
+    fake[4], fake[8] = 1.9e13, 1.9e13
+    rows = scaling.sweep([1, 2, 4, 8])
+    assert all("skipped" not in r for r in rows)
+    assert [bool(r.get("ranks_share_gpus")) for r in rows] == [False, False, True, True]
+    assert "weak_eff" not in rows[2] and "allreduce_8B_us" not in rows[3]
+    assert "weak_eff" in rows[1] and "allreduce_8B_us" in rows[1]
 
 
 def test_bench_driver_launch_form_json_contract():

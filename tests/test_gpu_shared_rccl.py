@@ -77,3 +77,25 @@ def test_bench_driver_launch_form_two_ranks(cuda):
     r = rec[0]
     assert r["launcher"] == "torchrun" and r["verified"] and r["rccl_world"] == 2
     assert abs(r["ms_per_step"] - max(r["per_rank_ms"])) <= 1e-9
+
+
+@pytest.mark.parametrize("algo", ["fused", "lookback"])
+def test_trainscan_parity_seven_rccl_ranks(cuda, algo):
+    """4main.c at P = 7 prints 0.000000 (its fill/scan partitions disagree): the
+    GPU plan reproduces it with seven real RCCL ranks (allgather-fed carries)."""
+    p = subprocess.run(_np(7, os.path.join(BIN, "trainscan"), "--parity", "--algo", algo),
+                       capture_output=True, text=True, timeout=200, env=_env(), cwd=REPO)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if not l.startswith(("[", " "))]
+    assert "Step size of 10000" in lines
+    assert "Total distance traveled = 0.000000" in lines
+
+
+def test_riemann_parity_master_worker_rccl_equals_loopback(cuda):
+    """riemann --parity: P - 1 workers of (int)(N / W) samples each, rank 0 idle
+    (riemann.cpp:65-86) — the same value over RCCL ranks as over the loopback transport."""
+    args = ["--parity", "--n", "1e8", "--json"]
+    lb = _records([os.path.join(BIN, "riemann"), *args, "--loopback", "3"])[0]
+    rc = _records(_np(3, os.path.join(BIN, "riemann"), *args))[0]
+    assert rc["gpus"] == 3 and rc["parity"]
+    assert rc["result"] == pytest.approx(lb["result"], rel=1e-15, abs=0)

@@ -108,6 +108,9 @@ def parse(argv=None) -> argparse.Namespace:
     p.add_argument("--step-streams", type=int, default=0,
                    help="streams a chained graph batch deals its steps over (0 = auto: 4 below "
                         "6e8 samples per GPU per step, else 1)")
+    p.add_argument("--no-multistep", action="store_true",
+                   help="graph batches as one kernel launch per step (chained) instead of one "
+                        "persistent launch for the whole batch")
     p.add_argument("--no-bucket", action="store_true",
                    help="one all-reduce per step instead of one per graph batch of steps")
     p.add_argument("--force-collective", action="store_true",
@@ -229,7 +232,8 @@ def main(argv=None) -> int:
                           div=args.div, backend="cpu" if cpu else "hip", ctx=ctx, comm=comm,
                           fused=not args.unfused, grid=args.grid, slots=args.slots,
                           force_collective=args.force_collective, bucket=not args.no_bucket,
-                          step_streams=args.step_streams, block=args.block)
+                          step_streams=args.step_streams, block=args.block,
+                          multistep=not args.no_multistep)
 
     # A native RCCL communicator that fails to come up on every rank (the failure is agreed
     # over the torch process group, so all ranks switch together) falls back to the
@@ -420,6 +424,8 @@ def main(argv=None) -> int:
                 "bucketed_allreduce": bool(plan.bucketed) if plan is not None else False,
                 "fused_reduction": not args.unfused,
                 "chained_batches": bool(plan.chained) and graphs if plan is not None else False,
+                # a graph batch is ONE persistent launch of all its steps + a closing kernel
+                "multistep": bool(plan.multistep) and graphs if plan is not None else False,
                 "step_streams": plan.step_streams(min(args.steps, plan.slots))
                 if plan is not None else 1,
                 "grid": plan.grid if plan is not None else 0,
@@ -513,7 +519,8 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
     comm = getattr(integ, "_comm", None)
     kw = dict(rule=args.rule, dtype=args.dtype, ctx=ctx, comm=args.comm, slots=args.slots,
               bucket=not args.no_bucket, force_collective=args.force_collective,
-              comm_obj=comm, step_streams=args.step_streams)
+              comm_obj=comm, step_streams=args.step_streams,
+              multistep=not args.no_multistep)
     pi4 = args.integrand == "pi4"
     # (1) the same config with correctly rounded division for every sample
     if pi4 and args.div != "ieee":

@@ -214,6 +214,7 @@ constexpr const char* kUsage =
     "       miint bench [--integrand pi4] [--n 1e9] [--dtype fp64|fp32|fp32acc] [--rule left]\n"
     "                   [--iters 200] [--gpus G] [--div series|ieee] [--unfused] [--no-graph]\n"
     "                   [--block B] [--grid G] [--step-streams S] [--trig-library] [--settle N]\n"
+    "                   [--no-multistep] [--slots K]\n"
     "       miint sweep [--gpus G]\n"
     "       miint table2d [--grid 4096] [--gpus G] [--slice R/W] [--no-graph]\n"
     "                     [--step-streams S] [--min-wg W] [--settle-ms MS]\n"
@@ -248,6 +249,8 @@ int main(int argc, char** argv) {
       c.grid = static_cast<int>(a.integer("grid", 0));
       c.block = static_cast<int>(a.integer("block", kRiemannBlock));
       c.step_streams = static_cast<int>(a.integer("step-streams", 0));
+      c.multistep = !a.flag("no-multistep");  // A-B: chained batches instead
+      c.slots = static_cast<int>(a.integer("slots", c.slots));
       // validation / A-B: kIeee sin and cos by ocml per sample instead of fast_trig.hpp
       if (a.flag("trig-library")) set_trig_library(true);
       MIINT_CHECK(riemann_block_ok(c.block), "--block must be 64, 128, 256, 512 or 1024");

@@ -73,6 +73,13 @@ struct RiemannConfig {
                                // torch.distributed path reduces results itself)
   bool force_collective = false;  // run the RCCL stage even with a 1-rank communicator
                                   // (exercises the multi-GPU graph path on one GPU)
+  bool multistep = true;        // chained graph batches as ONE persistent launch of all the
+                                // batch's steps plus one closing kernel
+                                // (launch_riemann_multistep): one launch ramp and drain per
+                                // batch instead of per step. The plan's grid is then capped at
+                                // the multi-step kernel's residency (auto grid), so every path
+                                // of the plan sums the same partials: values bit for bit equal.
+                                // An explicit grid above residency turns it off.
   int step_streams = 0;         // chained graph batches: steps dealt round-robin to this many
                                 // streams (each its own chain, ramp and tail of one step
                                 // overlapping the next one's work); 0 = auto (kAutoStepStreams
@@ -170,6 +177,8 @@ class RiemannPlan {
   bool bucketed() const { return collective() && cfg_.bucket; }
   // Graph batches run chained kernels (see RiemannConfig::chain): single GPU, or bucketed.
   bool chained() const { return cfg_.fused && cfg_.chain && (!collective() || bucketed()); }
+  // Chained batches run as one multi-step launch (RiemannConfig::multistep, in effect).
+  bool multistep() const { return chained() && multistep_; }
 
  private:
   void enqueue_batch(hipStream_t cs, hipStream_t rs, int nsteps, bool overlap);
@@ -193,6 +202,8 @@ class RiemannPlan {
   LaunchShape shape_{1, kRiemannBlock};
   DeviceBuffer<double> partials_;  // 2 x grid: chained batches alternate halves (+ 2-kernel)
   DeviceBuffer<double> slots_;     // grid write-once slots of the fused (ticket) kernel
+  DeviceBuffer<double> ms_partials_;  // multistep: slots x grid partials
+  bool multistep_ = false;
   DeviceBuffer<double> result_;
   DeviceBuffer<unsigned int> ticket_;
   DeviceBuffer<double> table_;

@@ -122,6 +122,19 @@ void launch_riemann_chained(const RiemannParams& p, DType dtype, DivMode div, La
                             const double* prev, int nprev, double scale, double* out_prev,
                             hipStream_t stream);
 
+// K = `steps` complete integrations in one persistent launch, closed by one K-workgroup
+// kernel (riemann.hip "multi-step"): out[s] = step s's scaled sum, bitwise the fused /
+// chained / two-kernel value at the same grid. `partials` holds steps x grid doubles. The
+// grid should be resident as a whole: at most riemann_multistep_grid(...) workgroups.
+// 1 <= steps <= kMaxMultiSteps.
+constexpr int kMaxMultiSteps = 64;
+int riemann_multistep_grid(const RiemannParams& p, DType dtype, DivMode div, int block,
+                           int num_cus);
+void launch_riemann_multistep(const RiemannParams& p, DType dtype, DivMode div,
+                              LaunchShape shape, const double* table, int table_n,
+                              double* partials, int steps, double scale, double* out,
+                              hipStream_t stream);
+
 // Debug/validation: write every sample's f value (as the hot tile path computes it) to
 // `out[0..p.n)`; fp64 only. Used by the per-point accuracy tests of the series division.
 void launch_riemann_point_values(const RiemannParams& p, DivMode div, const double* table,

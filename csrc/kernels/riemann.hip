@@ -56,13 +56,16 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
 // all-fp32 variant (Pi4F32Acc32: fp32 lanes, v_add_f32_dpp wave sums, fp32 LDS step).
 template <class F> struct AccOf { using type = double; };
 
+// `block` is the workgroup's index in the sample decomposition: blockIdx.x, or the multi-step
+// kernel's per-step rotated (virtual) index.
 template <DivMode M, class F>
-__device__ __forceinline__ typename AccOf<F>::type lane_sum(const RiemannParams& p, const F& f) {
+__device__ __forceinline__ typename AccOf<F>::type lane_sum(const RiemannParams& p, const F& f,
+                                                            unsigned block) {
   using Acc = typename AccOf<F>::type;
   constexpr int T = F::template tile_len<M>();
   const uint64_t bs = blockDim.x;
   const uint64_t lanes = static_cast<uint64_t>(gridDim.x) * bs;
-  const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * bs + threadIdx.x;
+  const uint64_t gid = static_cast<uint64_t>(block) * bs + threadIdx.x;
   const uint64_t ntile = p.n / T;
   const uint64_t rounds = gid < ntile ? (ntile - 1 - gid) / lanes + 1 : 0;
   const uint64_t r_all = readlane_u64(rounds, kWave - 1);  // lane 63 has the fewest rounds
@@ -504,7 +507,7 @@ __device__ __forceinline__ void partials_body(const RiemannParams& p, const doub
   __shared__ Acc red[kMaxBlock / kWave];
   __shared__ double lds[lds_words<M, F>()];
   const F f = make_functor<M, F>(p, table, table_n, lds);
-  const double s = static_cast<double>(block_sum_dyn(lane_sum<M>(p, f), red));
+  const double s = static_cast<double>(block_sum_dyn(lane_sum<M>(p, f, blockIdx.x), red));
   if (threadIdx.x == 0) partials[blockIdx.x] = s;
 }
 template <DivMode M, class F>
@@ -549,8 +552,8 @@ __device__ __forceinline__ void fused_body(const RiemannParams& p, const double*
   __shared__ int is_last;
   const F f = make_functor<M, F>(p, table, table_n, lds);
   double s;
-  if constexpr (__is_same(Acc, double)) s = block_sum_dyn(lane_sum<M>(p, f), red);
-  else s = static_cast<double>(block_sum_dyn(lane_sum<M>(p, f), red_acc));
+  if constexpr (__is_same(Acc, double)) s = block_sum_dyn(lane_sum<M>(p, f, blockIdx.x), red);
+  else s = static_cast<double>(block_sum_dyn(lane_sum<M>(p, f, blockIdx.x), red_acc));
   if (!publish_and_ticket(s, partials, ticket, blockIdx.x, gridDim.x, &is_last)) return;
   const double v = ordered_partials<0, true>(partials, static_cast<int>(gridDim.x));
   rearm_slots<0>(partials, static_cast<int>(gridDim.x));
@@ -595,10 +598,10 @@ __device__ __forceinline__ void chained_body(const RiemannParams& p, const doubl
   const F f = make_functor<M, F>(p, table, table_n, lds);
   double s;
   if constexpr (__is_same(typename AccOf<F>::type, double)) {
-    s = block_sum_dyn(lane_sum<M>(p, f), red);
+    s = block_sum_dyn(lane_sum<M>(p, f, blockIdx.x), red);
   } else {
     __shared__ typename AccOf<F>::type red_acc[kMaxBlock / kWave];
-    s = static_cast<double>(block_sum_dyn(lane_sum<M>(p, f), red_acc));
+    s = static_cast<double>(block_sum_dyn(lane_sum<M>(p, f, blockIdx.x), red_acc));
   }
   if (threadIdx.x == 0) partials[blockIdx.x] = s;
 }
@@ -614,6 +617,63 @@ __global__ __launch_bounds__(kMaxBlock) kFullOccupancy void riemann_chained_kern
     RiemannParams p, const double* table, int table_n, double* partials, const double* prev,
     int nprev, double scale, double* out_prev) {
   chained_body<M, F>(p, table, table_n, partials, prev, nprev, scale, out_prev);
+}
+
+// ---------------------------------------------------------------------------- multi-step
+// K complete integrations in ONE launch (graph batches with RiemannConfig::multistep). A
+// chained batch pays every step's launch ramp, tail drain and end-of-kernel release; here the
+// workgroups stay resident for the whole batch. At step s every workgroup computes the
+// partial of its VIRTUAL block (blockIdx + s * rot) mod grid and stores it into
+// partials[s][virtual block] — no ticket, no wait, no hand-off inside the launch. The
+// rotation moves the blocks that own one tile round more than the rest (the first `rot`,
+// lane_sum) to other workgroups every step, so over a batch every workgroup does the same
+// work. multistep_close_kernel then closes all K steps at once (one workgroup per step,
+// index-ordered sums, the kernel boundary orders the partials): every step's value is the
+// fused / chained / two-kernel value at the same grid, bit for bit (a partial depends only on
+// its virtual block). The grid should be resident as a whole (riemann_multistep_grid): a
+// second round of workgroups would start only after the first finished every step.
+// Each step re-derives its sample coordinates from p.a laundered through an empty asm, so
+// nothing of a step is loop-invariant: no step's work can be hoisted out of the loop or shared
+// with another, K steps are K full integrations.
+template <DivMode M, class F>
+__device__ __forceinline__ void multistep_body(const RiemannParams& p, const double* table,
+                                               int table_n, double* partials, int steps,
+                                               unsigned rot) {
+  using Acc = typename AccOf<F>::type;
+  __shared__ double red[kMaxBlock / kWave];
+  __shared__ Acc red_acc[__is_same(Acc, double) ? 1 : kMaxBlock / kWave];
+  __shared__ double lds[lds_words<M, F>()];
+  const F f = make_functor<M, F>(p, table, table_n, lds);
+  const unsigned nb = gridDim.x;
+  unsigned vb = blockIdx.x;
+  for (int s = 0; s < steps; ++s) {
+    RiemannParams q = p;
+    asm volatile("" : "+s"(q.a));  // a fresh value every step (no instructions)
+    double v;
+    if constexpr (__is_same(Acc, double)) v = block_sum_dyn(lane_sum<M>(q, f, vb), red);
+    else v = static_cast<double>(block_sum_dyn(lane_sum<M>(q, f, vb), red_acc));
+    if (threadIdx.x == 0) partials[static_cast<size_t>(s) * nb + vb] = v;
+    __syncthreads();  // wave 0 has read red before the next step writes it
+    vb += rot;
+    if (vb >= nb) vb -= nb;
+  }
+}
+template <DivMode M, class F>
+__global__ __launch_bounds__(kMaxBlock) void riemann_multistep_kernel(
+    RiemannParams p, const double* table, int table_n, double* partials, int steps,
+    unsigned rot) {
+  multistep_body<M, F>(p, table, table_n, partials, steps, rot);
+}
+
+// Closes a multi-step launch: workgroup s sums step s's partials in index order (finalize
+// order) into out[s].
+__global__ __launch_bounds__(kMaxBlock) void multistep_close_kernel(const double* partials,
+                                                                   int nb, double scale,
+                                                                   double* out) {
+  __shared__ double red[kMaxBlock / kWave];
+  const double t = ordered_partials<0, false>(partials + static_cast<size_t>(blockIdx.x) * nb, nb);
+  const double tot = block_sum_dyn(t, red);
+  if (threadIdx.x == 0) out[blockIdx.x] = tot * scale;
 }
 
 // ---------------------------------------------------------------------------- validation
@@ -705,6 +765,22 @@ void launch_chained_t(const RiemannParams& p, LaunchShape shape, const double* t
   else
     riemann_chained_kernel<M, F><<<shape.grid, shape.block, 0, stream>>>(p, table, table_n, partials,
                                                                prev, nprev, scale, out_prev);
+}
+
+template <DivMode M, class F>
+void launch_multistep_t(const RiemannParams& p, LaunchShape shape, const double* table,
+                        int table_n, double* partials, int steps, unsigned rot,
+                        hipStream_t stream) {
+  riemann_multistep_kernel<M, F><<<shape.grid, shape.block, 0, stream>>>(p, table, table_n,
+                                                                          partials, steps, rot);
+}
+// Workgroups of the multi-step kernel resident at once on one CU at this block size.
+template <DivMode M, class F>
+void multistep_per_cu_t(int block, int* out) {
+  int n = 0;
+  MIINT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &n, reinterpret_cast<const void*>(&riemann_multistep_kernel<M, F>), block, 0));
+  *out = n;
 }
 
 // kIeee Pi4 launches take Pi4::recip_narrow when both end coordinates (the extremes: x is
@@ -808,6 +884,12 @@ template <DivMode M, class F> struct FusedOp {
 };
 template <DivMode M, class F> struct ChainedOp {
   template <class... A> static void run(A... a) { launch_chained_t<M, F>(a...); }
+};
+template <DivMode M, class F> struct MultiStepOp {
+  template <class... A> static void run(A... a) { launch_multistep_t<M, F>(a...); }
+};
+template <DivMode M, class F> struct MultiStepOccOp {
+  static void run(int block, int* out) { multistep_per_cu_t<M, F>(block, out); }
 };
 template <DivMode M, class F> struct TileLenOp {
   static void run(int* out) { *out = F::template tile_len<M>(); }
@@ -943,6 +1025,39 @@ void launch_riemann_chained(const RiemannParams& p, DType dtype, DivMode div, La
   const DivMode eff = effective_div(p, div, dtype);
   dispatch<ChainedOp>(p, dtype, eff, prepared(p, eff), shape, table, table_n, partials, prev,
                       nprev, scale, out_prev, stream);
+  MIINT_HIP(hipGetLastError());
+}
+
+int riemann_multistep_grid(const RiemannParams& p, DType dtype, DivMode div, int block,
+                          int num_cus) {
+  MIINT_CHECK(riemann_block_ok(block), "unsupported Riemann block size");
+  int per_cu = 0;
+  dispatch<MultiStepOccOp>(p, dtype, effective_div(p, div, dtype), block, &per_cu);
+  MIINT_CHECK(per_cu >= 1, "multi-step kernel does not fit a CU at this block size");
+  return per_cu * num_cus;
+}
+
+void launch_riemann_multistep(const RiemannParams& p, DType dtype, DivMode div,
+                              LaunchShape shape, const double* table, int table_n,
+                              double* partials, int steps, double scale, double* out,
+                              hipStream_t stream) {
+  check_shape(shape);
+  check_params(p, table, table_n);
+  MIINT_CHECK(steps >= 1 && steps <= kMaxMultiSteps, "multi-step launch: 1..64 steps");
+  MIINT_CHECK(partials != nullptr && out != nullptr, "multi-step launch needs partials and results");
+  const DivMode eff = effective_div(p, div, dtype);
+  // rotation: the blocks owning one tile round more than the rest (lane_sum: the first
+  // `heavy`) move by `heavy` blocks a step, so each workgroup gets its share of them
+  int tl = 0;
+  dispatch<TileLenOp>(p, dtype, eff, &tl);
+  const uint64_t lanes = static_cast<uint64_t>(shape.grid) * static_cast<uint64_t>(shape.block);
+  const uint64_t extra = (p.n / static_cast<uint64_t>(tl)) % lanes;
+  const unsigned heavy = static_cast<unsigned>((extra + shape.block - 1) / shape.block);
+  const unsigned rot = heavy % static_cast<unsigned>(shape.grid);
+  dispatch<MultiStepOp>(p, dtype, eff, prepared(p, eff), shape, table, table_n, partials, steps,
+                        rot, stream);
+  MIINT_HIP(hipGetLastError());
+  multistep_close_kernel<<<steps, shape.block, 0, stream>>>(partials, shape.grid, scale, out);
   MIINT_HIP(hipGetLastError());
 }
 

@@ -220,6 +220,7 @@ PYBIND11_MODULE(_miint, m) {
       .def_readwrite("world", &RiemannConfig::world)
       .def_readwrite("force_collective", &RiemannConfig::force_collective)
       .def_readwrite("step_streams", &RiemannConfig::step_streams)
+      .def_readwrite("multistep", &RiemannConfig::multistep)
       .def_readwrite("slice_rank", &RiemannConfig::slice_rank)
       .def_readwrite("slice_world", &RiemannConfig::slice_world)
       .def_readwrite("timeout_s", &RiemannConfig::timeout_s)
@@ -268,6 +269,7 @@ PYBIND11_MODULE(_miint, m) {
       .def_property_readonly("slots", &RiemannPlan::slots)
       .def_property_readonly("bucketed", &RiemannPlan::bucketed)
       .def_property_readonly("chained", &RiemannPlan::chained)
+      .def_property_readonly("multistep", &RiemannPlan::multistep)
       .def_property_readonly("direct", &RiemannPlan::direct)
       .def_property_readonly("graph_nodes", &RiemannPlan::graph_nodes)
       .def_property_readonly("graphs_ready", &RiemannPlan::graphs_ready)

@@ -76,6 +76,15 @@ RiemannPlan::RiemannPlan(const RiemannConfig& cfg, int device, const Comm* comm)
     if (g > cus) g -= g % cus;
     shape_.grid = static_cast<int>(g);
   }
+  // Multi-step batches keep every workgroup resident for a whole batch: the auto grid is
+  // capped at the multi-step kernel's residency (pi4 fp64: 7 x 256-thread workgroups per CU,
+  // 106 SGPRs); an explicit grid above it runs chained batches instead.
+  if (cfg.multistep) {
+    const int resident =
+        riemann_multistep_grid(params_, cfg.dtype, cfg.div, cfg.block, info.num_cus);
+    if (cfg.grid <= 0 && shape_.grid > resident) shape_.grid = resident;
+    multistep_ = shape_.grid <= resident;
+  }
 
   // chained batches: two partial halves per step stream
   const int lanes = step_streams(cfg.slots);
@@ -87,6 +96,8 @@ RiemannPlan::RiemannPlan(const RiemannConfig& cfg, int device, const Comm* comm)
   }
   slots_ = DeviceBuffer<double>(static_cast<size_t>(shape_.grid));
   fill_unset_slots(slots_.get(), slots_.size(), nullptr);
+  if (multistep_)
+    ms_partials_ = DeviceBuffer<double>(static_cast<size_t>(cfg.slots) * shape_.grid);
   result_ = DeviceBuffer<double>(static_cast<size_t>(cfg.slots));
   ticket_ = DeviceBuffer<unsigned int>(kTicketWords);
   MIINT_HIP(hipMemset(ticket_.get(), 0, ticket_.bytes()));
@@ -179,7 +190,7 @@ void RiemannPlan::enqueue_chain(hipStream_t s, int nsteps) const {
 }
 
 int RiemannPlan::step_streams(int nsteps) const {
-  if (!chained()) return 1;
+  if (!chained() || multistep_) return 1;
   const int want = cfg_.step_streams > 0            ? cfg_.step_streams
                    : params_.n >= kStepStreamsMaxCount ? 1
                                                        : kAutoStepStreams;
@@ -223,7 +234,12 @@ void RiemannPlan::enqueue_chain_streams(hipStream_t cs, int nsteps) {
 
 void RiemannPlan::enqueue_batch(hipStream_t cs, hipStream_t rs, int nsteps, bool overlap) {
   if (chained()) {
-    enqueue_chain_streams(cs, nsteps);
+    if (multistep_)
+      launch_riemann_multistep(params_, cfg_.dtype, cfg_.div, shape_, table_.get(),
+                               static_cast<int>(cfg_.table.size()), ms_partials_.get(), nsteps,
+                               scale_, result_ptr(0), cs);
+    else
+      enqueue_chain_streams(cs, nsteps);
     if (bucketed()) {  // one all-reduce + one copy of all the batch's results
       comm_->allreduce_sum(result_.get(), result_.get(), static_cast<size_t>(nsteps), cs);
       MIINT_HIP(hipMemcpyAsync(host_.get(), result_.get(), sizeof(double) * nsteps,

@@ -71,7 +71,7 @@ class Integrator:
                  b: float | None = None, force_collective: bool = False, bucket: bool = True,
                  chain: bool = True, comm_obj=None, threads: int = 0,
                  slice_of: tuple[int, int] | None = None, step_streams: int = 0,
-                 block: int = 256, **spec_kw):
+                 block: int = 256, multistep: bool = True, **spec_kw):
         spec = integrands.get(integrand, **spec_kw) if isinstance(integrand, str) else integrand
         if a is not None or b is not None:
             spec = dataclasses.replace(spec, a=spec.a if a is None else a,
@@ -114,6 +114,7 @@ class Integrator:
             cfg.bucket = bucket
             cfg.chain = chain
             cfg.step_streams = step_streams
+            cfg.multistep = multistep  # graph batches as one persistent launch
             if slice_of is not None:  # (rank, world): that rank's share, on this device
                 cfg.slice_rank, cfg.slice_world = int(slice_of[0]), int(slice_of[1])
             self._m = m

@@ -54,6 +54,44 @@ def test_chained_batches_equal_fused_bitwise(cuda, name, collective):
             assert it.plan.host_result(it.plan.host_index_of(k, True)) == want, (chain, k)
 
 
+@pytest.mark.parametrize("name", ["pi4", "pi4_fp32", "pi4_fp32acc", "sin", "table", "poly",
+                                  "train", "pi4_ieee"])
+def test_multistep_batches_equal_chained_bitwise(cuda, name):
+    """A graph batch as ONE persistent multi-step launch + a closing kernel (workgroups rotate
+    over virtual blocks from step to step) gives every step the chained batch's value, bit for
+    bit: 47 steps = two 20-step replays + a 7-step one, and 1-step batches."""
+    parts = name.split("_")
+    dtype = parts[1] if len(parts) > 1 and parts[1].startswith("fp") else "fp64"
+    div = "ieee" if name.endswith("_ieee") else "series"
+    kw = dict(n=60_000_011, rule="mid", dtype=dtype, div=div)
+    ms = Integrator(parts[0], slots=20, **kw)
+    ch = Integrator(parts[0], slots=20, multistep=False, grid=ms.plan.grid, **kw)
+    assert ms.plan.multistep and not ch.plan.multistep and ms.plan.grid == ch.plan.grid
+    assert ms.plan.step_streams(20) == 1
+    for it in (ms, ch):
+        it.run_steps(47, pipeline=True, graphs=True)
+        assert it.plan.graphs_ready, it.plan.graph_error
+    assert ms.plan.graph_nodes == 2  # the persistent kernel and the closing kernel
+    got = [ms.plan.host_result(ms.plan.host_index_of(k, True)) for k in range(40, 47)]
+    want = [ch.plan.host_result(ch.plan.host_index_of(k, True)) for k in range(40, 47)]
+    assert got == want and len(set(got)) == 1
+    one = Integrator(parts[0], slots=1, **kw)
+    one.run_steps(3, pipeline=True, graphs=True)
+    assert one.plan.host_result(one.plan.host_index_of(2, True)) == want[0]
+
+
+def test_multistep_residency_rules_the_grid(cuda):
+    """The auto grid is capped at the multi-step kernel's residency (every workgroup of a
+    persistent launch resident at once); an explicit grid above it runs chained batches."""
+    it = Integrator("pi4", n=10**9)
+    g = it.plan.grid
+    assert it.plan.multistep and 0 < g <= 8 * 256 and g % 256 == 0
+    big = Integrator("pi4", n=10**9, grid=g + 256)
+    assert big.plan.grid == g + 256 and not big.plan.multistep and big.plan.chained
+    small = Integrator("pi4", n=10**7)  # small N keeps its small auto grid
+    assert small.plan.multistep and small.plan.grid <= g
+
+
 @pytest.mark.parametrize("bucket", [True, False])
 @pytest.mark.parametrize("graphs", [False, True])
 def test_plan_rccl_stage_on_one_gpu(cuda, graphs, bucket):

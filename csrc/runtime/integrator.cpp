@@ -322,7 +322,8 @@ bool RiemannPlan::use_graphs(bool requested, int steps) {
 }
 
 int RiemannPlan::host_index_of(int k, bool graphs) const {
-  const bool batched = last_mode_ < 0 ? ((graphs && graphs_ready()) || bucketed()) : last_mode_ == 1;
+  const bool batched = last_mode_ < 0 ? ((graphs && graphs_ready()) || bucketed() || multistep())
+                                       : last_mode_ == 1;
   return batched ? k % cfg_.slots : k % host_capacity();
 }
 
@@ -347,8 +348,9 @@ void RiemannPlan::launch_steps(int steps, bool pipeline, bool graphs) {
     return;
   }
   direct_steps_ += steps;
-  last_mode_ = bucketed() ? 1 : 0;
-  if (bucketed()) {
+  last_mode_ = (bucketed() || multistep()) ? 1 : 0;
+  if (bucketed() || multistep()) {  // whole batches enqueued directly (a multi-step batch is
+                                    // two launches: no graph needed)
     for (int k = 0; k < steps; k += S) enqueue_batch(cs, rs, std::min(S, steps - k), false);
     return;
   }

@@ -471,16 +471,16 @@ def test_step_streams_bitwise(native, cuda, streams):
     """Chained graph batches dealt over several streams (each its own chain, own partials,
     own finalize; the compute stream joins them) give every step exactly the one-stream
     result, bitwise — including remainder batches whose step count the streams do not
-    divide."""
+    divide. (Chained batches: multistep=False; a multi-step batch is one launch.)"""
     from cuda_v_mpi_amd import Integrator
 
     n = 10**8 + 7
-    ref = Integrator("pi4", n=n, rule="mid", slots=48, step_streams=1)
+    ref = Integrator("pi4", n=n, rule="mid", slots=48, step_streams=1, multistep=False)
     assert ref.plan.step_streams(48) == 1
     ref.plan.run_steps(48, False, True)
     want = [ref.plan.host_result(ref.plan.host_index_of(k, True)) for k in range(48)]
     assert len(set(want)) == 1
-    it = Integrator("pi4", n=n, rule="mid", slots=48, step_streams=streams)
+    it = Integrator("pi4", n=n, rule="mid", slots=48, step_streams=streams, multistep=False)
     assert it.plan.step_streams(48) == streams
     for steps in (48, 29, 5):
         it.plan.run_steps(steps, False, True)
@@ -489,12 +489,15 @@ def test_step_streams_bitwise(native, cuda, streams):
 
 
 def test_step_streams_auto_policy(native, cuda):
-    """Auto: four streams below 6e8 samples per step, one at or above (N = 1e9 on one GPU)."""
+    """Auto (chained batches): four streams below 6e8 samples per step, one at or above (N =
+    1e9 on one GPU); a multi-step batch (the default) is one launch on one stream."""
     from cuda_v_mpi_amd import Integrator
 
-    assert Integrator("pi4", n=10**9, slots=48).plan.step_streams(48) == 1
-    assert Integrator("pi4", n=10**9, slots=48, slice_of=(0, 8)).plan.step_streams(48) == 4
-    assert Integrator("pi4", n=10**9, slots=48, slice_of=(0, 8)).plan.step_streams(3) == 3
+    kw = dict(n=10**9, slots=48, multistep=False)
+    assert Integrator("pi4", **kw).plan.step_streams(48) == 1
+    assert Integrator("pi4", slice_of=(0, 8), **kw).plan.step_streams(48) == 4
+    assert Integrator("pi4", slice_of=(0, 8), **kw).plan.step_streams(3) == 3
+    assert Integrator("pi4", n=10**9, slots=48, slice_of=(0, 8)).plan.step_streams(48) == 1
 
 
 def test_table2d_step_streams_equal(native, cuda):

@@ -596,7 +596,8 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
 
         m = native()
         g = 4096
-        p2 = m.Table2DPlan(g, 1800.0, ctx.device, comm, not args.no_bucket)
+        p2 = m.Table2DPlan(g, 1800.0, ctx.device, comm, not args.no_bucket,
+                           multistep=not args.no_multistep)
         p2.run()
         # each time() call first replays ~30 ms untimed (steady clocks); best of 3
         ms = min(p2.time(p2.graph_steps * 10, True) for _ in range(3))
@@ -610,7 +611,7 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
             "samples_per_s": g * g / (ms * 1e-3), "result": v, "midpoint_oracle": want,
             "rel_err_vs_oracle": rel, "rows_this_rank": [p2.row0, p2.row1],
             "bucketed_allreduce": bool(p2.bucketed), "n_gpus": ctx.world,
-            "step_streams": p2.step_streams,
+            "step_streams": p2.step_streams, "multistep": bool(p2.multistep),
             "verified": bool(rel <= 1e-12)}
         del p2
     # (6) BASELINE config #4: the same integral through the packed-fp32 path. Samples are

@@ -217,7 +217,7 @@ constexpr const char* kUsage =
     "                   [--no-multistep] [--slots K]\n"
     "       miint sweep [--gpus G]\n"
     "       miint table2d [--grid 4096] [--gpus G] [--slice R/W] [--no-graph]\n"
-    "                     [--step-streams S] [--min-wg W] [--settle-ms MS]\n"
+    "                     [--step-streams S] [--min-wg W] [--settle-ms MS] [--no-multistep]\n"
     "       miint selfcheck\n"
     "       miint comm [--gpus G] [--max-bytes 144e6] [--iters 20]\n"
     "Every record is one JSON line on stdout; --jsonl FILE also appends it to FILE.\n";
@@ -272,6 +272,7 @@ int main(int argc, char** argv) {
       c.step_streams = static_cast<int>(a.integer("step-streams", 0));  // chains per replay
       c.min_wg = static_cast<int>(a.integer("min-wg", 0));
       c.settle_ms = a.num("settle-ms", c.settle_ms);
+      c.multistep = !a.flag("no-multistep");  // A-B: chained launches per integration
       // --slice R/W: time only rank R's rows of a W-GPU split, on this GPU (no collective)
       const std::string sl = a.str("slice", "");
       if (!sl.empty()) {
@@ -281,7 +282,7 @@ int main(int argc, char** argv) {
         c.world = std::stoi(sl.substr(k + 1));
       }
       double value = 0.0, timed = 0.0, ms = 0.0;
-      bool bucketed = false, chained = false;
+      bool bucketed = false, chained = false, multistep = false;
       int streams = 1;
       std::mutex mu;
       cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
@@ -294,6 +295,7 @@ int main(int argc, char** argv) {
           timed = plan.last_result();
           bucketed = plan.bucketed() && graphs;
           chained = plan.chained() && graphs;
+          multistep = plan.multistep() && graphs;
           streams = chained ? plan.step_streams() : 1;
         }
         if (t > ms) ms = t;
@@ -301,7 +303,7 @@ int main(int argc, char** argv) {
       if (topo.rank0 == 0) {
         cli::JsonRecord r;
         r.add("program", "table2d").add("grid", c.grid);
-        r.add("step_streams", streams);
+        r.add("step_streams", streams).add("multistep", multistep);
         if (c.world > 1) {
           r.add("slice", std::to_string(c.rank) + "/" + std::to_string(c.world))
               .add("partial", value);

@@ -216,6 +216,13 @@ int table2d_grid(const Table2DParams& p);
 // Which kernel a launch runs: "stream" (LDS footprint + row streaming, fine grids) or
 // "tile" (coarse grids, table read from global memory).
 const char* table2d_path(const Table2DParams& p);
+// Multi-step row stream: `steps` integrations in one launch of resident workgroups, then one
+// closing kernel: outs[s] = integration s, bitwise the chained / fused value. `partials`
+// holds steps x table2d_grid(p) doubles. Only for launches table2d_multistep_ok accepts (the
+// row-stream shape, every workgroup resident at once on num_cus CUs).
+bool table2d_multistep_ok(const Table2DParams& p, int num_cus);
+void launch_table2d_multistep(const Table2DParams& p, double* partials, int steps, double* outs,
+                              hipStream_t stream);
 void launch_table2d_partials(const Table2DParams& p, double* partials, hipStream_t stream);
 // One launch: partials + last-workgroup reduction into out[0] (ticket: kTicketWords words,
 // zero before the first launch; partials: table2d_grid(p) doubles filled with the unset

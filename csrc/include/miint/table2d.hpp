@@ -44,6 +44,11 @@ struct Table2DConfig {
   // result), so one launch's staging latency and tail overlap the next one's work. 0 = auto
   // (kAutoT2Streams); 1 = one chain on the plan's stream.
   int step_streams = 0;
+  // Chained graph timing as ONE multi-step launch of resident workgroups for the replay's
+  // kGraphSteps integrations plus one closing kernel (launch_table2d_multistep): one launch
+  // ramp and tail per replay. Used when the row-stream shape fits the GPU at once; bitwise
+  // the same values.
+  bool multistep = true;
   int min_wg = 0;  // row stream: fewest workgroups its shape aims for (0 = kernel default)
   double settle_ms = 30.0;  // graph time(): untimed warm-up replays first (steady clocks)
 };
@@ -68,6 +73,8 @@ class Table2DPlan {
   bool chained() const { return cfg_.chain && (!comm_ || world_ == 1 || bucketed_); }
   static constexpr int kGraphSteps = 32;
   int step_streams() const;  // chains a chained replay runs (1 when not chained)
+  // A chained replay is one multi-step launch (Table2DConfig::multistep, in effect).
+  bool multistep() const { return chained() && multistep_; }
   int row0() const { return row0_; }
   int row1() const { return row1_; }
 
@@ -75,6 +82,8 @@ class Table2DPlan {
   void enqueue(hipStream_t s);
   void launch_local(double* out, hipStream_t s);  // this rank's rows -> *out (device ptr)
   Table2DConfig cfg_;
+  bool multistep_ = false;
+  DeviceBuffer<double> ms_partials_;  // multistep: kGraphSteps x workgroups
   int device_;
   const Comm* comm_;
   int rank_ = 0, world_ = 1;

@@ -282,21 +282,21 @@ __device__ __forceinline__ double fma_sv(double a, double s, double c) {
   return r;
 }
 
+// One workgroup's share of a row-stream integration: column block bx, row block by (the
+// launch's blockIdx, or the multi-step kernel's). Returns the block's partial in thread 0.
+// `between` runs while the staging loads are in flight (the chained close).
 // POISON (validation instantiation, set_lds_poison): tile slots outside the computed footprint
 // hold NaN instead of the corner value, so a read outside the footprint shows.
-template <int MODE, int SH, bool POISON>
-__global__ __launch_bounds__(kB) void table2d_stream_kernel(Table2DParams p, int rows_per_wave,
-                                                            double* partials, unsigned* ticket,
-                                                            double* out, Table2DChain chain) {
-  __shared__ double tile[SH * kSW];
-  __shared__ double red[kB / kWave];
-  __shared__ int is_last;
+template <int SH, bool POISON, class Between>
+__device__ __forceinline__ double table2d_stream_block(const Table2DParams& p, int rows_per_wave,
+                                                       int bx, int by, double* tile, double* red,
+                                                       Between between) {
   const double sx = p.X / p.gx, sy = p.Y / p.gy;
   const double cx = (p.nx - 1) / p.X, cy = (p.ny - 1) / p.Y;
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) / kWave);
   const int lane = static_cast<int>(threadIdx.x) % kWave;
-  const int c0 = blockIdx.x * (kWave * kSCols);
-  const int r0 = p.row0 + blockIdx.y * (4 * rows_per_wave);
+  const int c0 = bx * (kWave * kSCols);
+  const int r0 = p.row0 + by * (4 * rows_per_wave);
   const int r1 = min(r0 + 4 * rows_per_wave, p.row1);
   // table footprint of the workgroup's samples (first / last column and row)
   // (computed on the VALU: readfirstlane moves the uniform results to SGPRs, so the staging
@@ -329,10 +329,7 @@ __global__ __launch_bounds__(kB) void table2d_stream_kernel(Table2DParams p, int
     // chained: workgroup 0 closes the previous integration while its staging loads fly
     // (the loads above hold 32 VGPRs; the kernel is LDS-limited to 4 waves per SIMD, whose
     // 128-VGPR budget the close's 16 loads in flight fit beside them)
-    if constexpr (MODE == kT2Chained) {
-      if (chain.prev && blockIdx.x == 0 && blockIdx.y == 0)
-        table2d_close(chain.prev, chain.prev_n, chain.prev_out, red);
-    }
+    between();
 #pragma unroll
     for (int j = 0; j < kPasses; ++j) tile[(ly + kRowsPer * j) * kSW + lx] = v[j];
     if constexpr (POISON) {  // validation: NaN in the tile slots outside the footprint
@@ -402,7 +399,23 @@ __global__ __launch_bounds__(kB) void table2d_stream_kernel(Table2DParams p, int
   double a = 0.0;
 #pragma unroll
   for (int b = 0; b < kSCols; ++b) a += ok[b] ? acc[b] : 0.0;
-  const double s = block_sum<kB>(a, red) * (sx * sy);
+  return block_sum<kB>(a, red) * (sx * sy);
+}
+
+template <int MODE, int SH, bool POISON>
+__global__ __launch_bounds__(kB) void table2d_stream_kernel(Table2DParams p, int rows_per_wave,
+                                                            double* partials, unsigned* ticket,
+                                                            double* out, Table2DChain chain) {
+  __shared__ double tile[SH * kSW];
+  __shared__ double red[kB / kWave];
+  __shared__ int is_last;
+  const double s = table2d_stream_block<SH, POISON>(
+      p, rows_per_wave, blockIdx.x, blockIdx.y, tile, red, [&] {
+        if constexpr (MODE == kT2Chained) {
+          if (chain.prev && blockIdx.x == 0 && blockIdx.y == 0)
+            table2d_close(chain.prev, chain.prev_n, chain.prev_out, red);
+        }
+      });
   const unsigned bid = blockIdx.y * gridDim.x + blockIdx.x;
   if constexpr (MODE != kT2Fused) {
     if (threadIdx.x == 0) partials[bid] = s;
@@ -415,6 +428,36 @@ __global__ __launch_bounds__(kB) void table2d_stream_kernel(Table2DParams p, int
     if (threadIdx.x == 0) out[0] = tot;
     rearm_ticket(ticket, nb);
   }
+}
+
+// Multi-step row stream (Table2DConfig::multistep): `steps` complete integrations in one
+// launch of resident workgroups (a 1-D grid of the stream shape's gx x gy blocks, block b =
+// column block b % gx, row block b / gx: the same linear index as the 2-D launch). Each step
+// stages its table footprint again and writes partials[step][b]; multistep_close sums every
+// step's partials in index order — bitwise the chained / fused value. One launch ramp and
+// tail per replay instead of per integration. The table pointer is laundered through an empty
+// asm every step, so no step's loads or arithmetic can be hoisted or shared.
+template <int SH>
+__global__ __launch_bounds__(kB) void table2d_multistep_kernel(Table2DParams p, int rows_per_wave,
+                                                               int gx, double* partials,
+                                                               int steps) {
+  __shared__ double tile[SH * kSW];
+  __shared__ double red[kB / kWave];
+  const unsigned nb = gridDim.x;
+  const int bx = static_cast<int>(blockIdx.x) % gx, by = static_cast<int>(blockIdx.x) / gx;
+  for (int st = 0; st < steps; ++st) {
+    Table2DParams q = p;
+    asm volatile("" : "+s"(q.table));  // a fresh pointer every step (no instructions)
+    const double v = table2d_stream_block<SH, false>(q, rows_per_wave, bx, by, tile, red, [] {});
+    if (threadIdx.x == 0) partials[static_cast<size_t>(st) * nb + blockIdx.x] = v;
+    __syncthreads();  // the next step rewrites tile and red
+  }
+}
+
+__global__ __launch_bounds__(kB) void table2d_multistep_close_kernel(const double* partials,
+                                                                     int nb, double* outs) {
+  __shared__ double red[kB / kWave];
+  table2d_close(partials + static_cast<size_t>(blockIdx.x) * nb, nb, outs + blockIdx.x, red);
 }
 
 }  // namespace
@@ -564,6 +607,42 @@ void launch_table2d_chained(const Table2DParams& p, double* partials, const doub
   MIINT_CHECK(prev == nullptr || prev != partials, "chained table2d: prev aliases partials");
   const int nb = table2d_grid(p);
   launch_table2d<kT2Chained>(p, partials, nullptr, nullptr, {prev, nb, prev_out}, stream);
+}
+
+namespace {
+template <int SH>
+int t2d_ms_per_cu() {
+  int n = 0;
+  MIINT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &n, reinterpret_cast<const void*>(&table2d_multistep_kernel<SH>), kB, 0));
+  return n;
+}
+}  // namespace
+
+bool table2d_multistep_ok(const Table2DParams& p, int num_cus) {
+  check_table2d(p);
+  const Table2DShape sh = table2d_shape(p);
+  if (!sh.stream) return false;
+  const int per_cu = sh.short_tile ? t2d_ms_per_cu<kSHShort>() : t2d_ms_per_cu<kSH>();
+  return static_cast<long>(sh.grid.x) * sh.grid.y <= static_cast<long>(per_cu) * num_cus;
+}
+
+void launch_table2d_multistep(const Table2DParams& p, double* partials, int steps, double* outs,
+                              hipStream_t stream) {
+  check_table2d(p);
+  MIINT_CHECK(steps >= 1 && steps <= 1024, "table2d multi-step: 1..1024 steps");
+  const Table2DShape sh = table2d_shape(p);
+  MIINT_CHECK(sh.stream, "table2d multi-step runs the row-stream shape only");
+  const int nb = static_cast<int>(sh.grid.x * sh.grid.y);
+  const int gx = static_cast<int>(sh.grid.x);
+  if (sh.short_tile)
+    table2d_multistep_kernel<kSHShort><<<nb, kB, 0, stream>>>(p, sh.rows_per_wave, gx, partials,
+                                                             steps);
+  else
+    table2d_multistep_kernel<kSH><<<nb, kB, 0, stream>>>(p, sh.rows_per_wave, gx, partials, steps);
+  MIINT_HIP(hipGetLastError());
+  table2d_multistep_close_kernel<<<steps, kB, 0, stream>>>(partials, nb, outs);
+  MIINT_HIP(hipGetLastError());
 }
 
 void launch_table2d_finalize(const double* partials, int n, double* out, hipStream_t stream) {

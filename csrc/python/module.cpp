@@ -429,13 +429,15 @@ PYBIND11_MODULE(_miint, m) {
   // ------------------------------------------------------------------ 2-D field plan
   py::class_<Table2DPlan>(m, "Table2DPlan")
       .def(py::init([](int grid, double extent, int device, const Comm* comm, bool bucket,
-                       bool chain, int step_streams, int slice_rank, int slice_world) {
+                       bool chain, int step_streams, int slice_rank, int slice_world,
+                       bool multistep) {
              Table2DConfig c;
              c.grid = grid;
              c.extent = extent;
              c.bucket = bucket;
              c.chain = chain;
              c.step_streams = step_streams;
+             c.multistep = multistep;
              c.rank = slice_rank;   // without a communicator: that rank's rows only
              c.world = slice_world;
              return new Table2DPlan(c, device, comm);
@@ -443,9 +445,10 @@ PYBIND11_MODULE(_miint, m) {
            py::arg("grid") = 4096, py::arg("extent") = 1800.0, py::arg("device") = 0,
            py::arg("comm") = nullptr, py::arg("bucket") = true, py::arg("chain") = true,
            py::arg("step_streams") = 0, py::arg("slice_rank") = 0, py::arg("slice_world") = 1,
-           py::keep_alive<1, 5>())
+           py::arg("multistep") = true, py::keep_alive<1, 5>())
       .def_property_readonly("step_streams",
                              [](const Table2DPlan& p) { return p.step_streams(); })
+      .def_property_readonly("multistep", &Table2DPlan::multistep)
       .def("run", &Table2DPlan::run, py::call_guard<py::gil_scoped_release>())
       .def("time", &Table2DPlan::time, py::arg("iters"), py::arg("graphs") = true,
            py::call_guard<py::gil_scoped_release>())

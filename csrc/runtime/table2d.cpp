@@ -32,6 +32,9 @@ Table2DPlan::Table2DPlan(const Table2DConfig& cfg, int device, const Comm* comm)
   const Table2DParams p{table_.get(), n, n, cfg.extent, cfg.extent, cfg.grid, cfg.grid,
                         row0_, std::max(row1_, row0_ + 1), cfg.min_wg};
   partials_ = DeviceBuffer<double>(static_cast<size_t>(table2d_grid(p)));
+  multistep_ = cfg.multistep && row1_ > row0_ &&
+               table2d_multistep_ok(p, device_info(device).num_cus);
+  if (multistep_) ms_partials_ = DeviceBuffer<double>(kGraphSteps * partials_.size());
   const int L = step_streams();
   // chained launches: a double buffer per chain
   chain_ = DeviceBuffer<double>(2 * static_cast<size_t>(L) * partials_.size());
@@ -49,7 +52,7 @@ Table2DPlan::Table2DPlan(const Table2DConfig& cfg, int device, const Comm* comm)
 }
 
 int Table2DPlan::step_streams() const {
-  if (!chained()) return 1;
+  if (!chained() || multistep_) return 1;
   return std::max(1, std::min(kGraphSteps, cfg_.step_streams > 0 ? cfg_.step_streams
                                                                   : kAutoT2Streams));
 }
@@ -107,6 +110,11 @@ double Table2DPlan::time(int iters, bool graphs) {
       double* outs = multi ? result_.get() : host_.device_ptr();
       if (row1_ <= row0_) {  // more ranks than rows
         MIINT_HIP(hipMemsetAsync(outs, 0, kGraphSteps * sizeof(double), cs));
+      } else if (multistep()) {  // one launch for the replay's integrations + one close
+        const int n = static_cast<int>(oracle::profile_table().size());
+        const Table2DParams p{table_.get(), n, n, cfg_.extent, cfg_.extent, cfg_.grid,
+                              cfg_.grid, row0_, row1_, cfg_.min_wg};
+        launch_table2d_multistep(p, ms_partials_.get(), kGraphSteps, outs, cs);
       } else if (chained()) {
         // integration i runs on chain i % L as that chain's step i / L: launch j of a chain
         // closes the chain's launch j - 1 (its workgroup 0), a finalize closes each chain,

@@ -501,11 +501,37 @@ def test_step_streams_auto_policy(native, cuda):
 
 
 def test_table2d_step_streams_equal(native, cuda):
-    """The 2-D replay on 1, 2 and 4 chained streams: the same 32 results, bitwise."""
+    """The 2-D replay on 1, 2 and 4 chained streams and as one multi-step launch: the same 32
+    results, bitwise."""
     res = []
     for ss in (1, 2, 4):
-        p = native.Table2DPlan(4096, 1800.0, 0, None, True, True, ss)
-        assert p.step_streams == ss
+        p = native.Table2DPlan(4096, 1800.0, 0, None, True, True, ss, multistep=False)
+        assert p.step_streams == ss and not p.multistep
         p.time(p.graph_steps, True)
         res.append(p.last_result())
-    assert res[0] == res[1] == res[2] == native.table2d_oracle(4096)
+    ms = native.Table2DPlan(4096, 1800.0, 0, None, True, True, 2)
+    assert ms.multistep and ms.step_streams == 1
+    ms.time(ms.graph_steps, True)
+    res.append(ms.last_result())
+    assert res[0] == res[1] == res[2] == res[3] == native.table2d_oracle(4096)
+
+
+@pytest.mark.parametrize("g,sl", [(4096, (0, 8)), (4096, (7, 8)), (5000, (3, 8)), (4096, (0, 1)),
+                                  (4095, (0, 4))])
+def test_table2d_multistep_equals_chained(native, cuda, g, sl):
+    """Row slices and grids of several shapes: the multi-step replay (every integration
+    re-stages its footprint in one persistent launch) gives the chained replay's partial,
+    bitwise."""
+    a = native.Table2DPlan(g, 1800.0, 0, None, True, True, 1, sl[0], sl[1], multistep=False)
+    b = native.Table2DPlan(g, 1800.0, 0, None, True, True, 1, sl[0], sl[1])
+    assert b.multistep
+    a.time(a.graph_steps, True)
+    b.time(b.graph_steps, True)
+    assert a.last_result() == b.last_result()
+
+
+def test_table2d_multistep_needs_residency(native, cuda):
+    """8192^2 in one piece needs more row-stream workgroups than the GPU holds at once: the
+    plan keeps chained launches (a persistent launch must be resident as a whole)."""
+    p = native.Table2DPlan(8192, 1800.0, 0, None, True, True, 0)
+    assert not p.multistep and p.step_streams == 2

@@ -125,7 +125,8 @@ void launch_riemann_chained(const RiemannParams& p, DType dtype, DivMode div, La
 // K = `steps` complete integrations in one persistent launch, closed by one K-workgroup
 // kernel (riemann.hip "multi-step"): out[s] = step s's scaled sum, bitwise the fused /
 // chained / two-kernel value at the same grid. `partials` holds steps x grid doubles. The
-// grid should be resident as a whole: at most riemann_multistep_grid(...) workgroups.
+// grid should be resident as a whole: at most riemann_multistep_grid(...) workgroups (0 for
+// the instantiations that keep chained batches).
 // 1 <= steps <= kMaxMultiSteps.
 constexpr int kMaxMultiSteps = 64;
 int riemann_multistep_grid(const RiemannParams& p, DType dtype, DivMode div, int block,

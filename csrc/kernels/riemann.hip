@@ -664,6 +664,28 @@ __global__ __launch_bounds__(kMaxBlock) void riemann_multistep_kernel(
     unsigned rot) {
   multistep_body<M, F>(p, table, table_n, partials, steps, rot);
 }
+template <DivMode M, class F>
+__global__ __launch_bounds__(kMaxBlock) kFullOccupancy void riemann_multistep_kernel_o8(
+    RiemannParams p, const double* table, int table_n, double* partials, int steps,
+    unsigned rot) {
+  multistep_body<M, F>(p, table, table_n, partials, steps, rot);
+}
+// The step loop's state lifts every multi-step kernel to 106 SGPRs: 7 waves per SIMD. Those
+// with few VGPRs take the 8-wave hint instead (the extra SGPRs go to VGPR lanes, outside the
+// tile loop): the per-sample IEEE division tiles, latency-bound, ran 3.4 % slower at 7
+// (profiles/r3/multistep_ab.md).
+template <DivMode M, class F>
+constexpr bool multistep_o8() {
+  return M == DivMode::kIeee && (__is_same(F, Pi4) || __is_same(F, Pi4Wide) ||
+                                 __is_same(F, Pi4F32) || __is_same(F, Pi4F32Wide) ||
+                                 __is_same(F, Pi4F32Acc32));
+}
+// Instantiations the multi-step batch does not pay for: the table's segment tiles hold 106
+// VGPRs in it (4 waves per SIMD against 8 chained): 70.3 vs 69.4 us per 1e9.
+template <DivMode M, class F>
+constexpr bool multistep_pays() {
+  return !(__is_same(F, Table) || __is_same(F, TableF32));
+}
 
 // Closes a multi-step launch: workgroup s sums step s's partials in index order (finalize
 // order) into out[s].
@@ -771,15 +793,26 @@ template <DivMode M, class F>
 void launch_multistep_t(const RiemannParams& p, LaunchShape shape, const double* table,
                         int table_n, double* partials, int steps, unsigned rot,
                         hipStream_t stream) {
-  riemann_multistep_kernel<M, F><<<shape.grid, shape.block, 0, stream>>>(p, table, table_n,
-                                                                          partials, steps, rot);
+  if constexpr (multistep_o8<M, F>())
+    riemann_multistep_kernel_o8<M, F><<<shape.grid, shape.block, 0, stream>>>(
+        p, table, table_n, partials, steps, rot);
+  else
+    riemann_multistep_kernel<M, F><<<shape.grid, shape.block, 0, stream>>>(
+        p, table, table_n, partials, steps, rot);
 }
 // Workgroups of the multi-step kernel resident at once on one CU at this block size.
+// (0 for instantiations whose batches run chained: multistep_pays)
 template <DivMode M, class F>
 void multistep_per_cu_t(int block, int* out) {
   int n = 0;
-  MIINT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      &n, reinterpret_cast<const void*>(&riemann_multistep_kernel<M, F>), block, 0));
+  if constexpr (!multistep_pays<M, F>())
+    n = 0;
+  else if constexpr (multistep_o8<M, F>())
+    MIINT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &n, reinterpret_cast<const void*>(&riemann_multistep_kernel_o8<M, F>), block, 0));
+  else
+    MIINT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &n, reinterpret_cast<const void*>(&riemann_multistep_kernel<M, F>), block, 0));
   *out = n;
 }
 
@@ -1033,8 +1066,7 @@ int riemann_multistep_grid(const RiemannParams& p, DType dtype, DivMode div, int
   MIINT_CHECK(riemann_block_ok(block), "unsupported Riemann block size");
   int per_cu = 0;
   dispatch<MultiStepOccOp>(p, dtype, effective_div(p, div, dtype), block, &per_cu);
-  MIINT_CHECK(per_cu >= 1, "multi-step kernel does not fit a CU at this block size");
-  return per_cu * num_cus;
+  return per_cu * num_cus;  // 0: this instantiation runs chained batches
 }
 
 void launch_riemann_multistep(const RiemannParams& p, DType dtype, DivMode div,

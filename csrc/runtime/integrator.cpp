@@ -82,8 +82,8 @@ RiemannPlan::RiemannPlan(const RiemannConfig& cfg, int device, const Comm* comm)
   if (cfg.multistep) {
     const int resident =
         riemann_multistep_grid(params_, cfg.dtype, cfg.div, cfg.block, info.num_cus);
-    if (cfg.grid <= 0 && shape_.grid > resident) shape_.grid = resident;
-    multistep_ = shape_.grid <= resident;
+    if (resident > 0 && cfg.grid <= 0 && shape_.grid > resident) shape_.grid = resident;
+    multistep_ = resident > 0 && shape_.grid <= resident;
   }
 
   // chained batches: two partial halves per step stream

@@ -36,7 +36,7 @@ VALU_SLACK = 1.03
 
 # name -> (kernel file, symbol regex, samples per hot-loop iteration or 0 = not one tile)
 CH = r"riemann_chained_kernel(?:_o8)?ILNS_7DivModeE"
-MS = r"riemann_multistep_kernelILNS_7DivModeE"
+MS = r"riemann_multistep_kernel(?:_o8)?ILNS_7DivModeE"
 GUARDED = {
     "pi4_series": ("riemann", CH + r"0ENS_3Pi4EE", 192),
     "pi4_ieee": ("riemann", CH + r"1ENS_3Pi4EE", 32),
@@ -56,7 +56,6 @@ GUARDED = {
     "ms_sin_series": ("riemann", MS + r"0ENS_3SinEE", 0),
     "ms_sin_ieee": ("riemann", MS + r"1ENS_3SinEE", 0),
     "ms_train_series": ("riemann", MS + r"0ENS_8TrainVelEE", 0),
-    "ms_table_series": ("riemann", MS + r"0ENS_5TableEE", 0),
     "ms_poly7_series": ("riemann", MS + r"0ENS_4PolyILi7EEE", 0),
     "table2d_stream_0_16": ("table", r"table2d_stream_kernelILi0ELi16ELb0EE", 0),
     "table2d_stream_0_32": ("table", r"table2d_stream_kernelILi0ELi32ELb0EE", 0),

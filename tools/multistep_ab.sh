@@ -29,7 +29,7 @@ for rep in 1 2; do
   run pi4_ieee bench --integrand pi4 --div ieee --iters 40 --slots 20
   run sin bench --integrand sin --iters 200 --slots 20
   run train bench --integrand train --iters 200 --slots 20
-  run table bench --integrand table --iters 200 --slots 20
+  run table bench --integrand table --iters 200 --slots 20  # chained either way (multistep_pays)
   run poly bench --integrand poly --iters 100 --slots 20
   run t2d_4096 table2d --grid 4096
   run t2d_4096_slice_0_8 table2d --grid 4096 --slice 0/8

@@ -672,19 +672,20 @@ __global__ __launch_bounds__(kMaxBlock) kFullOccupancy void riemann_multistep_ke
 }
 // The step loop's state lifts every multi-step kernel to 106 SGPRs: 7 waves per SIMD. Those
 // with few VGPRs take the 8-wave hint instead (the extra SGPRs go to VGPR lanes, outside the
-// tile loop): the per-sample IEEE division tiles, latency-bound, ran 3.4 % slower at 7
-// (profiles/r3/multistep_ab.md).
+// tile loop).
 template <DivMode M, class F>
 constexpr bool multistep_o8() {
-  return M == DivMode::kIeee && (__is_same(F, Pi4) || __is_same(F, Pi4Wide) ||
-                                 __is_same(F, Pi4F32) || __is_same(F, Pi4F32Wide) ||
+  return M == DivMode::kIeee && (__is_same(F, Pi4F32) || __is_same(F, Pi4F32Wide) ||
                                  __is_same(F, Pi4F32Acc32));
 }
-// Instantiations the multi-step batch does not pay for: the table's segment tiles hold 106
-// VGPRs in it (4 waves per SIMD against 8 chained): 70.3 vs 69.4 us per 1e9.
+// Instantiations the multi-step batch does not pay for (profiles/r3/multistep_ab.md): the
+// table's segment tiles hold 106 VGPRs in it (4 waves per SIMD against 8 chained: 70.3 vs
+// 69.4 us per 1e9), and the fp64 per-sample IEEE division tiles ran 3.3 % slower even at 8
+// waves (371 vs 359 us).
 template <DivMode M, class F>
 constexpr bool multistep_pays() {
-  return !(__is_same(F, Table) || __is_same(F, TableF32));
+  return !(__is_same(F, Table) || __is_same(F, TableF32) ||
+           (M == DivMode::kIeee && (__is_same(F, Pi4) || __is_same(F, Pi4Wide))));
 }
 
 // Closes a multi-step launch: workgroup s sums step s's partials in index order (finalize

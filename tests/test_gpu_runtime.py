@@ -54,8 +54,8 @@ def test_chained_batches_equal_fused_bitwise(cuda, name, collective):
             assert it.plan.host_result(it.plan.host_index_of(k, True)) == want, (chain, k)
 
 
-@pytest.mark.parametrize("name", ["pi4", "pi4_fp32", "pi4_fp32acc", "sin", "table", "poly",
-                                  "train", "pi4_ieee"])
+@pytest.mark.parametrize("name", ["pi4", "pi4_fp32", "pi4_fp32acc", "sin", "poly", "train",
+                                  "sin_ieee", "pi4_fp32_ieee"])
 def test_multistep_batches_equal_chained_bitwise(cuda, name):
     """A graph batch as ONE persistent multi-step launch + a closing kernel (workgroups rotate
     over virtual blocks from step to step) gives every step the chained batch's value, bit for
@@ -78,6 +78,14 @@ def test_multistep_batches_equal_chained_bitwise(cuda, name):
     one = Integrator(parts[0], slots=1, **kw)
     one.run_steps(3, pipeline=True, graphs=True)
     assert one.plan.host_result(one.plan.host_index_of(2, True)) == want[0]
+
+
+@pytest.mark.parametrize("name,div", [("table", "series"), ("pi4", "ieee")])
+def test_multistep_not_where_it_does_not_pay(cuda, name, div):
+    """The table's segment tiles and the fp64 per-sample IEEE division measured slower as
+    multi-step batches: their plans keep chained batches (multistep_pays)."""
+    it = Integrator(name, n=10**8, div=div)
+    assert it.plan.chained and not it.plan.multistep
 
 
 def test_multistep_residency_rules_the_grid(cuda):

@@ -51,7 +51,6 @@ GUARDED = {
     # the multi-step kernels (graph batches by default): the hot loop found is the step loop
     # around a tile, so no per-sample figure; max_block_valu is one tile's straight line
     "ms_pi4_series": ("riemann", MS + r"0ENS_3Pi4EE", 0),
-    "ms_pi4_ieee": ("riemann", MS + r"1ENS_3Pi4EE", 0),
     "ms_pi4f32_series": ("riemann", MS + r"0ENS0_6Pi4F32EE", 0),
     "ms_sin_series": ("riemann", MS + r"0ENS_3SinEE", 0),
     "ms_sin_ieee": ("riemann", MS + r"1ENS_3SinEE", 0),

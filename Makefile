@@ -62,8 +62,8 @@ $(OBJ)/cli_%.o: csrc/cli/%.cpp csrc/cli/cli_common.hpp $(HDRS) | $(OBJ)
 	$(HIPCC) -x c++ $(HOSTFLAGS) -c $< -o $@
 
 # the launcher links no HIP (it must never initialise a GPU: it forks and execs the ranks)
-$(BIN)/miintrun: csrc/cli/miintrun.cpp | $(BIN)
-	$(HOSTCXX) -std=c++17 -O2 -Wall -o $@ $<
+$(BIN)/miintrun: csrc/cli/miintrun.cpp csrc/include/miint/net.hpp | $(BIN)
+	$(HOSTCXX) -std=c++17 -O2 -Wall -Icsrc/include -o $@ $<
 
 $(BIN)/%: $(OBJ)/cli_%.o $(LIB) | $(BIN)
 	$(HIPCC) -o $@ $< $(LIB) $(LDLIBS)

@@ -127,7 +127,32 @@ def parse(argv=None) -> argparse.Namespace:
 
 
 # ------------------------------------------------------------------ launcher (no GPU here)
-def _free_port() -> int:
+def rendezvous_port(offsets=(0, 17, 19)) -> int:
+    """A MASTER_PORT P with P + o free for every offset o (the native CLIs add 17 and 19), below
+    the kernel's ephemeral range: a port from bind(0) lies inside it, where a rank retrying its
+    connect() can be handed it as a local port and self-connect (csrc/include/miint/net.hpp)."""
+    import random
+
+    try:
+        with open("/proc/sys/net/ipv4/ip_local_port_range") as f:
+            low = int(f.read().split()[0])
+    except (OSError, ValueError, IndexError):
+        low = 32768
+    hi = low - max(offsets)
+    lo = 20000 if hi > 21000 else 1024
+
+    def free(port: int) -> bool:
+        with socket.socket() as s:
+            try:
+                s.bind(("", port))
+                return True
+            except OSError:
+                return False
+
+    for _ in range(64):
+        p = random.randint(lo, hi - 1)
+        if all(free(p + o) for o in offsets):
+            return p
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
@@ -140,7 +165,7 @@ def spawn_ranks(n: int, argv: list[str]) -> int:
     initialises HIP (a GPU-initialised parent may not fork/exec on the pool). The first rank
     that fails ends the others; the exit status is the first non-zero one.
     """
-    port = _free_port()
+    port = rendezvous_port()
     base = dict(os.environ)
     base.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n),
                 LOCAL_WORLD_SIZE=str(n), MIINT_BENCH_LAUNCHER="spawn",

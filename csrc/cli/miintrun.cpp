@@ -27,26 +27,12 @@
 #include <thread>
 #include <vector>
 
+#include "miint/net.hpp"
+
 namespace {
 
 volatile sig_atomic_t g_signal = 0;
 void on_signal(int s) { g_signal = s; }
-
-int free_port() {
-  const int fd = ::socket(AF_INET, SOCK_STREAM, 0);
-  if (fd < 0) return 29500;
-  sockaddr_in sa{};
-  sa.sin_family = AF_INET;
-  sa.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
-  sa.sin_port = 0;
-  socklen_t len = sizeof(sa);
-  int port = 29500;
-  if (::bind(fd, reinterpret_cast<sockaddr*>(&sa), sizeof(sa)) == 0 &&
-      ::getsockname(fd, reinterpret_cast<sockaddr*>(&sa), &len) == 0)
-    port = ntohs(sa.sin_port);
-  ::close(fd);
-  return port;
-}
 
 int usage(FILE* out = stderr) {
   std::fprintf(out,
@@ -84,7 +70,7 @@ int main(int argc, char** argv) {
     } else break;
   }
   if (np < 1 || i >= argc) return usage();
-  if (port == 0) port = free_port();
+  if (port == 0) port = miint::pick_rendezvous_port({0, 17, 19});  // + the CLIs' offsets (net.hpp)
 
   struct sigaction sa{};
   sa.sa_handler = on_signal;

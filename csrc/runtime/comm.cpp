@@ -15,6 +15,7 @@
 #include <cstring>
 #include <thread>
 
+#include "miint/net.hpp"
 #include "miint/runtime.hpp"
 
 namespace miint {
@@ -189,7 +190,8 @@ std::string rendezvous_share(const std::string& addr, int port, int rank, int wo
   std::string id(kLen, '\0');
   for (;;) {
     int fd = ::socket(AF_INET, SOCK_STREAM, 0);
-    if (fd >= 0 && ::connect(fd, res->ai_addr, res->ai_addrlen) == 0 &&
+    // (a self-connected socket is not rank 0: drop it and retry, net.hpp)
+    if (fd >= 0 && ::connect(fd, res->ai_addr, res->ai_addrlen) == 0 && !self_connected(fd) &&
         recv_all(fd, &id[0], kLen)) {
       ::close(fd);
       break;

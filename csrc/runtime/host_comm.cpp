@@ -20,6 +20,7 @@
 
 #include "miint/common.hpp"
 #include "miint/host.hpp"
+#include "miint/net.hpp"
 #include "miint/runtime.hpp"
 
 namespace miint {
@@ -99,7 +100,7 @@ HostComm::HostComm(const std::string& addr, int port, int rank, int world, doubl
               "host comm: getaddrinfo(" + addr + ")");
   for (;;) {
     const int fd = ::socket(AF_INET, SOCK_STREAM, 0);
-    if (fd >= 0 && ::connect(fd, res->ai_addr, res->ai_addrlen) == 0) {
+    if (fd >= 0 && ::connect(fd, res->ai_addr, res->ai_addrlen) == 0 && !self_connected(fd)) {
       no_delay(fd);
       peers_.assign(1, fd);
       break;

@@ -162,11 +162,9 @@ def test_bench_driver_launch_form_json_contract():
     """The driver's exact launch form (torch.distributed.run, 127.0.0.1, a chosen port) on the
     CPU (gloo ranks): rank 0 prints ONE line carrying every field of the bench contract, with
     the whole-job value and the MAX over ranks as the step time."""
-    import socket
+    from bench import rendezvous_port
 
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
+    port = rendezvous_port()
     p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                         "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
                         "--master-port", str(port), os.path.join(REPO, "bench.py"),

@@ -8,7 +8,6 @@ from __future__ import annotations
 
 import math
 import os
-import socket
 
 import pytest
 import torch.multiprocessing as mp
@@ -17,9 +16,9 @@ from cuda_v_mpi_amd.parallel import decomposition
 
 
 def _free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    from bench import rendezvous_port  # below the ephemeral range (no self-connect)
+
+    return rendezvous_port()
 
 
 def _worker(rank: int, world: int, port: int, name: str, n: int, rule: str, q) -> None:

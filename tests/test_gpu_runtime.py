@@ -330,12 +330,11 @@ def test_bench_two_ranks_share_one_gpu_over_gloo():
     GPU: torch.distributed over gloo, kernels on each rank's torch stream and one
     all_reduce per step (TorchStepper). Checks rank slicing, MAX-over-ranks timing and the
     rank-0-only JSON line; not speed (two processes time-share the card)."""
-    import socket
     import sys
 
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
+    from bench import rendezvous_port
+
+    port = rendezvous_port()
     p = _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
               "--master-addr", "127.0.0.1", f"--master-port={port}",
               os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo", "--comm",
@@ -368,10 +367,9 @@ def test_cli_selfcheck(cli_built):
 
 
 def _torchrun(nproc, args, timeout=300):
-    import socket
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
+    from bench import rendezvous_port
+
+    port = rendezvous_port()
     return _run(["python", "-m", "torch.distributed.run", "--nnodes=1",
                  f"--nproc-per-node={nproc}", "--master-addr", "127.0.0.1",
                  "--master-port", str(port)] + args, timeout=timeout)

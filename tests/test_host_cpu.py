@@ -11,7 +11,6 @@ from __future__ import annotations
 import json
 import math
 import os
-import socket
 import subprocess
 import sys
 
@@ -146,9 +145,9 @@ def test_host_trainscan_prefix_matches_fsum(native):
 
 
 def _free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    from bench import rendezvous_port  # below the ephemeral range (no self-connect)
+
+    return rendezvous_port()
 
 
 _COMM_RANK = r"""

@@ -9,7 +9,6 @@ from __future__ import annotations
 
 import json
 import os
-import socket
 import subprocess
 import sys
 
@@ -30,9 +29,9 @@ def _devices() -> int:
 
 
 def _port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    from bench import rendezvous_port  # below the ephemeral range (no self-connect)
+
+    return rendezvous_port()
 
 
 def _run(args, timeout=600):

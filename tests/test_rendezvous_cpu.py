@@ -4,16 +4,15 @@ reference's MPI_Init bootstrap (riemann.cpp:62-64, 4main.c:69-71). CPU only: the
 comes from RCCL's bootstrap, which needs no GPU."""
 from __future__ import annotations
 
-import socket
 import threading
 
 import pytest
 
 
 def _port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    from bench import rendezvous_port  # below the ephemeral range (no self-connect)
+
+    return rendezvous_port()
 
 
 def test_rendezvous_every_rank_gets_rank0_id(native):
@@ -50,3 +49,21 @@ def test_rendezvous_times_out_without_rank0(native):
 def test_rendezvous_rank0_times_out_without_peers(native):
     with pytest.raises(Exception, match="timed out"):
         native.rendezvous_unique_id("127.0.0.1", _port(), 0, 3, 0.3)
+
+
+def test_rendezvous_port_below_ephemeral_range():
+    """Launcher ports sit below the ephemeral range with the CLIs' +17 / +19 free too: a port
+    inside it can be handed to a rank's retrying connect() as its local port (self-connect;
+    csrc/include/miint/net.hpp)."""
+    import socket
+
+    from bench import rendezvous_port
+
+    with open("/proc/sys/net/ipv4/ip_local_port_range") as f:
+        low = int(f.read().split()[0])
+    for _ in range(8):
+        p = rendezvous_port()
+        assert p + 19 < low
+        for o in (0, 17, 19):
+            with socket.socket() as s:
+                s.bind(("", p + o))

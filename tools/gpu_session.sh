@@ -16,7 +16,7 @@ mkdir -p gpurun_out
 # in-tree extension and CLIs count as current when no source or build file is newer.)
 # Every shipped artifact is checked on its own against the sources it is built from: `make
 # ext` refreshes the .so but not the CLIs, so a source newer than ANY of them means a rebuild
-# (miintrun is built from its one file only).
+# (miintrun is built from its one file and net.hpp only).
 newer_src() {  # artifact, sources... -> true if a source is newer than the artifact
   local a="$1"; shift
   [ -n "$(find "$@" -newer "$a" -type f -print -quit)" ]
@@ -28,7 +28,7 @@ built_ok() {
     [ -e "$a" ] || return 1
     newer_src "$a" csrc/include csrc/kernels csrc/runtime csrc/python csrc/cli Makefile && return 1
   done
-  newer_src build/bin/miintrun csrc/cli/miintrun.cpp && return 1
+  newer_src build/bin/miintrun csrc/cli/miintrun.cpp csrc/include/miint/net.hpp && return 1
   return 0
 }
 if ! built_ok && ! make -q all >/dev/null 2>&1; then

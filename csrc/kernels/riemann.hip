@@ -56,32 +56,63 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
 // all-fp32 variant (Pi4F32Acc32: fp32 lanes, v_add_f32_dpp wave sums, fp32 LDS step).
 template <class F> struct AccOf { using type = double; };
 
+// The launch's tiles over its lanes: with ntile = q * lanes + rem every lane runs q rounds and
+// the first rem lanes one more. Wave-uniform, computed once per launch (one scalar 64-bit
+// division) — the per-lane form (ntile - 1 - gid) / lanes + 1 was a VALU 64-bit division
+// (~50 VALU + ~60 SALU) that the multi-step kernel paid again every step, together with a
+// reload of blockDim.x and its wait.
+// Lane indices and rem are below lanes < 2^32, so the per-wave compares are 32-bit (SALU has
+// no 64-bit less-than: a 64-bit one would put the round counts, and the tile loop's exit
+// test, on the VALU).
+struct TileSplit {
+  uint64_t lanes, q;
+  uint32_t bs, rem;
+};
+template <int T>
+__device__ __forceinline__ TileSplit tile_split(uint64_t n) {
+  const uint32_t bs = blockDim.x;
+  const uint64_t lanes = static_cast<uint64_t>(gridDim.x) * bs;
+  const uint64_t ntile = n / T;
+  const uint64_t q = ntile / lanes;
+  return {lanes, q, bs, static_cast<uint32_t>(ntile - q * lanes)};
+}
+
 // `block` is the workgroup's index in the sample decomposition: blockIdx.x, or the multi-step
 // kernel's per-step rotated (virtual) index.
 template <DivMode M, class F>
 __device__ __forceinline__ typename AccOf<F>::type lane_sum(const RiemannParams& p, const F& f,
-                                                            unsigned block) {
+                                                            unsigned block, const TileSplit& sp) {
   using Acc = typename AccOf<F>::type;
   constexpr int T = F::template tile_len<M>();
-  const uint64_t bs = blockDim.x;
-  const uint64_t lanes = static_cast<uint64_t>(gridDim.x) * bs;
-  const uint64_t gid = static_cast<uint64_t>(block) * bs + threadIdx.x;
-  const uint64_t ntile = p.n / T;
-  const uint64_t rounds = gid < ntile ? (ntile - 1 - gid) / lanes + 1 : 0;
-  const uint64_t r_all = readlane_u64(rounds, kWave - 1);  // lane 63 has the fewest rounds
-  const uint64_t r_any = readlane_u64(rounds, 0);          // lane 0 the most (<= r_all + 1)
+  const uint64_t lanes = sp.lanes;
+  const uint32_t b0 = block * sp.bs;
+  const uint32_t g32 = b0 + threadIdx.x;
+  const uint64_t gid = g32;
+  const uint32_t w0 =  // the wave's first lane (SGPR)
+      b0 + static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(threadIdx.x / kWave)) * kWave;
+  // lane g runs q + (g < rem) rounds: every lane of the wave the first q + all_extra (a
+  // count-down with a 64-bit != test: SALU), the wave's lanes below rem one more, exec-masked
+  const bool all_extra = w0 + (kWave - 1) < sp.rem;  // lane 63, the wave's fewest
+  const bool extra = !all_extra && g32 < sp.rem;      // a lane mask (SGPRs)
   const double base = static_cast<double>(p.i_begin) + p.off;
   const double istep = static_cast<double>(lanes * T);
   double ib = base + static_cast<double>(gid * T) + F::template anchor<T, M>();
   Acc acc = 0;
-  uint64_t r = 0;
-  for (; r < r_all; ++r, ib += istep) acc = f.template tile_acc<T, M>(fma(ib, p.h, p.a), p.h, acc);
-  if (r < r_any && r < rounds) acc = f.template tile_acc<T, M>(fma(ib, p.h, p.a), p.h, acc);
+  // (readlane: left to itself, isel widens the uniform bool through a VGPR and runs the
+  // counter on the VALU)
+  for (uint64_t left = readlane_u64(sp.q + (all_extra ? 1 : 0), 0); left != 0; --left, ib += istep)
+    acc = f.template tile_acc<T, M>(fma(ib, p.h, p.a), p.h, acc);
+  if (extra) acc = f.template tile_acc<T, M>(fma(ib, p.h, p.a), p.h, acc);
   // remainder (< T samples): one per lane (a grid of fewer lanes than T loops)
-  const uint64_t done = ntile * T;
+  const uint64_t done = (sp.q * lanes + sp.rem) * T;
   for (uint64_t k = gid; k < p.n - done; k += lanes)
     acc += static_cast<Acc>(f.point(fma(base + static_cast<double>(done + k), p.h, p.a)));
   return acc;
+}
+template <DivMode M, class F>
+__device__ __forceinline__ typename AccOf<F>::type lane_sum(const RiemannParams& p, const F& f,
+                                                            unsigned block) {
+  return lane_sum<M>(p, f, block, tile_split<F::template tile_len<M>()>(p.n));
 }
 
 constexpr int kMaxTable = 2048;  // LDS budget for a 1-D table: 16 KB
@@ -645,13 +676,14 @@ __device__ __forceinline__ void multistep_body(const RiemannParams& p, const dou
   __shared__ double lds[lds_words<M, F>()];
   const F f = make_functor<M, F>(p, table, table_n, lds);
   const unsigned nb = gridDim.x;
+  const TileSplit sp = tile_split<F::template tile_len<M>()>(p.n);  // the same every step
   unsigned vb = blockIdx.x;
   for (int s = 0; s < steps; ++s) {
     RiemannParams q = p;
     asm volatile("" : "+s"(q.a));  // a fresh value every step (no instructions)
     double v;
-    if constexpr (__is_same(Acc, double)) v = block_sum_dyn(lane_sum<M>(q, f, vb), red);
-    else v = static_cast<double>(block_sum_dyn(lane_sum<M>(q, f, vb), red_acc));
+    if constexpr (__is_same(Acc, double)) v = block_sum_dyn(lane_sum<M>(q, f, vb, sp), red);
+    else v = static_cast<double>(block_sum_dyn(lane_sum<M>(q, f, vb, sp), red_acc));
     if (threadIdx.x == 0) partials[static_cast<size_t>(s) * nb + vb] = v;
     __syncthreads();  // wave 0 has read red before the next step writes it
     vb += rot;

@@ -57,3 +57,29 @@ def test_guard_flags_a_regression():
                 {"hot_loop_scratch_ops": 2}, {"max_block_valu": 52}):
         now = {"k": dict(ok["k"], **bad)}
         assert len(isa_guard.compare(base, now)) == 1, bad
+
+
+def test_loops_are_natural_loops():
+    """A loop closed by an unconditional latch counts; a backward jump of the block layout
+    that re-enters code before a loop (no dominating target) does not."""
+    body = "\n".join([
+        "  s_cmp_eq_u32 s0, 0",
+        "  s_cbranch_scc1 .LBB0_4",   # entry -> 4 (a block laid out after the loop)
+        ".LBB0_1:",
+        "  v_add_f64 v[0:1], v[0:1], v[2:3]",
+        ".LBB0_2:",                   # loop: 2 -> 3 -> 2 (unconditional latch)
+        "  v_fma_f64 v[0:1], v[0:1], v[2:3], v[4:5]",
+        "  v_fma_f64 v[0:1], v[0:1], v[2:3], v[4:5]",
+        "  s_add_u32 s1, s1, -1",
+        "  s_cbranch_scc0 .LBB0_5",
+        ".LBB0_3:",
+        "  v_mul_f64 v[0:1], v[0:1], v[2:3]",
+        "  s_branch .LBB0_2",
+        ".LBB0_4:",
+        "  v_mov_b32 v0, 0",
+        "  s_branch .LBB0_1",          # layout jump back: 1 does not dominate 4
+        ".LBB0_5:",
+        "  s_endpgm",
+    ])
+    found = [sum(1 for s in lp if s.startswith("v_")) for lp in isa_guard.loops(body)]
+    assert found == [3]

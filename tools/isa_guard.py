@@ -9,7 +9,8 @@ without any test failing. This tool compiles the kernel files device-only to gfx
 assembly (hipcc --cuda-device-only -S, no GPU needed), and for every guarded instantiation
 reads the compiler's kernel-info block (TotalNumSgprs, NumVgprs, NumAgprs, ScratchSize,
 Occupancy) and the VALU count of its hot loop (the loop body with the most VALU
-instructions = one tile of the lane loop for the series kernels).
+instructions = one tile of the lane loop for the series kernels; for the multi-step kernels
+the step loop around it, i.e. a tile plus the per-step overhead).
 
     python tools/isa_guard.py --write   # refresh tools/isa_baseline.json
     python tools/isa_guard.py           # compare; exit 1 on a regression
@@ -88,25 +89,82 @@ def functions(text: str):
         yield name, text[m.end():end], info
 
 
-def loops(body: str):
-    """Instruction lists of every loop: a block range closed by a branch back to a label."""
-    labels, ins = {}, []
+def cfg(body: str):
+    """Basic blocks of a function body: (instructions, successor indices) per block."""
+    blocks, labels, cur = [], {}, []
+
+    def close():
+        blocks.append(cur)
+
     for ln in body.splitlines():
         s = ln.split(";")[0].strip()
-        if not s or s.startswith("."):
-            if s.endswith(":"):
-                labels[s[:-1]] = len(ins)
+        if not s:
             continue
         if s.endswith(":"):
-            labels[s[:-1]] = len(ins)
+            if cur:
+                close()
+                cur = []
+            labels[s[:-1]] = len(blocks)
             continue
-        ins.append(s)
-    for i, s in enumerate(ins):
+        if s.startswith("."):
+            continue
+        cur.append(s)
         op = s.split()[0]
-        if op.startswith("s_cbranch") or op == "s_branch":
-            tgt = s.split()[-1]
-            if tgt in labels and labels[tgt] <= i:
-                yield ins[labels[tgt]:i + 1]
+        if op.startswith("s_cbranch") or op in ("s_branch", "s_endpgm", "s_setpc_b64"):
+            close()
+            cur = []
+    if cur:
+        close()
+    succ = []
+    for i, ins in enumerate(blocks):
+        last = ins[-1].split() if ins else [""]
+        out = []
+        if last[0].startswith("s_cbranch") or last[0] == "s_branch":
+            if last[-1] in labels:
+                out.append(labels[last[-1]])
+        if not (last[0] in ("s_branch", "s_endpgm", "s_setpc_b64")) and i + 1 < len(blocks):
+            out.append(i + 1)
+        succ.append(out)
+    return blocks, succ
+
+
+def loops(body: str):
+    """Instruction lists of every natural loop (a back edge to a block that dominates its
+    source, and every block that reaches the source without passing the header). A backward
+    jump of the block layout that is not a loop (a block placed after a loop that re-enters
+    the code before it) has no dominating target and is not counted."""
+    blocks, succ = cfg(body)
+    n = len(blocks)
+    if n == 0:
+        return
+    pred = [[] for _ in range(n)]
+    for i, ss in enumerate(succ):
+        for j in ss:
+            pred[j].append(i)
+    full = set(range(n))
+    dom = [full.copy() for _ in range(n)]
+    dom[0] = {0}
+    changed = True
+    while changed:
+        changed = False
+        for i in range(1, n):
+            new = set.intersection(*(dom[p] for p in pred[i])) if pred[i] else set()
+            new = new | {i}
+            if new != dom[i]:
+                dom[i], changed = new, True
+    heads: dict = {}
+    for i, ss in enumerate(succ):
+        for h in ss:
+            if h in dom[i]:  # back edge i -> h
+                body_set = heads.setdefault(h, {h})
+                stack = [i]
+                while stack:
+                    b = stack.pop()
+                    if b not in body_set:
+                        body_set.add(b)
+                        stack.extend(pred[b])
+    for h, members in heads.items():
+        yield [ins for b in sorted(members) for ins in blocks[b]]
 
 
 def field(info: str, key: str) -> int:

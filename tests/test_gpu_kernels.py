@@ -42,6 +42,19 @@ def test_riemann_vs_torch(cuda, spec, n):
     assert got == pytest.approx(want, rel=1e-12, abs=1e-12)
 
 
+@pytest.mark.parametrize("spec", [integrands.pi4(), integrands.sin()], ids=lambda s: s.name)
+@pytest.mark.parametrize("grid", [1, 3, 7, 130])
+@pytest.mark.parametrize("n", [192 * 64 * 3 + 191, 192 * 256 * 7 + 192 * 100 + 5, 10_000_019])
+def test_tile_split_covers_every_tile(cuda, spec, grid, n):
+    """Lane g of the launch runs q + (g < rem) tile rounds (riemann.hip tile_split): grids
+    where rem falls inside a wave, q = 0 (fewer tiles than lanes) and remainder samples
+    (pi4: 32-sample tiles at these N, sin: 192), against the fp64 torch sum. A tile dropped
+    or counted twice moves the sum by ~T / n."""
+    got = float(kernels.riemann(spec, n, rule="mid", grid=grid).item())
+    want = _ref_sum(spec, n, rule="mid")
+    assert got == pytest.approx(want, rel=1e-12)
+
+
 @pytest.mark.parametrize("dtype", ["fp32", "fp32acc"])
 @pytest.mark.parametrize("n", [1, 63, 4097, 1_000_003, 40_000_001, 50_000_017])
 def test_riemann_fp32_small_and_odd_n(cuda, n, dtype):

@@ -80,6 +80,26 @@ def test_multistep_batches_equal_chained_bitwise(cuda, name):
     assert one.plan.host_result(one.plan.host_index_of(2, True)) == want[0]
 
 
+@pytest.mark.parametrize("block", [64, 256, 1024])
+def test_multistep_tile_split_vs_torch(cuda, block):
+    """Multi-step batches (the tile split formed once per batch, every step rotating its
+    virtual blocks) at 64-, 256- and 1024-thread workgroups and a small grid: sin's
+    192-sample series tiles against the fp64 torch sum of the same samples."""
+    import math
+
+    import torch
+
+    n = 192 * 1000 + 77
+    it = Integrator("sin", n=n, rule="mid", block=block, grid=5, slots=8)
+    assert it.plan.multistep
+    it.run_steps(8, pipeline=True, graphs=True)
+    got = it.plan.host_result(it.plan.host_index_of(7, True))
+    h = math.pi / n
+    x = (torch.arange(n, dtype=torch.float64) + 0.5) * h
+    want = math.fsum(torch.sin(x).tolist()) * h
+    assert got == pytest.approx(want, rel=1e-12)
+
+
 @pytest.mark.parametrize("name,div", [("table", "series"), ("pi4", "ieee")])
 def test_multistep_not_where_it_does_not_pay(cuda, name, div):
     """The table's segment tiles and the fp64 per-sample IEEE division measured slower as

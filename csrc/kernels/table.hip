@@ -282,90 +282,111 @@ __device__ __forceinline__ double fma_sv(double a, double s, double c) {
   return r;
 }
 
-// One workgroup's share of a row-stream integration: column block bx, row block by (the
-// launch's blockIdx, or the multi-step kernel's). Returns the block's partial in thread 0.
-// `between` runs while the staging loads are in flight (the chained close).
-// POISON (validation instantiation, set_lds_poison): tile slots outside the computed footprint
-// hold NaN instead of the corner value, so a read outside the footprint shows.
-template <int SH, bool POISON, class Between>
-__device__ __forceinline__ double table2d_stream_block(const Table2DParams& p, int rows_per_wave,
-                                                       int bx, int by, double* tile, double* red,
-                                                       Between between) {
-  const double sx = p.X / p.gx, sy = p.Y / p.gy;
-  const double cx = (p.nx - 1) / p.X, cy = (p.ny - 1) / p.Y;
-  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) / kWave);
-  const int lane = static_cast<int>(threadIdx.x) % kWave;
-  const int c0 = bx * (kWave * kSCols);
-  const int r0 = p.row0 + by * (4 * rows_per_wave);
-  const int r1 = min(r0 + 4 * rows_per_wave, p.row1);
+// One workgroup's share of a row-stream integration, in three parts: its table footprint
+// (t2d_footprint), the staging loads of that footprint (t2d_stage_load: SH / kStageRows doubles per
+// thread, in registers) and their LDS writes (t2d_stage_store), then the rows
+// (t2d_stream_rows). table2d_stream_block runs them in that order for one integration; the
+// multi-step kernel issues the NEXT step's staging loads before this step's rows, so their
+// latency hides behind the row loop.
+struct T2DFoot {
+  double sx, sy, cx, cy;
+  int c0, r0, r1, tx0, ty0, tx1, ty1;
+};
+
+__device__ __forceinline__ T2DFoot t2d_footprint(const Table2DParams& p, int rows_per_wave,
+                                                 int bx, int by) {
+  T2DFoot f;
+  f.sx = p.X / p.gx;
+  f.sy = p.Y / p.gy;
+  f.cx = (p.nx - 1) / p.X;
+  f.cy = (p.ny - 1) / p.Y;
+  f.c0 = bx * (kWave * kSCols);
+  f.r0 = p.row0 + by * (4 * rows_per_wave);
+  f.r1 = min(f.r0 + 4 * rows_per_wave, p.row1);
   // table footprint of the workgroup's samples (first / last column and row)
   // (computed on the VALU: readfirstlane moves the uniform results to SGPRs, so the staging
   // addresses below are an SGPR base plus 32-bit lane offsets)
-  const int clast = min(c0 + kWave * kSCols, p.gx) - 1;
-  const int tx0 = __builtin_amdgcn_readfirstlane(
-      clampi(static_cast<int>(((c0 + 0.5) * sx) * cx), 0, p.nx - 2));
-  const int ty0 = __builtin_amdgcn_readfirstlane(
-      clampi(static_cast<int>(((r0 + 0.5) * sy) * cy), 0, p.ny - 2));
-  const int tx1 = __builtin_amdgcn_readfirstlane(
-      clampi(static_cast<int>(((clast + 0.5) * sx) * cx), 0, p.nx - 2) + 1);
-  const int ty1 = __builtin_amdgcn_readfirstlane(
-      clampi(static_cast<int>(((r1 - 1 + 0.5) * sy) * cy), 0, p.ny - 2) + 1);
-  {
-    // kSW consecutive lanes per table row, 2 rows per pass; every pass's load in flight
-    // before the LDS writes. Branch-free: a lane outside the footprint loads the corner
-    // (its LDS slot is never read), and addresses are a uniform base plus 32-bit offsets.
-    constexpr int kRowsPer = kB / kSW, kPasses = SH / kRowsPer;
-    const int w = tx1 - tx0 + 1, hgt = ty1 - ty0 + 1;
-    const int lx = threadIdx.x % kSW, ly = threadIdx.x / kSW;
-    const double* tb = p.table + static_cast<size_t>(ty0) * p.nx + tx0;
-    double v[kPasses];
-#pragma unroll
-    for (int j = 0; j < kPasses; ++j) {
-      const int rr = ly + kRowsPer * j;
-      const unsigned off = (lx < w && rr < hgt) ? static_cast<unsigned>(rr * p.nx + lx) * 8u : 0u;
-      v[j] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(tb) + off);
-    }
+  const int clast = min(f.c0 + kWave * kSCols, p.gx) - 1;
+  f.tx0 = __builtin_amdgcn_readfirstlane(
+      clampi(static_cast<int>(((f.c0 + 0.5) * f.sx) * f.cx), 0, p.nx - 2));
+  f.ty0 = __builtin_amdgcn_readfirstlane(
+      clampi(static_cast<int>(((f.r0 + 0.5) * f.sy) * f.cy), 0, p.ny - 2));
+  f.tx1 = __builtin_amdgcn_readfirstlane(
+      clampi(static_cast<int>(((clast + 0.5) * f.sx) * f.cx), 0, p.nx - 2) + 1);
+  f.ty1 = __builtin_amdgcn_readfirstlane(
+      clampi(static_cast<int>(((f.r1 - 1 + 0.5) * f.sy) * f.cy), 0, p.ny - 2) + 1);
+  return f;
+}
 
-    // chained: workgroup 0 closes the previous integration while its staging loads fly
-    // (the loads above hold 32 VGPRs; the kernel is LDS-limited to 4 waves per SIMD, whose
-    // 128-VGPR budget the close's 16 loads in flight fit beside them)
-    between();
+// kSW consecutive lanes per table row, 2 rows per pass; every pass's load in flight before
+// the LDS writes. Branch-free: a lane outside the footprint loads the corner (its LDS slot is
+// never read), and addresses are a uniform base plus 32-bit offsets.
+constexpr int kStageRows = kB / kSW;
+template <int SH>
+__device__ __forceinline__ void t2d_stage_load(const double* table, int nx, const T2DFoot& f,
+                                               double (&v)[SH / kStageRows]) {
+  const int w = f.tx1 - f.tx0 + 1, hgt = f.ty1 - f.ty0 + 1;
+  const int lx = threadIdx.x % kSW, ly = threadIdx.x / kSW;
+  const double* tb = table + static_cast<size_t>(f.ty0) * nx + f.tx0;
 #pragma unroll
-    for (int j = 0; j < kPasses; ++j) tile[(ly + kRowsPer * j) * kSW + lx] = v[j];
-    if constexpr (POISON) {  // validation: NaN in the tile slots outside the footprint
-#pragma unroll
-      for (int j = 0; j < kPasses; ++j)
-        if (!(lx < w && ly + kRowsPer * j < hgt))
-          tile[(ly + kRowsPer * j) * kSW + lx] = __builtin_nan("");
-    }
+  for (int j = 0; j < SH / kStageRows; ++j) {
+    const int rr = ly + kStageRows * j;
+    const unsigned off = (lx < w && rr < hgt) ? static_cast<unsigned>(rr * nx + lx) * 8u : 0u;
+    v[j] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(tb) + off);
   }
+}
+
+// POISON (validation instantiation, set_lds_poison): tile slots outside the computed
+// footprint hold NaN instead of the corner value, so a read outside the footprint shows.
+template <int SH, bool POISON>
+__device__ __forceinline__ void t2d_stage_store(const T2DFoot& f, const double (&v)[SH / kStageRows],
+                                                double* tile) {
+  const int lx = threadIdx.x % kSW, ly = threadIdx.x / kSW;
+#pragma unroll
+  for (int j = 0; j < SH / kStageRows; ++j) tile[(ly + kStageRows * j) * kSW + lx] = v[j];
+  if constexpr (POISON) {
+    const int w = f.tx1 - f.tx0 + 1, hgt = f.ty1 - f.ty0 + 1;
+#pragma unroll
+    for (int j = 0; j < SH / kStageRows; ++j)
+      if (!(lx < w && ly + kStageRows * j < hgt))
+        tile[(ly + kStageRows * j) * kSW + lx] = __builtin_nan("");
+  }
+}
+
+// The rows of the workgroup's block from the staged tile (the barrier before them makes every
+// thread's tile writes visible). Returns the block's partial in thread 0.
+__device__ __forceinline__ double t2d_stream_rows(const Table2DParams& p, int rows_per_wave,
+                                                  const T2DFoot& f, const double* tile,
+                                                  double* red) {
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) / kWave);
+  const int lane = static_cast<int>(threadIdx.x) % kWave;
   // per-lane columns: LDS column and x fraction, computed once
   int col[kSCols];
   double fx[kSCols];
   bool ok[kSCols];
 #pragma unroll
   for (int b = 0; b < kSCols; ++b) {
-    const int c = c0 + lane + kWave * b;
+    const int c = f.c0 + lane + kWave * b;
     ok[b] = c < p.gx;
-    const double xx = ((min(c, p.gx - 1) + 0.5) * sx) * cx;
+    const double xx = ((min(c, p.gx - 1) + 0.5) * f.sx) * f.cx;
     const int ix = clampi(static_cast<int>(xx), 0, p.nx - 2);
     fx[b] = xx - ix;
-    col[b] = ix - tx0;
+    col[b] = ix - f.tx0;
   }
   // this wave's rows; lane k holds row k's table row and fraction
-  const int rbase = r0 + wave * rows_per_wave;
-  const int nrows = max(0, min(rows_per_wave, r1 - rbase));
+  const int rbase = f.r0 + wave * rows_per_wave;
+  const int nrows = max(0, min(rows_per_wave, f.r1 - rbase));
   int iyl;
   double fyl;
   {
     const int r = rbase + min(lane, max(nrows - 1, 0));
-    const double yy = ((r + 0.5) * sy) * cy;
+    const double yy = ((r + 0.5) * f.sy) * f.cy;
     iyl = clampi(static_cast<int>(yy), 0, p.ny - 2);
     fyl = yy - iyl;
   }
   __syncthreads();
   auto line = [&](int j, int b) {  // table row j interpolated at column b's x
-    const double* t = tile + (j - ty0) * kSW + col[b];
+    const double* t = tile + (j - f.ty0) * kSW + col[b];
     return fma(t[1] - t[0], fx[b], t[0]);
   };
   double acc[kSCols], lc[kSCols], ln[kSCols], d[kSCols];
@@ -399,7 +420,24 @@ __device__ __forceinline__ double table2d_stream_block(const Table2DParams& p, i
   double a = 0.0;
 #pragma unroll
   for (int b = 0; b < kSCols; ++b) a += ok[b] ? acc[b] : 0.0;
-  return block_sum<kB>(a, red) * (sx * sy);
+  return block_sum<kB>(a, red) * (f.sx * f.sy);
+}
+
+// One workgroup's share of a row-stream integration: column block bx, row block by (the
+// launch's blockIdx, or the multi-step kernel's). Returns the block's partial in thread 0.
+// `between` runs while the staging loads are in flight (the chained close: the loads hold 32
+// VGPRs; the kernel is LDS-limited to 4 waves per SIMD, whose 128-VGPR budget the close's 16
+// loads in flight fit beside them).
+template <int SH, bool POISON, class Between>
+__device__ __forceinline__ double table2d_stream_block(const Table2DParams& p, int rows_per_wave,
+                                                       int bx, int by, double* tile, double* red,
+                                                       Between between) {
+  const T2DFoot f = t2d_footprint(p, rows_per_wave, bx, by);
+  double v[SH / kStageRows];
+  t2d_stage_load<SH>(p.table, p.nx, f, v);
+  between();
+  t2d_stage_store<SH, POISON>(f, v, tile);
+  return t2d_stream_rows(p, rows_per_wave, f, tile, red);
 }
 
 template <int MODE, int SH, bool POISON>
@@ -445,11 +483,29 @@ __global__ __launch_bounds__(kB) void table2d_multistep_kernel(Table2DParams p, 
   __shared__ double red[kB / kWave];
   const unsigned nb = gridDim.x;
   const int bx = static_cast<int>(blockIdx.x) % gx, by = static_cast<int>(blockIdx.x) / gx;
+  const T2DFoot f = t2d_footprint(p, rows_per_wave, bx, by);
+  // Each step loads its own footprint from a table pointer laundered per step (no step's
+  // loads are shared or hoisted). Short tiles (the multi-GPU row slices): step st's loads are
+  // issued during step st - 1, before its rows, so their latency hides behind the row loop
+  // (1/8 slice 2.20 -> 2.04 us, profiles/r3/t2d_prefetch_ab.jsonl). The full tile keeps
+  // loading at the top of its step: holding its 16 loads across the rows takes 139 VGPRs, 3
+  // waves per SIMD, and the 4096^2 grid would no longer be resident.
+  constexpr bool kPrefetch = SH <= kSHShort;
+  double v[SH / kStageRows];
+  auto load = [&] {
+    const double* t = p.table;
+    asm volatile("" : "+s"(t));  // a fresh pointer every step (no instructions)
+    t2d_stage_load<SH>(t, p.nx, f, v);
+  };
+  if constexpr (kPrefetch) load();
   for (int st = 0; st < steps; ++st) {
-    Table2DParams q = p;
-    asm volatile("" : "+s"(q.table));  // a fresh pointer every step (no instructions)
-    const double v = table2d_stream_block<SH, false>(q, rows_per_wave, bx, by, tile, red, [] {});
-    if (threadIdx.x == 0) partials[static_cast<size_t>(st) * nb + blockIdx.x] = v;
+    if constexpr (!kPrefetch) load();
+    t2d_stage_store<SH, false>(f, v, tile);
+    if constexpr (kPrefetch) {
+      if (st + 1 < steps) load();
+    }
+    const double val = t2d_stream_rows(p, rows_per_wave, f, tile, red);
+    if (threadIdx.x == 0) partials[static_cast<size_t>(st) * nb + blockIdx.x] = val;
     __syncthreads();  // the next step rewrites tile and red
   }
 }

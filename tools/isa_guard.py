@@ -63,6 +63,10 @@ GUARDED = {
     "table2d_stream_1_32": ("table", r"table2d_stream_kernelILi1ELi32ELb0EE", 0),
     "table2d_stream_2_16": ("table", r"table2d_stream_kernelILi2ELi16ELb0EE", 0),
     "table2d_stream_2_32": ("table", r"table2d_stream_kernelILi2ELi32ELb0EE", 0),
+    # the 2-D multi-step kernels: the full tile must keep 4 waves per SIMD (at 3 the 4096^2
+    # grid is no longer resident and the plan falls back to chained replays)
+    "table2d_ms_16": ("table", r"table2d_multistep_kernelILi16EE", 0),
+    "table2d_ms_32": ("table", r"table2d_multistep_kernelILi32EE", 0),
 }
 
 

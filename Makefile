@@ -84,8 +84,9 @@ SAN := -fsanitize=address,undefined -fno-sanitize-recover=undefined -fno-omit-fr
 .PHONY: sanitize
 sanitize: $(BIN)/host_selftest_asan
 SAN_SRC := csrc/cli/host_selftest.cpp csrc/runtime/oracle.cpp csrc/runtime/profile_data.cpp \
-           csrc/runtime/comm.cpp csrc/runtime/runtime.cpp csrc/runtime/host.cpp csrc/runtime/host_comm.cpp
+           csrc/runtime/comm.cpp csrc/runtime/agree.cpp csrc/runtime/trace.cpp csrc/runtime/runtime.cpp \
+           csrc/runtime/host.cpp csrc/runtime/host_comm.cpp
 $(BIN)/host_selftest_asan: $(SAN_SRC) csrc/cli/cli_common.hpp $(HDRS) | $(BIN)
 	$(HIPCC) -x c++ -std=c++17 -Icsrc/include -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ $(SAN) \
 	  -o $@ $(SAN_SRC) \
-	  -L/opt/rocm/lib -lamdhip64 -lrccl -lpthread
+	  -L/opt/rocm/lib -lamdhip64 -lrccl -lpthread -ldl

@@ -187,11 +187,18 @@ def spawn_ranks(n: int, argv: list[str]) -> int:
 
     old = {s: signal.signal(s, on_signal) for s in (signal.SIGTERM, signal.SIGINT)}
     rc = 0
+    linger_until = None
     try:
         while True:
             codes = [p.poll() for p in procs]
             bad = [c for c in codes if c not in (None, 0)]
-            if bad and rc == 0:
+            # a rank that exited with a status (not a signal) may be one of several ending the
+            # same agreed failure (a verification every rank computes alike): give the others
+            # 2 s to finish, so rank 0's record is printed rather than cut off
+            if bad and rc == 0 and linger_until is None and bad[0] > 0:
+                linger_until = time.time() + 2.0
+            if bad and rc == 0 and (bad[0] < 0 or time.time() >= linger_until
+                                    or all(c is not None for c in codes)):
                 rc = bad[0]
                 print(f"bench.py: a rank exited with {rc}; stopping the others", file=sys.stderr)
                 stop_all()
@@ -234,6 +241,12 @@ def main(argv=None) -> int:
     from cuda_v_mpi_amd.parallel import dist as mdist
 
     cpu = args.device == "cpu"
+    if not cpu:
+        # RCCL's INIT log into a per-process file before anything initialises RCCL (the
+        # native communicator, or torch's with --comm torch): the record names the transport
+        from cuda_v_mpi_amd import native as _native_mod
+
+        _native_mod().capture_rccl_log()
     backend_auto = args.backend is None
     if backend_auto:
         args.backend = mdist.control_backend(args.comm, args.device)
@@ -371,10 +384,17 @@ def main(argv=None) -> int:
     comm = getattr(integ, "_comm", None)
     rccl_world = comm.transport_world if comm is not None else None
     rccl_version = None
+    transport = {}
     if not cpu:
         from cuda_v_mpi_amd import native
 
         rccl_version = native().Comm.version()
+        if world > 1:
+            transport = native().rccl_transport()
+    share = mdist.ranks_share_devices() and world > 1
+    transport_error = transport_check(world, share, transport)
+    if transport_error:
+        print(f"bench.py: {transport_error}", file=sys.stderr)
     extras = {}
     extras_ok = True
     if not cpu and not use_torch and not args.no_extras:
@@ -409,14 +429,21 @@ def main(argv=None) -> int:
             "data": "synthetic (analytic integrand 4/(1+x^2); no dataset)",
             "abs_err": abs_err,
             "result": vals[-1],
-            "verified": bool(ok and extras_ok),
+            "verified": bool(ok and extras_ok and not transport_error),
             "headline_verified": ok,
             "extras_verified": extras_ok,
+            "transport_verified": not transport_error,
+            "transport_error": transport_error,
             "verify_rule": verify_rule(args.integrand, args.rule, args.dtype),
             "launcher": launcher,
             "parent_imported_torch": os.environ.get("MIINT_BENCH_PARENT_TORCH") == "1",
             "rccl_world": rccl_world,
             "rccl_version": rccl_version,
+            # what RCCL's INIT log says rank 0's connections use (P2P/IPC over xGMI on one
+            # node; NET/Socket when ranks share a GPU) and how many nodes it counted
+            "rccl_transport": transport.get("transport") if transport else None,
+            "rccl_nnodes": transport.get("nnodes") if transport else None,
+            "rccl_connections": transport.get("connections") if transport else None,
             # one RCCL communicator per rank: the native one (data plane); the torch group is
             # the control plane (gloo unless --comm torch), torch RCCL groups counted here
             "control_plane": ctx.backend,
@@ -424,7 +451,7 @@ def main(argv=None) -> int:
             "native_rccl_comms": int(comm is not None and getattr(comm, "kind", "") == "rccl"),
             # MIINT_OVERSUBSCRIBE: ranks share GPUs and RCCL runs over loopback sockets — a
             # correctness run of the multi-rank path, not a scaling number
-            "ranks_share_gpus": mdist.ranks_share_devices() and world > 1,
+            "ranks_share_gpus": share,
             "per_rank_ms": per_rank_ms,
             "per_rank_spread_ms": max(per_rank_ms) - min(per_rank_ms),
             "graph_replays_timed": graph_replays,
@@ -464,6 +491,25 @@ def main(argv=None) -> int:
                 f.write(json.dumps(out) + "\n")
     ctx.destroy()
     return 0 if ok else 1
+
+
+def transport_check(world: int, share: bool, transport: dict) -> str | None:
+    """None, or why the multi-GPU record cannot stand: ranks of ONE node on distinct GPUs must
+    meet over xGMI peer-to-peer, not a network transport (a silent fallback — P2P disabled, a
+    leaked NCCL_HOSTID splitting the node into W "hosts" — would corrupt the scaling curve).
+    Ranks sharing a GPU (MIINT_OVERSUBSCRIBE) legitimately use sockets; an unknown transport
+    (no RCCL log) is recorded as null, not failed."""
+    if world <= 1 or share or not transport or not transport.get("transport"):
+        return None
+    local = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if local != world:  # a multi-node job: NET between nodes is expected
+        return None
+    if transport.get("uses_net"):
+        return (f"RCCL transport is {transport['transport']} (nNodes {transport.get('nnodes')}) "
+                f"between {world} ranks on distinct local GPUs: expected P2P over xGMI")
+    if transport.get("nnodes", 1) not in (0, 1):
+        return f"RCCL counted {transport['nnodes']} nodes for {world} ranks of one node"
+    return None
 
 
 # ------------------------------------------------------------------ verification
@@ -532,6 +578,65 @@ def _timed_steps(ctx, plan, steps, pipeline, dev) -> float:
     t = torch.tensor([(time.perf_counter() - t0) / steps * 1e3], dtype=torch.float64, device=dev)
     ctx.all_reduce_max(t)
     return float(t.item())
+
+
+def single_shot(ctx, kw, args, pipeline, dev, reps: int = 50) -> dict:
+    """One pi4 N = 1e9 integration per call, launch to pinned result (median of `reps`).
+
+    One GPU: the plan is built for single integrations (multistep off: the full grid, one
+    fused launch whose last workgroup stores the value straight into pinned host memory), and
+    RiemannPlan.time_one_shot times four forms in C++: direct (fused launch + stream sync),
+    direct_poll (the same launch, the host spinning on the pinned result word), graph /
+    graph_poll (a captured 1-step batch replayed). Several GPUs: one step per call through
+    the rank's collective plan (barrier, launch, all-reduce, copy, sync), slowest rank."""
+    import torch
+
+    from cuda_v_mpi_amd import Integrator
+
+    n1 = 10**9
+    want = pi4_expected_abs_err(args.rule, n1)
+    rec: dict = {"N": n1, "reps": reps, "n_gpus": ctx.world, "forms": {}}
+    if ctx.world == 1:
+        one = Integrator("pi4", n=n1, div=args.div, **dict(kw, dtype="fp64", multistep=False))
+        p = one.plan
+        rec["grid"] = p.grid
+        ok = True
+        for mode in ("direct_poll", "direct", "graph_poll", "graph"):
+            r = p.time_one_shot(reps, mode, 20)
+            e = abs(r["value"] - math.pi)
+            ok = ok and abs(e - want) <= PI4_TOL
+            rec["forms"][mode] = {"median_us": r["median_us"], "min_us": r["min_us"],
+                                  "max_us": r["max_us"],
+                                  "device_median_us": r["device_median_us"],
+                                  "result": r["value"]}
+        best = min(rec["forms"], key=lambda k: rec["forms"][k]["median_us"])
+        rec.update(best_form=best, ms_one_shot=rec["forms"][best]["median_us"] * 1e-3,
+                   device_ms_one_shot=rec["forms"][best]["device_median_us"] * 1e-3,
+                   verified=bool(ok))
+        del one
+        return rec
+    st = Integrator("pi4", n=n1, div=args.div, **dict(kw, dtype="fp64"))
+    p = st.plan
+    for _ in range(20):  # warm: code objects, RCCL connections, clocks
+        p.run_steps(1, pipeline, False)
+    walls, devs = [], []
+    for _ in range(reps):
+        t = p.run_steps(1, pipeline, False)  # barrier inside: every rank starts together
+        walls.append(t["wall_s"] * 1e6)
+        devs.append(t["device_ms"] * 1e3)
+    walls.sort()
+    devs.sort()
+    m = torch.tensor([walls[reps // 2], devs[reps // 2]], dtype=torch.float64, device=dev)
+    ctx.all_reduce_max(m)
+    v = p.host_result(p.host_index_of(0, False))
+    e = abs(v - math.pi)
+    rec["forms"]["collective_step"] = {"median_us": float(m[0]), "device_median_us": float(m[1]),
+                                       "result": v}
+    rec.update(best_form="collective_step", ms_one_shot=float(m[0]) * 1e-3,
+               device_ms_one_shot=float(m[1]) * 1e-3, grid=p.grid,
+               verified=bool(abs(e - want) <= PI4_TOL))
+    del st
+    return rec
 
 
 def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
@@ -669,6 +774,28 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
                                          "rel_diff_vs_fp64": rd, "dtype": "fp32",
                                          "accum": "fp32", "verified": bool(rd <= 1e-6)}
         del fa
+    # (6b) one integration per call — the reference's own timing unit (cintegrate.cu:102-104,
+    #      127-141 and riemann.cpp:49-51,90-93 clock exactly one run): pi4 N = 1e9 IN TOTAL,
+    #      from the launch call to the result in pinned host memory, median of 50 calls
+    if pi4 and args.dtype == "fp64":
+        out["single_shot_1e9"] = single_shot(ctx, kw, args, pipeline, dev)
+    # (6c) the reference's own integrands (sin: riemann.cpp:37, cintegrate.cu:68; the table
+    #      interpolant: cintegrate.cu:36-44; the analytic train model: riemann.cpp:103-116) and
+    #      the random-coefficient polynomial, each one timed 48-step graph batch of the same
+    #      shape as the headline (N per GPU, weak), checked against its analytic value
+    if pi4:
+        for name in ("sin", "train", "table", "poly"):
+            it = Integrator(name, n=n_total, **dict(kw, dtype="fp64"))
+            steps = 48
+            ms = _timed_steps(ctx, it.plan, steps, pipeline, dev)
+            v = it.plan.host_result(it.plan.host_index_of(steps - 1, True))
+            e = abs(v - it.spec.analytic())
+            out[f"integrand_{name}"] = {
+                "N": n_total, "value": n_total / (ms * 1e-3), "ms_per_step": ms, "steps": steps,
+                "result": v, "abs_err": e, "domain": [it.spec.a, it.spec.b],
+                "multistep": bool(it.plan.multistep), "grid": it.plan.grid,
+                "verified": result_ok(name, args.rule, "fp64", n_total, e, it.spec)}
+            del it
     # (7) BASELINE config #1: the serial CPU sum at N = 1e6 (the reference's plumbing case),
     #     on one host thread of the native host engine
     if pi4:

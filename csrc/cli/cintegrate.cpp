@@ -25,6 +25,7 @@
 #include <cstdio>
 
 #include "cli_common.hpp"
+#include "miint/fault.hpp"
 #include "miint/host.hpp"
 #include "miint/integrator.hpp"
 #include "miint/kernels.hpp"
@@ -57,6 +58,7 @@ int main(int argc, char** argv) {
     }
     const bool sin_kernel = a.str("kernel", "table") == "sin";
     double result = 0.0, dev_ms = 0.0;
+    cli::RankFacts facts;
     std::mutex mu;
 
     if (cpu) {  // the host engine; rank 0 prints
@@ -73,6 +75,7 @@ int main(int argc, char** argv) {
         cfg.b = seconds;
         cfg.n = static_cast<uint64_t>(seconds) * static_cast<uint64_t>(sps);
       }
+      if (hr.comm) hr.comm->barrier();  // every rank's clock starts after every rank is here
       const double t0 = wall_seconds();
       if (a.flag("parity") && !sin_kernel) {
         MIINT_CHECK(sps == oracle::kStepsPerSec, "--parity uses the reference's 1e4 samples/s");
@@ -84,7 +87,13 @@ int main(int argc, char** argv) {
         result = c ? host_riemann(cfg, b, c, pool) : 0.0;
         if (hr.comm) hr.comm->allreduce_sum(&result, 1);
       }
-      const double host_ms = (wall_seconds() - t0) * 1e3;
+      fault::delay(hr.rank);
+      double host_ms = (wall_seconds() - t0) * 1e3;
+      if (hr.comm) {  // the slowest rank's time
+        std::vector<double> all(static_cast<size_t>(hr.world));
+        hr.comm->allgather(&host_ms, all.data(), 1);
+        for (double x : all) host_ms = std::max(host_ms, x);
+      }
       if (hr.rank != 0) return 0;
       const double secs = wall_seconds() - process_start_seconds();
       std::printf("%lf seconds\n", secs);
@@ -104,6 +113,7 @@ int main(int argc, char** argv) {
     if (a.flag("materialize") && !sin_kernel) {
       cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
         DeviceGuard g(dev);
+        RankAgree agree(comm);
         const uint64_t total = static_cast<uint64_t>(seconds) * sps;
         uint64_t b, c;
         rank_slice(total, rank, topo.world, &b, &c);
@@ -116,6 +126,8 @@ int main(int argc, char** argv) {
         MIINT_HIP(hipMemcpyAsync(dtab.get(), tab.data(), dtab.bytes(), hipMemcpyHostToDevice, s.get()));
         Event e0, e1;
         for (int pass = 0; pass < 2; ++pass) {  // pass 0 cold (untimed), pass 1 timed
+          s.sync();
+          agree.barrier();  // every rank's clock starts after every rank is here
           e0.record(s.get());
           launch_interp_fill(dtab.get(), static_cast<int>(tab.size()), 1.0 / sps, b, c, prof.get(),
                              s.get());
@@ -123,11 +135,17 @@ int main(int argc, char** argv) {
           if (comm) comm->allreduce_sum(out.get(), out.get(), 1, s.get());
           MIINT_HIP(hipMemcpyAsync(host.get(), out.get(), sizeof(double), hipMemcpyDeviceToHost,
                                    s.get()));
+          fault::delay(rank);
           e1.record(s.get());
           s.sync();
         }
+        const double ms = agree.max(Event::elapsed_ms(e0, e1));  // the slowest rank's
         std::lock_guard<std::mutex> lk(mu);
-        if (rank == topo.rank0) { result = host[0]; dev_ms = Event::elapsed_ms(e0, e1); }
+        if (rank == topo.rank0) {
+          result = host[0];
+          dev_ms = ms;
+          facts.note(comm);
+        }
       });
     } else {
       RiemannConfig cfg;
@@ -145,20 +163,27 @@ int main(int argc, char** argv) {
       }
       cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
         RiemannPlan plan(cfg, dev, comm);
+        RankAgree agree(comm);
         plan.run_steps(1, false, false);  // cold: code-object load, first-launch set-up
+        // barrier before the clock (run_steps), the slowest rank's time
         StepTiming t = plan.run_steps(1, false, false);
+        const double ms = agree.max(t.device_ms);
         std::lock_guard<std::mutex> lk(mu);
-        if (rank == topo.rank0) { result = plan.host_result(0); dev_ms = t.device_ms; }
+        if (rank == topo.rank0) {
+          result = plan.host_result(plan.host_index_of(0, false));
+          dev_ms = ms;
+          facts.note(comm);
+        }
       });
     }
     if (topo.rank0 != 0) return 0;
     const double secs = wall_seconds() - process_start_seconds();
     std::printf("%lf seconds\n", secs);
     std::printf("final distance is:%lf\n", result);
-    cli::emit(a, cli::JsonRecord()
-                     .add("program", "cintegrate")
-                     .add("gpus", topo.world)
-                     .add("parity", a.flag("parity"))
+    cli::JsonRecord rec;
+    rec.add("program", "cintegrate").add("gpus", topo.world);
+    facts.add(rec, topo);
+    cli::emit(a, rec.add("parity", a.flag("parity"))
                      .add("result", result)
                      .add("device_ms", dev_ms)
                      .add("seconds_device", dev_ms * 1e-3)

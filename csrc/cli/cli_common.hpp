@@ -147,6 +147,7 @@ inline Topology topology(const Args& a) {
 inline void run_ranks(const Topology& t,
                       const std::function<void(int rank, int device, const Comm* comm)>& fn) {
   std::vector<std::unique_ptr<Comm>> comms;
+  if (!t.loopback && t.world > 1) capture_rccl_log();  // transport evidence for the record
   if (t.loopback) {
     run_loopback(t.world, 0, [&](int r, const Comm* c) { fn(r, 0, t.world > 1 ? c : nullptr); });
     return;
@@ -252,6 +253,8 @@ class JsonRecord {
     return raw(k, "\"" + json_escape(v) + "\"");
   }
   JsonRecord& add(const std::string& k, const char* v) { return add(k, std::string(v)); }
+  // a value that is already JSON (an array, a nested object)
+  JsonRecord& add_raw(const std::string& k, const std::string& json) { return raw(k, json); }
   std::string str() const { return "{" + body_ + "}"; }
 
  private:
@@ -281,6 +284,35 @@ inline void emit(const Args& a, JsonRecord r, bool print = false) {
     std::fprintf(f, "%s\n", line.c_str());
     std::fclose(f);
   }
+}
+
+// What a multi-rank record says about its ranks (the records must show how the
+// ranks met). Filled by the rank that prints (note()), added by add().
+struct RankFacts {
+  std::string comm = "none";  // communicator kind: rccl | loopback | none (one rank)
+  int rccl_world = 0;         // ranks the transport reports (ncclCommCount); 0 without RCCL
+  void note(const Comm* c) {
+    if (!c) return;
+    comm = c->kind();
+    if (comm == "rccl") rccl_world = c->transport_world();
+  }
+  // ranks_share_gpus: MIINT_OVERSUBSCRIBE (W ranks on fewer GPUs, RCCL over loopback
+  // sockets): a correctness run of the multi-rank path, never a performance number.
+  // rccl_transport / rccl_nnodes: what RCCL's INIT log says the connections use.
+  void add(JsonRecord& r, const Topology& t) const {
+    r.add("comm", comm).add("ranks_share_gpus", ranks_share_devices() && t.world > 1);
+    r.add("rccl_world", rccl_world);
+    const RcclTransport tr = rccl_world > 0 ? rccl_transport() : RcclTransport{};
+    r.add("rccl_transport", tr.transport).add("rccl_nnodes", tr.nnodes);
+  }
+};
+
+// Median of a sample (host timings).
+inline double median(std::vector<double> v) {
+  if (v.empty()) return 0.0;
+  std::sort(v.begin(), v.end());
+  const size_t n = v.size();
+  return n % 2 ? v[n / 2] : 0.5 * (v[n / 2 - 1] + v[n / 2]);
 }
 
 }  // namespace cli

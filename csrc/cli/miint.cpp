@@ -36,6 +36,8 @@ struct BenchRow {
   double n = 0, result = 0, exact = 0, ms = 0;
   int gpus = 1;
   int block = 0, grid = 0;  // launch shape of rank 0's plan
+  cli::RankFacts facts;
+  cli::Topology topo;
 };
 
 Integrand integrand_of(const std::string& s) { return cli::parse_integrand(s); }
@@ -63,9 +65,11 @@ BenchRow bench_one(const cli::Topology& topo, RiemannConfig cfg, int iters, bool
   row.n = static_cast<double>(cfg.n);
   row.gpus = topo.world;
   row.exact = oracle::analytic(cfg.integrand, cfg.a, cfg.b, cfg.coef, cfg.p0, cfg.p1);
+  row.topo = topo;
   std::mutex mu;
   cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
     RiemannPlan plan(cfg, dev, comm);
+    RankAgree agree(comm);
     plan.run_steps(3, comm != nullptr, graphs);  // warmup + capture
     // Clock settle (see bench.py): ~60 ms of back-to-back steps before timing. The count is
     // a function of the rank's sample count only, so every rank issues the same collectives.
@@ -73,11 +77,14 @@ BenchRow bench_one(const cli::Topology& topo, RiemannConfig cfg, int iters, bool
     const int settle = settle_steps >= 0 ? settle_steps
                        : static_cast<int>(std::min(20000.0, std::max(3.0, 0.06 / est_s)));
     plan.run_steps(settle, comm != nullptr, graphs);
+    // barrier before every rank's clock (run_steps), the slowest rank's time over all ranks
+    // of the communicator (not only this process's)
     StepTiming t = plan.run_steps(iters, comm != nullptr, graphs);
+    const double ms = agree.max(t.wall_s * 1e3 / iters);
     std::lock_guard<std::mutex> g(mu);
-    const double ms = t.wall_s * 1e3 / iters;
-    if (ms > row.ms) row.ms = ms;  // slowest rank
+    if (ms > row.ms) row.ms = ms;
     if (rank == topo.rank0) {
+      row.facts.note(comm);
       row.result = plan.host_result(plan.host_index_of(iters - 1, graphs));
       row.block = plan.shape().block;
       row.grid = plan.shape().grid;
@@ -88,13 +95,10 @@ BenchRow bench_one(const cli::Topology& topo, RiemannConfig cfg, int iters, bool
 
 void print_row(const cli::Args& a, const BenchRow& r, const char* integ, const char* dtype,
                const char* rule) {
-  cli::emit(a, cli::JsonRecord()
-                   .add("integrand", integ)
-                   .add("dtype", dtype)
-                   .add("rule", rule)
-                   .add("n", r.n)
-                   .add("gpus", r.gpus)
-                   .add("block", r.block)
+  cli::JsonRecord rec;
+  rec.add("integrand", integ).add("dtype", dtype).add("rule", rule).add("n", r.n).add("gpus", r.gpus);
+  r.facts.add(rec, r.topo);
+  cli::emit(a, rec.add("block", r.block)
                    .add("grid", r.grid)
                    .add("ms_per_integration", r.ms)
                    .add("subintervals_per_s", r.n / (r.ms * 1e-3))
@@ -159,6 +163,7 @@ int comm_sweep(const cli::Args& a, const cli::Topology& topo, double max_bytes, 
   auto body = [&](int /*rank*/, int dev, const Comm* comm) {
     DeviceGuard g(dev);
     Stream s;
+    RankAgree agree(comm);  // each op's time is the slowest rank's, over every process
     const size_t cmax = counts.back();
     DeviceBuffer<double> a(cmax), b(cmax * static_cast<size_t>(comm->world()));
     MIINT_HIP(hipMemsetAsync(a.get(), 0, a.bytes(), s.get()));
@@ -171,16 +176,19 @@ int comm_sweep(const cli::Args& a, const cli::Topology& topo, double max_bytes, 
           else comm->broadcast(a.get(), counts[k], 0, s.get());
         };
         for (int w = 0; w < 3; ++w) issue();
+        s.sync();
+        agree.barrier();
         e0.record(s.get());
         for (int i = 0; i < iters; ++i) issue();
         e1.record(s.get());
         e1.sync();
         comm->check_async();
-        const double t = Event::elapsed_ms(e0, e1) / iters;
+        const double t = agree.max(Event::elapsed_ms(e0, e1) / iters);
         std::lock_guard<std::mutex> l(mu);
         ms[k * 3 + op] = std::max(ms[k * 3 + op], t);
       }
   };
+  capture_rccl_log();
   if (!topo.multiproc && topo.world == 1) {
     auto one = RcclComm::init_all({0});
     body(0, 0, one[0].get());
@@ -189,6 +197,7 @@ int comm_sweep(const cli::Args& a, const cli::Topology& topo, double max_bytes, 
   }
   if (topo.rank0 != 0) return 0;
   const double P = topo.world;
+  const RcclTransport tr = rccl_transport();  // the connections the sweep's collectives used
   for (size_t k = 0; k < counts.size(); ++k)
     for (int op = 0; op < 3; ++op) {
       const double bytes = counts[k] * 8.0 * (op == 1 ? P : 1.0);
@@ -201,7 +210,10 @@ int comm_sweep(const cli::Args& a, const cli::Topology& topo, double max_bytes, 
                        .add("bytes", bytes)
                        .add("us", t * 1e3)
                        .add("algbw_GBps", alg)
-                       .add("busbw_GBps", alg * factor),
+                       .add("busbw_GBps", alg * factor)
+                       .add("ranks_share_gpus", ranks_share_devices() && topo.world > 1)
+                       .add("rccl_transport", tr.transport)
+                       .add("rccl_nnodes", tr.nnodes),
                 true);
     }
   return 0;
@@ -284,13 +296,16 @@ int main(int argc, char** argv) {
       double value = 0.0, timed = 0.0, ms = 0.0;
       bool bucketed = false, chained = false, multistep = false;
       int streams = 1;
+      cli::RankFacts facts;
       std::mutex mu;
       cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
         Table2DPlan plan(c, dev, comm);
+        RankAgree agree(comm);
         const double v = plan.run();
-        const double t = plan.time(iters, graphs);
+        const double t = agree.max(plan.time(iters, graphs));  // barrier inside; slowest rank
         std::lock_guard<std::mutex> g(mu);
         if (rank == topo.rank0) {
+          facts.note(comm);
           value = v;
           timed = plan.last_result();
           bucketed = plan.bucketed() && graphs;
@@ -304,6 +319,7 @@ int main(int argc, char** argv) {
         cli::JsonRecord r;
         r.add("program", "table2d").add("grid", c.grid);
         r.add("step_streams", streams).add("multistep", multistep);
+        facts.add(r, topo);
         if (c.world > 1) {
           r.add("slice", std::to_string(c.rank) + "/" + std::to_string(c.world))
               .add("partial", value);

@@ -2,14 +2,17 @@
 // each, and wait for them (the reference launches riemann and 4main with Intel MPI's mpirun,
 // riemann.cpp:62-64, 4main.c:69-71; there is no MPI in this image).
 //
-//   miintrun -np P [--addr 127.0.0.1] [--port 0] [--grace 10] [--] PROGRAM [ARGS...]
+//   miintrun -np P [--addr 127.0.0.1] [--port 0] [--grace 10] [--linger 2] [--] PROGRAM [ARGS...]
 //
 // Every rank gets RANK, LOCAL_RANK, WORLD_SIZE, LOCAL_WORLD_SIZE, MASTER_ADDR and MASTER_PORT
 // (a free port when --port 0), the environment torchrun gives and the native CLIs, bench.py
 // and the Python package read: GPU ranks bootstrap RCCL from it, --device cpu ranks their
 // host collectives. The first rank that fails (non-zero exit or a signal) ends the others
 // (SIGTERM, SIGKILL after --grace seconds, to each rank's process group, so a rank's own
-// children go too) and its status is miintrun's; SIGINT / SIGTERM are forwarded. This
+// children go too) and its status is miintrun's; SIGINT / SIGTERM are forwarded. A rank
+// that EXITS with a status (rather than dying of a signal) first gives the others --linger
+// seconds to finish on their own: a failure the ranks agreed on (every rank exits 3 after a
+// scan timeout anywhere) then ends with rank 0's record printed, not cut off. This
 // process links no HIP and touches no GPU, so starting programs from it is safe; ranks are
 // started with fork + exec before anything in them has run.
 #include <arpa/inet.h>
@@ -36,7 +39,8 @@ void on_signal(int s) { g_signal = s; }
 
 int usage(FILE* out = stderr) {
   std::fprintf(out,
-               "usage: miintrun -np P [--addr A] [--port N] [--grace S] [--] PROGRAM [ARGS...]\n");
+               "usage: miintrun -np P [--addr A] [--port N] [--grace S] [--linger S] [--] "
+               "PROGRAM [ARGS...]\n");
   return out == stderr ? 2 : 0;
 }
 
@@ -46,7 +50,7 @@ int status_code(int st) { return WIFEXITED(st) ? WEXITSTATUS(st) : 128 + WTERMSI
 
 int main(int argc, char** argv) {
   int np = 0, port = 0;
-  double grace = 10.0;
+  double grace = 10.0, linger = 2.0;
   std::string addr = "127.0.0.1";
   int i = 1;
   for (; i < argc; ++i) {
@@ -63,6 +67,7 @@ int main(int argc, char** argv) {
     else if (a == "--addr") addr = val("--addr");
     else if (a == "--port") port = std::atoi(val("--port"));
     else if (a == "--grace") grace = std::atof(val("--grace"));
+    else if (a == "--linger") linger = std::atof(val("--linger"));
     else if (a == "--") { ++i; break; }
     else if (!a.empty() && a[0] == '-') {
       std::fprintf(stderr, "miintrun: unknown option %s\n", a.c_str());
@@ -106,8 +111,12 @@ int main(int argc, char** argv) {
   }
 
   int rc = 0, left = np;
-  bool stopping = false;
+  bool stopping = false, lingering = false;
   auto t_stop = std::chrono::steady_clock::now();
+  auto t_linger = t_stop;
+  auto since = [](std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count();
+  };
   auto signal_all = [&](int sig) {  // every live rank's whole process group
     for (pid_t p : pids)
       if (p > 0) ::kill(-p, sig);
@@ -124,12 +133,20 @@ int main(int argc, char** argv) {
         rc = code;
         std::fprintf(stderr, "miintrun: a rank exited with %d; stopping the others\n", code);
       }
-      if (code != 0 && !stopping) {
+      if (code != 0 && !stopping && !lingering && WIFEXITED(st) && linger > 0) {
+        lingering = true;  // an exit status: the peers may be finishing the same failure
+        t_linger = std::chrono::steady_clock::now();
+      } else if (code != 0 && !stopping) {
         stopping = true;
         t_stop = std::chrono::steady_clock::now();
         signal_all(SIGTERM);
       }
       continue;
+    }
+    if (lingering && !stopping && since(t_linger) > linger) {
+      stopping = true;
+      t_stop = std::chrono::steady_clock::now();
+      signal_all(SIGTERM);
     }
     if (g_signal && !stopping) {  // forwarded; the ranks' exits decide the status
       stopping = true;
@@ -137,9 +154,7 @@ int main(int argc, char** argv) {
       signal_all(g_signal);
       if (rc == 0) rc = 128 + g_signal;
     }
-    if (stopping && std::chrono::duration<double>(std::chrono::steady_clock::now() - t_stop)
-                            .count() > grace)
-      signal_all(SIGKILL);
+    if (stopping && since(t_stop) > grace) signal_all(SIGKILL);
     std::this_thread::sleep_for(std::chrono::milliseconds(20));
   }
   return rc;

@@ -6,8 +6,14 @@
 // Differences by design: every GPU works (the reference's rank 0 only receives, so P
 // processes give P-1 workers and P=1 prints 0 — SURVEY B10); the partial sums meet in one
 // RCCL all-reduce instead of P-1 MPI_Send/Recv pairs; N is 64-bit (1e10 works, B9).
-// --parity reproduces the master/worker partition numerics (P-1 workers, (int)(N/W)
-// samples each, rank-order sum, P=1 -> 0) on the GPU.
+// --parity runs the master/worker program itself on the GPUs: under P ranks (miintrun -np P,
+// torchrun, --gpus P, --loopback P) rank 0 coordinates and integrates nothing, rank r >= 1
+// integrates worker r-1's (int)(N/W) samples on its own GPU, the partials meet in one
+// allgather and rank 0 adds them in rank order (P=1 -> 0).
+//
+// Timing: every rank's clock starts after a collective barrier and the reported time is the
+// slowest rank's (max over the communicator); --json also reports ms_one_shot, one
+// integration per call from launch to the result in pinned host memory (median).
 //
 // --device cpu runs the reference's own side of the comparison natively on the host: every
 // rank (process) integrates its slice on --threads T vector threads (miint/host.hpp), and
@@ -27,10 +33,13 @@
 #include <cmath>
 #include <cstdio>
 #include <iostream>
+#include <memory>
 #include <sstream>
+#include <vector>
 
 #include "cli_common.hpp"
 #include "miint/expr.hpp"
+#include "miint/fault.hpp"
 #include "miint/host.hpp"
 #include "miint/integrator.hpp"
 #include "miint/oracle.hpp"
@@ -72,6 +81,7 @@ int run_host(const cli::Args& a, const RiemannConfig& cfg, double nd, int iters)
       const double t0 = wall_seconds();
       double v = c ? host_riemann(cfg, b, c, pool) : 0.0;
       if (hr.comm) hr.comm->allreduce_sum(&v, 1);
+      fault::delay(hr.rank);  // MIINT_FAULT_*: a slow rank (agreement tests)
       const double ms = (wall_seconds() - t0) * 1e3;
       if (i == 0 || ms < host_ms) host_ms = ms;
       result = v;
@@ -152,15 +162,22 @@ int run_expr(const cli::Args& a, const RiemannConfig& cfg, double nd, int iters)
   const cli::Topology topo = cli::topology(a);
   double result = 0.0, dev_ms = 0.0;
   std::mutex mu;
+  cli::RankFacts facts;
   cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
     ExprIntegrator ei(expr, dev);
+    RankAgree agree(comm);
     uint64_t b = 0, c = 0;
     rank_slice(cfg.n, rank, topo.world, &b, &c);
     const double v = ei.integrate(cfg.a, cfg.b, cfg.n, cfg.rule, b, c, 1.0, comm);
-    const double ms = ei.time(cfg.a, cfg.b, cfg.n, cfg.rule, b, c, iters);
+    // barrier right before the clock starts; the slowest rank's time
+    const double ms = agree.max(ei.time(cfg.a, cfg.b, cfg.n, cfg.rule, b, c, iters,
+                                        [&] { agree.barrier(); }, [&] { fault::delay(rank); }));
     std::lock_guard<std::mutex> g(mu);
-    if (rank == topo.rank0) result = v;
-    dev_ms = std::max(dev_ms, ms);
+    if (rank == topo.rank0) {
+      result = v;
+      dev_ms = ms;
+      facts.note(comm);
+    }
   });
   if (topo.rank0 != 0) return 0;
   const double secs = wall_seconds() - process_start_seconds();
@@ -174,6 +191,7 @@ int run_expr(const cli::Args& a, const RiemannConfig& cfg, double nd, int iters)
       .add("rule", a.str("rule", "left"))
       .add("gpus", topo.world)
       .add("result", result);
+  facts.add(r, topo);
   if (a.has("analytic")) {
     const double exact = a.num("analytic", 0.0);
     r.add("analytic", exact).add("abs_err", std::fabs(result - exact));
@@ -190,6 +208,7 @@ constexpr const char* kUsage =
     "usage: riemann [--n 1e9] [--gpus G] [--loopback W] [--integrand sin|pi4|poly|train|table]\n"
     "               [--rule left|mid|right] [--dtype fp64|fp32|fp32acc] [--div series|ieee]\n"
     "               [--iters K] [--block 64..1024] [--grid G] [--a A --b B] [--parity]\n"
+    "               [--no-one-shot]\n"
     "               [--json] [--jsonl FILE] [--profile FILE]\n"
     "               [--device cpu [--threads T] [--ranks P]]\n"
     "               [--expr EXPR --a A --b B [--analytic V]]\n"
@@ -239,39 +258,92 @@ int main(int argc, char** argv) {
     if (cli::on_cpu(a)) return run_host(a, cfg, nd, iters);
     const cli::Topology topo = cli::topology(a);
 
-    double result = 0.0, dev_ms = 0.0;
+    double result = 0.0, dev_ms = 0.0, wall_ms = 0.0, one_shot_ms = 0.0;
     LaunchShape launch_shape{0, cfg.block};
+    cli::RankFacts facts;
+    std::mutex mu;
+    std::vector<double> partials;  // --parity: the workers' partials, rank order
     if (a.flag("parity")) {
-      // riemann.cpp:65-86 numerics on the GPU: P = world ranks -> W = P-1 workers.
+      // riemann.cpp:62-86 as a distributed program: P = world ranks -> W = P - 1 workers. Rank
+      // 0 is the coordinator and integrates nothing; rank r >= 1 integrates worker r-1's
+      // slice [(r-1) R/W, r R/W) with (int)(N / W) samples on its own GPU; the partials meet
+      // in one allgather and rank 0 adds them in rank order (the MPI_Recv loop's rounding,
+      // riemann.cpp:82-85). P = 1: no workers, the sum is 0 (B10).
       const int P = topo.world;
       const int W = P - 1;
       MIINT_CHECK(W < 1 || nd / W < 2147483648.0,
                   "--parity reproduces riemann.cpp's int local_n: N / (P - 1) must stay below 2^31");
-      double g_sum = 0.0;
-      for (int w = 0; w < W; ++w) {
-        RiemannConfig c = cfg;
-        c.a = w * ((hi - lo) / W);
-        c.b = c.a + (hi - lo) / W;
-        c.n = static_cast<uint64_t>(static_cast<int>(nd / W));
-        RiemannPlan plan(c, w % device_count());
-        g_sum += plan.run();  // root receives in rank order
-      }
-      result = g_sum;
-    } else {
-      std::mutex mu;
       cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
-        RiemannPlan plan(cfg, dev, comm);
-        {
-          std::lock_guard<std::mutex> g(mu);
-          if (rank == topo.rank0) launch_shape = plan.shape();
+        RankAgree agree(comm);
+        std::unique_ptr<RiemannPlan> plan;
+        if (rank >= 1) {
+          RiemannConfig c = cfg;
+          const int w = rank - 1;
+          c.a = w * ((hi - lo) / W);
+          c.b = c.a + (hi - lo) / W;
+          c.n = static_cast<uint64_t>(static_cast<int>(nd / W));
+          c.multistep = false;  // one integration: the full grid, one fused launch
+          plan.reset(new RiemannPlan(c, dev));  // the worker's own; the partials meet below
+          plan->run();                          // cold: code-object load, first launch
         }
-        if (a.has("prepare")) plan.prepare_steps(static_cast<int>(a.integer("prepare", iters)));
-        plan.run_steps(1, comm != nullptr, false);  // cold: code-object load, first launch
-        StepTiming t = plan.run_steps(iters, comm != nullptr, iters > 1);
+        double partial = 0.0;
+        std::vector<double> best;
+        for (int it = 0; it < iters; ++it) {
+          agree.barrier();
+          const double t0 = wall_seconds();
+          if (plan) partial = plan->run();
+          const std::vector<double> all = agree.gather({partial});  // MPI_Send / MPI_Recv
+          fault::delay(rank);
+          best.push_back(agree.max((wall_seconds() - t0) * 1e3));
+          if (rank == topo.rank0 && it + 1 == iters) {
+            double g_sum = 0.0;
+            for (int q = 1; q < P; ++q) g_sum += all[static_cast<size_t>(q)];  // rank order
+            std::lock_guard<std::mutex> g(mu);
+            result = g_sum;
+            partials.assign(all.begin(), all.end());
+          }
+        }
         std::lock_guard<std::mutex> g(mu);
         if (rank == topo.rank0) {
-          result = plan.host_result(plan.host_index_of(iters - 1, iters > 1));
-          dev_ms = t.device_ms / iters;
+          dev_ms = *std::min_element(best.begin(), best.end());
+          wall_ms = dev_ms;
+          facts.note(comm);
+          if (plan) launch_shape = plan->shape();
+        }
+      });
+    } else {
+      cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
+        RiemannPlan plan(cfg, dev, comm);
+        RankAgree agree(comm);
+        if (a.has("prepare")) plan.prepare_steps(static_cast<int>(a.integer("prepare", iters)));
+        plan.run_steps(1, comm != nullptr, false);  // cold: code-object load, first launch
+        // the timed steps: every rank's clock starts after a collective barrier, the time
+        // reported is the slowest rank's (the reference's rank 0 stops its clock only after
+        // every worker's result has arrived, riemann.cpp:82-93)
+        StepTiming t = plan.run_steps(iters, comm != nullptr, iters > 1);
+        const double ms = agree.max(t.device_ms / iters);
+        const double wms = agree.max(t.wall_s * 1e3 / iters);
+        const double v = plan.host_result(plan.host_index_of(iters - 1, iters > 1));
+        // one integration per call, launch to pinned result (the reference's own timing unit)
+        double shot = 0.0;
+        if (!a.flag("no-one-shot")) {
+          if (!plan.collective()) {
+            shot = plan.time_one_shot(20, plan.direct() ? "direct_poll" : "direct", 5).median_us *
+                   1e-3;
+          } else {
+            std::vector<double> v1;
+            for (int k = 0; k < 10; ++k) v1.push_back(plan.run_steps(1, true, false).wall_s * 1e3);
+            shot = agree.max(cli::median(v1));
+          }
+        }
+        std::lock_guard<std::mutex> g(mu);
+        if (rank == topo.rank0) {
+          launch_shape = plan.shape();
+          result = v;
+          dev_ms = ms;
+          wall_ms = wms;
+          one_shot_ms = shot;
+          facts.note(comm);
         }
       });
     }
@@ -280,24 +352,46 @@ int main(int argc, char** argv) {
     print_result(secs, hi, nd, result);
     const double exact = f == Integrand::kTable ? oracle::table_integral(prof, lo, hi)
                                                 : oracle::analytic(f, lo, hi, cfg.coef, cfg.p0, cfg.p1);
-    cli::emit(a, cli::JsonRecord()
-                     .add("program", "riemann")
-                     .add("integrand", a.str("integrand", "sin"))
-                     .add("dtype", a.str("dtype", "fp64"))
-                     .add("rule", a.str("rule", "left"))
-                     .add("n", nd)
-                     .add("gpus", topo.world)
-                     .add("parity", a.flag("parity"))
-                     .add("result", result)
-                     .add("analytic", exact)
-                     .add("abs_err", std::fabs(result - exact))
-                     .add("rel_err", std::fabs(result - exact) / std::fabs(exact))
-                     .add("block", launch_shape.block)
-                     .add("grid", launch_shape.grid)
-                     .add("device_ms", dev_ms)
-                     .add("seconds_device", dev_ms * 1e-3)
-                     .add("subintervals_per_s", dev_ms > 0 ? nd / (dev_ms * 1e-3) : 0.0)
-                     .add("seconds_wall", secs));
+    cli::JsonRecord rec;
+    rec.add("program", "riemann")
+        .add("integrand", a.str("integrand", "sin"))
+        .add("dtype", a.str("dtype", "fp64"))
+        .add("rule", a.str("rule", "left"))
+        .add("n", nd)
+        .add("gpus", topo.world)
+        .add("parity", a.flag("parity"));
+    facts.add(rec, topo);
+    // --parity integrates W (int)(N / W) samples (fewer than N when W does not divide N)
+    const int workers = topo.world - 1;
+    const double work =
+        !a.flag("parity") ? nd
+                          : (workers >= 1 ? static_cast<double>(workers) *
+                                                static_cast<int>(nd / workers)
+                                          : 0.0);
+    if (a.flag("parity")) {
+      // the partials in rank order (rank 0, the coordinator, contributes 0)
+      std::string ps = "[";
+      for (size_t q = 0; q < partials.size(); ++q) {
+        char b[40];
+        std::snprintf(b, sizeof b, "%s%.17g", q ? "," : "", partials[q]);
+        ps += b;
+      }
+      rec.add("workers", workers).add("samples", work).add_raw("partials", ps + "]");
+    }
+    rec.add("result", result)
+        .add("analytic", exact)
+        .add("abs_err", std::fabs(result - exact))
+        .add("rel_err", std::fabs(result - exact) / std::fabs(exact))
+        .add("block", launch_shape.block)
+        .add("grid", launch_shape.grid)
+        .add("device_ms", dev_ms)
+        .add("seconds_device", dev_ms * 1e-3)
+        .add("wall_ms_per_integration", wall_ms)
+        .add("timing", a.flag("parity") ? "host, barrier to gathered partials, slowest rank"
+                                        : "hipEvent per integration, slowest rank")
+        .add("subintervals_per_s", dev_ms > 0 ? work / (dev_ms * 1e-3) : 0.0);
+    if (!a.flag("parity") && !a.flag("no-one-shot")) rec.add("ms_one_shot", one_shot_ms);
+    cli::emit(a, rec.add("seconds_wall", secs));
     return 0;
   } catch (const std::exception& e) {
     std::fprintf(stderr, "riemann: %s\n", e.what());

@@ -21,6 +21,7 @@
 //   ./trainscan [--gpus G] [--parity] [--replicate] [--no-phase2] [--algo onepass|fused|lookback]
 //               [--steps-per-sec S] [--iters K] [--json] [--jsonl FILE]
 //               [--device cpu [--threads T] [--ranks P] [--no-keep]] [--profile FILE]
+#include <cmath>
 #include <cstdio>
 
 #include "cli_common.hpp"
@@ -121,30 +122,52 @@ int main(int argc, char** argv) {
     if (topo.rank0 == 0)  // 4main.c:72-74 (tablelen/1800)
       std::printf("Step size of %ld\n", static_cast<long>(cfg.steps_per_sec));
     TrainScanResult res;
+    std::string timeout_what;
+    cli::RankFacts facts;
     std::mutex mu;
     cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
       TrainScan ts(cfg, dev, comm);
-      TrainScanResult r = ts.run();
-      for (int i = 1; i < iters; ++i) {  // --iters K: report the best device time
-        const TrainScanResult q = ts.run();
-        if (q.device_ms < r.device_ms) r.device_ms = q.device_ms;
-        r.timeout |= q.timeout;
+      RankAgree agree(comm);
+      TrainScanResult r;
+      try {
+        // every run starts behind a collective barrier; a timeout on any rank is agreed over
+        // the communicator and thrown on every rank together (TrainScan::run)
+        r = ts.run();
+        for (int i = 1; i < iters; ++i) {  // --iters K: report the best device time
+          const TrainScanResult q = ts.run();
+          if (q.device_ms < r.device_ms) r.device_ms = q.device_ms;
+        }
+      } catch (const ScanTimeout& e) {
+        r = TrainScanResult{};
+        r.distance = r.sum_of_sums = std::nan("");
+        r.timeout = 1;
+        r.timeout_ranks = e.ranks;
+        std::lock_guard<std::mutex> lk(mu);
+        timeout_what = e.what();
       }
+      if (!r.timeout) r.device_ms = agree.max(r.device_ms);  // the slowest rank's time
       std::lock_guard<std::mutex> lk(mu);
-      if (rank == topo.rank0) res = r;
+      if (rank == topo.rank0) {
+        res = r;
+        facts.note(comm);
+      }
+      if (r.timeout) res.timeout = 1;
     });
-    if (topo.rank0 != 0) return 0;
+    if (!timeout_what.empty()) std::fprintf(stderr, "trainscan: %s\n", timeout_what.c_str());
+    // exit status 3 on every rank when any rank's scan timed out (agreed in TrainScan::run)
+    if (topo.rank0 != 0) return res.timeout ? 3 : 0;
     const double secs = wall_seconds() - process_start_seconds();
     std::printf("%lf seconds\n", secs);
     std::printf("Total distance traveled = %lf\n", res.distance);
-    cli::emit(a, cli::JsonRecord()
-                     .add("program", "trainscan")
-                     .add("gpus", topo.world)
-                     .add("distance", res.distance)
+    cli::JsonRecord rec;
+    rec.add("program", "trainscan").add("gpus", topo.world);
+    facts.add(rec, topo);
+    cli::emit(a, rec.add("distance", res.distance)
                      .add("sum_of_sums", res.sum_of_sums)
                      .add("device_ms", res.device_ms)
                      .add("seconds_device", res.device_ms * 1e-3)
                      .add("timeout", static_cast<unsigned>(res.timeout))
+                     .add("timeout_ranks", res.timeout_ranks)
                      .add("seconds_wall", secs));
     return res.timeout ? 3 : 0;
   } catch (const std::exception& e) {

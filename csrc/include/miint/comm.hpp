@@ -245,6 +245,62 @@ class LoopbackGroup {
 void run_loopback(int world, int device, const std::function<void(int, const Comm*)>& fn,
                   double timeout_s = 120.0);
 
+// ------------------------------------------------------------------ rank agreement
+// Host values agreed over a communicator's ranks — what a multi-rank tool reports (the
+// reference's clock stops on rank 0 only after every worker's MPI_Recv, riemann.cpp:82-93, so
+// its time always covers the slowest worker):
+//   barrier()  every rank's clock starts after it returns (a 1-double all-reduce, drained)
+//   max(v)     the slowest rank's time        any(b)   a failure on one rank is every rank's
+// A null comm is one rank (everything is the identity). Collective: every rank of the
+// communicator calls the same methods in the same order. Each wait has the collective
+// watchdog (a rank that never arrives aborts the communicator and throws instead of hanging).
+class RankAgree {
+ public:
+  static constexpr size_t kMaxValues = 16;  // per rank per gather
+  explicit RankAgree(const Comm* comm, double timeout_s = 300.0);
+  ~RankAgree();
+  RankAgree(const RankAgree&) = delete;
+  RankAgree& operator=(const RankAgree&) = delete;
+  int world() const { return comm_ ? comm_->world() : 1; }
+  void barrier() const;
+  // world x v.size() values in rank order (v.size() <= kMaxValues)
+  std::vector<double> gather(const std::vector<double>& v) const;
+  double max(double v) const;
+  double min(double v) const;
+  bool any(bool v) const;
+
+ private:
+  const Comm* comm_;
+  double timeout_s_;
+  hipStream_t s_ = nullptr;
+  double* send_ = nullptr;  // device: kMaxValues
+  double* recv_ = nullptr;  // device: world x kMaxValues
+  double* host_ = nullptr;  // pinned: world x kMaxValues
+};
+
+// ------------------------------------------------------------------ RCCL transport evidence
+// Which transport RCCL picked between the ranks. RCCL reports it only in its INIT log ("...
+// via P2P/IPC", "... via NET/Socket/0", "nRanks 8 nNodes 1 localRanks 8"); a silent fallback
+// off xGMI (P2P disabled, a leaked NCCL_HOSTID splitting one node into W "hosts") would
+// otherwise go unrecorded. capture_rccl_log() routes RCCL's INIT-subsystem INFO lines into a
+// per-process file (NCCL_DEBUG_FILE; not stdout) — it must run before the process's first
+// RCCL call (RcclComm's constructors and unique_id() call it; MIINT_RCCL_LOG=0 turns it off)
+// — and rccl_transport() parses what RCCL wrote so far. Peer connections are made at a
+// communicator's first collective, so read it after one.
+struct RcclTransport {
+  std::string transport;   // distinct transports in first-seen order, '+'-joined: "P2P/IPC",
+                           // "NET/Socket", "SHM/direct", ...; "" = no connection line seen
+  int nranks = 0, nnodes = 0, local_ranks = 0;  // from "nRanks W nNodes N localRanks L"
+  int connections = 0;     // "via" lines
+  int comms = 0;           // "Init COMPLETE" lines
+  std::string log;         // the file parsed ("" when RCCL logging is not captured)
+  bool uses_net() const { return transport.find("NET/") != std::string::npos; }
+};
+RcclTransport parse_rccl_log(const std::string& text);
+void capture_rccl_log();
+std::string rccl_log_path();  // "" when not capturing
+RcclTransport rccl_transport();
+
 // Minimal TCP rendezvous for native multi-process launches (no MPI in the image, and the
 // CLI must not depend on Python): rank 0 listens on addr:port and hands the RCCL unique id
 // to every other rank. Used when the CLI is launched by torchrun --no-python.

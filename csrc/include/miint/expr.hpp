@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <functional>
 #include <memory>
 #include <string>
 
@@ -52,9 +53,11 @@ class ExprIntegrator {
   double integrate(double a, double b, uint64_t n, Rule rule, uint64_t begin, uint64_t count,
                    double scale = 1.0, const Comm* comm = nullptr);
   // Device ms per integration over `iters` back-to-back integrations (events, no host sync
-  // between them), for the same arguments.
+  // between them), for the same arguments. at_start runs on the host right before the first
+  // event is recorded (a multi-rank caller's barrier), at_end right before the last one.
   double time(double a, double b, uint64_t n, Rule rule, uint64_t begin, uint64_t count,
-              int iters);
+              int iters, const std::function<void()>& at_start = {},
+              const std::function<void()>& at_end = {});
   const std::string& expression() const { return expr_; }
 
  private:

@@ -104,6 +104,23 @@ struct StepTiming {
   int steps = 0;
 };
 
+// One integration per call, the reference's timing unit (cintegrate.cu:102-104,127-141 and
+// riemann.cpp:49-51,90-93 clock exactly one run): host time from the launch call to the
+// result readable in pinned host memory, and the device span of the same calls (hipEvents).
+//   direct       one fused launch (last-workgroup ticket) + hipStreamSynchronize
+//   direct_poll  the same launch; the host spins on the pinned result word the kernel
+//                stores (single GPU, host_direct), no stream synchronisation in the interval
+//   graph        a captured 1-step batch (+ its closing kernel) replayed + hipStreamSynchronize
+//   graph_poll   the same replay, host spinning on the pinned result
+// Every call starts from an idle stream; values are checked equal across calls.
+struct OneShotTiming {
+  std::string mode;
+  int reps = 0;
+  double median_us = 0.0, min_us = 0.0, max_us = 0.0;  // host: launch call -> result on host
+  double device_median_us = 0.0, device_min_us = 0.0;  // hipEvent span of the same calls
+  double value = 0.0;
+};
+
 class RiemannPlan {
  public:
   RiemannPlan(const RiemannConfig& cfg, int device, const Comm* comm = nullptr);
@@ -159,7 +176,13 @@ class RiemannPlan {
   // graphs=false: direct enqueue (result of step k in host slot k % host_capacity); with
   // pipeline=true and world > 1 the reduce/copy of step k overlaps compute of step k+1.
   // bucketed(): batches of `slots` steps, one all-reduce each, host slot k % slots.
+  // With a collective, every rank's clock starts after a collective barrier (barrier()).
   StepTiming run_steps(int steps, bool pipeline, bool graphs);
+  // Collective: returns once every rank of the plan's communicator has entered (a 1-double
+  // all-reduce, drained under the watchdog). No-op without a collective.
+  void barrier();
+  // See OneShotTiming. Single rank only.
+  OneShotTiming time_one_shot(int reps, const std::string& mode, int warmup = 20);
   // The same without synchronisation (bench.py brackets it with its own barrier + device
   // synchronize); call sync() before reading host results.
   void launch_steps(int steps, bool pipeline, bool graphs);
@@ -205,6 +228,7 @@ class RiemannPlan {
   DeviceBuffer<double> ms_partials_;  // multistep: slots x grid partials
   bool multistep_ = false;
   DeviceBuffer<double> result_;
+  DeviceBuffer<double> sync_;      // barrier(): the 1-double all-reduce's operand
   DeviceBuffer<unsigned int> ticket_;
   DeviceBuffer<double> table_;
   PinnedBuffer<double> host_;

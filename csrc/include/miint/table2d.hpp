@@ -73,6 +73,9 @@ class Table2DPlan {
   bool chained() const { return cfg_.chain && (!comm_ || world_ == 1 || bucketed_); }
   static constexpr int kGraphSteps = 32;
   int step_streams() const;  // chains a chained replay runs (1 when not chained)
+  // Collective over the plan's communicator (no-op on one rank): time() calls it right
+  // before its clock starts, so every rank's interval begins after every rank is here.
+  void barrier();
   // A chained replay is one multi-step launch (Table2DConfig::multistep, in effect).
   bool multistep() const { return chained() && multistep_; }
   int row0() const { return row0_; }
@@ -94,7 +97,7 @@ class Table2DPlan {
   std::vector<Stream> lanes_;  // streams 1.. of a multi-stream chained replay
   std::vector<std::unique_ptr<Event>> ev_join_;
   Event ev_fork_{false};
-  DeviceBuffer<double> v_, table_, partials_, chain_, result_;
+  DeviceBuffer<double> v_, table_, partials_, chain_, result_, sync_;
   DeviceBuffer<unsigned int> ticket_;
   PinnedBuffer<double> host_;
   Event e0_, e1_;

@@ -55,6 +55,15 @@ struct TrainScanResult {
   double distance_scan = 0.0;  // --parity: the printed element as the parallel scan rounds it
   double device_ms = 0.0;
   unsigned timeout = 0;      // look-back spin gave up (never expected)
+  int timeout_ranks = 0;     // ranks whose scan reported it (agreed over the communicator)
+};
+
+// A hand-off spin hit its limit on at least one rank. Every rank of the communicator throws
+// it together (the flag is all-reduced first), so no rank is left waiting in a collective
+// for a peer that gave up; the CLI turns it into exit status 3 on every rank.
+struct ScanTimeout : Error {
+  ScanTimeout(const std::string& what, int ranks_timed_out) : Error(what), ranks(ranks_timed_out) {}
+  int ranks = 0;  // how many ranks' scans gave up
 };
 
 // Kernel-level parameters of the fused pipeline (trainscan.hip).
@@ -128,7 +137,7 @@ class TrainScan {
   Stream stream_;
   DeviceBuffer<double> table_, vel_, pos_, full_;
   DeviceBuffer<char> state_;      // look-back scan state or fused-pipeline workspace
-  DeviceBuffer<double> scratch_;  // [0..7] scalars, [8..) gathered per-rank values
+  DeviceBuffer<double> scratch_;  // [0..11] scalars, [12..) gathered per-rank values
   PinnedBuffer<double> host_;
   Event e0_, e1_;
 };

@@ -195,6 +195,26 @@ PYBIND11_MODULE(_miint, m) {
       },
       py::arg("addr"), py::arg("port"), py::arg("rank"), py::arg("world"),
       py::arg("timeout_s") = 120.0);
+  // RCCL transport evidence (miint/comm.hpp): which transport the ranks' connections use
+  auto transport_dict = [](const RcclTransport& t) {
+    py::dict d;
+    d["transport"] = t.transport;
+    d["nranks"] = t.nranks;
+    d["nnodes"] = t.nnodes;
+    d["local_ranks"] = t.local_ranks;
+    d["connections"] = t.connections;
+    d["comms"] = t.comms;
+    d["uses_net"] = t.uses_net();
+    d["log"] = t.log;
+    return d;
+  };
+  m.def("parse_rccl_log", [transport_dict](const std::string& text) {
+    return transport_dict(parse_rccl_log(text));
+  });
+  m.def("capture_rccl_log", &capture_rccl_log,
+        "route RCCL's INIT log into a per-process file (call before the first RCCL call)");
+  m.def("rccl_log_path", &rccl_log_path);
+  m.def("rccl_transport", [transport_dict]() { return transport_dict(rccl_transport()); });
 
   // ------------------------------------------------------------------ Riemann plan
   py::class_<RiemannConfig>(m, "RiemannConfig")
@@ -264,6 +284,24 @@ PYBIND11_MODULE(_miint, m) {
              r["steps"] = t.steps;
              return r;
            }, py::arg("steps"), py::arg("pipeline") = true, py::arg("graphs") = true)
+      .def("barrier", &RiemannPlan::barrier, py::call_guard<py::gil_scoped_release>())
+      .def("time_one_shot", [](RiemannPlan& p, int reps, const std::string& mode, int warmup) {
+             OneShotTiming t;
+             {
+               py::gil_scoped_release nogil;
+               t = p.time_one_shot(reps, mode, warmup);
+             }
+             py::dict r;
+             r["mode"] = t.mode;
+             r["reps"] = t.reps;
+             r["median_us"] = t.median_us;
+             r["min_us"] = t.min_us;
+             r["max_us"] = t.max_us;
+             r["device_median_us"] = t.device_median_us;
+             r["device_min_us"] = t.device_min_us;
+             r["value"] = t.value;
+             return r;
+           }, py::arg("reps"), py::arg("mode") = "direct", py::arg("warmup") = 20)
       .def("host_result", &RiemannPlan::host_result)
       .def_property_readonly("host_capacity", &RiemannPlan::host_capacity)
       .def_property_readonly("slots", &RiemannPlan::slots)
@@ -521,9 +559,11 @@ PYBIND11_MODULE(_miint, m) {
       .def("integrate", &ExprIntegrator::integrate, py::arg("a"), py::arg("b"), py::arg("n"),
            py::arg("rule"), py::arg("begin"), py::arg("count"), py::arg("scale") = 1.0,
            py::arg("comm") = nullptr, py::call_guard<py::gil_scoped_release>())
-      .def("time", &ExprIntegrator::time, py::arg("a"), py::arg("b"), py::arg("n"),
-           py::arg("rule"), py::arg("begin"), py::arg("count"), py::arg("iters"),
-           py::call_guard<py::gil_scoped_release>())
+      .def("time",
+           [](ExprIntegrator& e, double a, double b, uint64_t n, Rule rule, uint64_t begin,
+              uint64_t count, int iters) { return e.time(a, b, n, rule, begin, count, iters); },
+           py::arg("a"), py::arg("b"), py::arg("n"), py::arg("rule"), py::arg("begin"),
+           py::arg("count"), py::arg("iters"), py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("expression", &ExprIntegrator::expression);
 
   // ------------------------------------------------------------------ host (CPU) engine

@@ -40,6 +40,7 @@ void prepare_shared_device_rccl(int rank) {
 }
 
 std::string RcclComm::unique_id() {
+  capture_rccl_log();  // before the process's first RCCL call (RCCL reads its env once)
   prepare_shared_device_rccl(-1);
   ncclUniqueId id;
   MIINT_RCCL(ncclGetUniqueId(&id));
@@ -52,6 +53,7 @@ RcclComm::RcclComm(const std::string& id, int rank, int world, int device)
   MIINT_CHECK(rank >= 0 && rank < world, "rank out of range");
   ncclUniqueId uid;
   std::memcpy(&uid, id.data(), sizeof(uid));
+  capture_rccl_log();
   prepare_shared_device_rccl(rank);
   DeviceGuard g(device);
   MIINT_RCCL(ncclCommInitRank(&comm_, world, uid, rank));
@@ -60,6 +62,7 @@ RcclComm::RcclComm(const std::string& id, int rank, int world, int device)
 std::vector<std::unique_ptr<Comm>> RcclComm::init_all(const std::vector<int>& devices) {
   const int n = static_cast<int>(devices.size());
   MIINT_CHECK(n >= 1, "need at least one device");
+  capture_rccl_log();
   std::vector<ncclComm_t> comms(n);
   MIINT_RCCL(ncclCommInitAll(comms.data(), n, devices.data()));
   std::vector<std::unique_ptr<Comm>> out;

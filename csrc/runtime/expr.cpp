@@ -181,14 +181,18 @@ double ExprIntegrator::integrate(double a, double b, uint64_t n, Rule rule, uint
 }
 
 double ExprIntegrator::time(double a, double b, uint64_t n, Rule rule, uint64_t begin,
-                            uint64_t count, int iters) {
+                            uint64_t count, int iters, const std::function<void()>& at_start,
+                            const std::function<void()>& at_end) {
   MIINT_CHECK(iters >= 1 && n >= 1 && begin + count <= n, "bad expression timing request");
   DeviceGuard g(device_);
   const double h = (b - a) / static_cast<double>(n);
   hipStream_t s = stream_.get();
   enqueue(a, h, rule_offset(rule), begin, count, h, s);  // warm
+  stream_.sync();
+  if (at_start) at_start();
   e0_.record(s);
   for (int i = 0; i < iters; ++i) enqueue(a, h, rule_offset(rule), begin, count, h, s);
+  if (at_end) at_end();
   e1_.record(s);
   stream_.sync();
   return Event::elapsed_ms(e0_, e1_) / iters;

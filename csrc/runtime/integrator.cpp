@@ -2,8 +2,12 @@
 #include "miint/integrator.hpp"
 
 #include <algorithm>
+#include <atomic>
+#include <cstring>
 #include <string>
+#include <vector>
 
+#include "miint/fault.hpp"
 #include "miint/trace.hpp"
 
 namespace miint {
@@ -78,8 +82,11 @@ RiemannPlan::RiemannPlan(const RiemannConfig& cfg, int device, const Comm* comm)
   }
   // Multi-step batches keep every workgroup resident for a whole batch: the auto grid is
   // capped at the multi-step kernel's residency (pi4 fp64: 7 x 256-thread workgroups per CU,
-  // 106 SGPRs); an explicit grid above it runs chained batches instead.
-  if (cfg.multistep) {
+  // 106 SGPRs); an explicit grid above it runs chained batches instead. The cap applies to
+  // every path of such a plan (run(), direct steps, graphs), so all of them sum the same
+  // partials, bit for bit. A plan whose batches can never run chained (unfused, or a
+  // collective without bucketing) keeps the full grid and allocates no multi-step partials.
+  if (cfg.multistep && chained()) {
     const int resident =
         riemann_multistep_grid(params_, cfg.dtype, cfg.div, cfg.block, info.num_cus);
     if (resident > 0 && cfg.grid <= 0 && shape_.grid > resident) shape_.grid = resident;
@@ -99,6 +106,8 @@ RiemannPlan::RiemannPlan(const RiemannConfig& cfg, int device, const Comm* comm)
   if (multistep_)
     ms_partials_ = DeviceBuffer<double>(static_cast<size_t>(cfg.slots) * shape_.grid);
   result_ = DeviceBuffer<double>(static_cast<size_t>(cfg.slots));
+  sync_ = DeviceBuffer<double>(1);
+  MIINT_HIP(hipMemset(sync_.get(), 0, sync_.bytes()));
   ticket_ = DeviceBuffer<unsigned int>(kTicketWords);
   MIINT_HIP(hipMemset(ticket_.get(), 0, ticket_.bytes()));
   MIINT_HIP(hipMemset(result_.get(), 0, result_.bytes()));
@@ -240,11 +249,13 @@ void RiemannPlan::enqueue_batch(hipStream_t cs, hipStream_t rs, int nsteps, bool
                                scale_, result_ptr(0), cs);
     else
       enqueue_chain_streams(cs, nsteps);
-    if (bucketed()) {  // one all-reduce + one copy of all the batch's results
+    if (bucketed())  // one all-reduce + one copy of all the batch's results
       comm_->allreduce_sum(result_.get(), result_.get(), static_cast<size_t>(nsteps), cs);
+    // results in device slots (a bucketed batch, or a single-GPU plan built with
+    // host_direct = false): one copy of the batch's results into pinned memory
+    if (!direct_)
       MIINT_HIP(hipMemcpyAsync(host_.get(), result_.get(), sizeof(double) * nsteps,
                                hipMemcpyDeviceToHost, cs));
-    }
     return;
   }
   if (bucketed()) {  // nsteps kernels, then one all-reduce + one copy of all their results
@@ -388,20 +399,95 @@ void RiemannPlan::sync() const {
   comm_stream_.sync();
 }
 
+void RiemannPlan::barrier() {
+  if (!collective()) return;
+  DeviceGuard g(device_);
+  comm_->allreduce_sum(sync_.get(), sync_.get(), 1, compute_.get());
+  if (cfg_.timeout_s > 0) wait_with_timeout(compute_.get(), cfg_.timeout_s, comm_);
+  else compute_.sync();
+}
+
 StepTiming RiemannPlan::run_steps(int steps, bool pipeline, bool graphs) {
   DeviceGuard g(device_);
   use_graphs(graphs, steps);
   StepTiming t;
   sync();
+  barrier();  // no rank's clock starts before every rank is here
   const double w0 = wall_seconds();
   ev_t0_.record(compute_.get());
   launch_steps(steps, pipeline, graphs);
+  fault::delay(rank_);            // MIINT_FAULT_*: a slow rank, for the agreement tests
   ev_t1_.record(compute_.get());  // every path leaves cs ordered after all of its work
   sync();
   t.wall_s = wall_seconds() - w0;
   t.device_ms = Event::elapsed_ms(ev_t0_, ev_t1_);
   t.steps = steps;
   return t;
+}
+
+OneShotTiming RiemannPlan::time_one_shot(int reps, const std::string& mode, int warmup) {
+  MIINT_CHECK(reps >= 1 && warmup >= 0, "time_one_shot: reps >= 1");
+  MIINT_CHECK(!collective(), "time_one_shot: single-rank plans only");
+  const bool graph = mode == "graph" || mode == "graph_poll";
+  const bool poll = mode == "direct_poll" || mode == "graph_poll";
+  MIINT_CHECK(graph || poll || mode == "direct",
+              "time_one_shot mode: direct|direct_poll|graph|graph_poll");
+  MIINT_CHECK(!poll || direct_, "a polled one-shot needs the result stored straight into pinned "
+                                "memory (single GPU, host_direct)");
+  DeviceGuard g(device_);
+  hipStream_t cs = compute_.get();
+  const Graph* g1 = graph ? batch_graph(1) : nullptr;
+  MIINT_CHECK(!graph || g1, "time_one_shot: 1-step graph capture failed: " + graph_error_);
+  // poll target: the host slot the launch stores into (step 0 of a batch, or run()'s slot 0)
+  volatile uint64_t* word = reinterpret_cast<volatile uint64_t*>(host_.get());
+  constexpr uint64_t kSentinel = 0x7ff8dead5eed0001ull;  // a NaN no integration produces
+  std::vector<double> host_us, dev_us;
+  double first = 0.0;
+  for (int i = 0; i < warmup + reps; ++i) {
+    MIINT_HIP(hipStreamSynchronize(cs));  // every call starts from an idle stream
+    *word = kSentinel;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    const double t0 = wall_seconds();
+    ev_t0_.record(cs);
+    if (graph) g1->launch(cs);
+    else enqueue(cs, 0, 0);
+    ev_t1_.record(cs);
+    if (poll) {
+      while (*word == kSentinel) {
+      }
+    } else {
+      MIINT_HIP(hipStreamSynchronize(cs));
+    }
+    const double t1 = wall_seconds();
+    MIINT_HIP(hipStreamSynchronize(cs));
+    uint64_t bits = *word;
+    double v;
+    std::memcpy(&v, &bits, sizeof(v));
+    if (!direct_) v = host_[0];
+    if (i == 0) first = v;
+    MIINT_CHECK(std::memcmp(&v, &first, sizeof(v)) == 0,
+                "time_one_shot: calls disagree (" + std::to_string(v) + " vs " +
+                    std::to_string(first) + ")");
+    if (i < warmup) continue;
+    host_us.push_back((t1 - t0) * 1e6);
+    dev_us.push_back(static_cast<double>(Event::elapsed_ms(ev_t0_, ev_t1_)) * 1e3);
+  }
+  last_mode_ = graph ? 1 : 0;
+  auto med = [](std::vector<double> v) {
+    std::sort(v.begin(), v.end());
+    const size_t n = v.size();
+    return n % 2 ? v[n / 2] : 0.5 * (v[n / 2 - 1] + v[n / 2]);
+  };
+  OneShotTiming r;
+  r.mode = mode;
+  r.reps = reps;
+  r.median_us = med(host_us);
+  r.min_us = *std::min_element(host_us.begin(), host_us.end());
+  r.max_us = *std::max_element(host_us.begin(), host_us.end());
+  r.device_median_us = med(dev_us);
+  r.device_min_us = *std::min_element(dev_us.begin(), dev_us.end());
+  r.value = first;
+  return r;
 }
 
 }  // namespace miint

@@ -3,8 +3,10 @@
 
 #include <algorithm>
 
+#include "miint/fault.hpp"
 #include "miint/integrator.hpp"
 #include "miint/oracle.hpp"
+#include "miint/trace.hpp"
 
 namespace miint {
 
@@ -32,10 +34,15 @@ Table2DPlan::Table2DPlan(const Table2DConfig& cfg, int device, const Comm* comm)
   const Table2DParams p{table_.get(), n, n, cfg.extent, cfg.extent, cfg.grid, cfg.grid,
                         row0_, std::max(row1_, row0_ + 1), cfg.min_wg};
   partials_ = DeviceBuffer<double>(static_cast<size_t>(table2d_grid(p)));
+  // bucketed_ first: chained() (and so the chain count below) depends on it
+  bucketed_ = cfg.bucket && comm_ && world_ > 1;
   multistep_ = cfg.multistep && row1_ > row0_ &&
                table2d_multistep_ok(p, device_info(device).num_cus);
   if (multistep_) ms_partials_ = DeviceBuffer<double>(kGraphSteps * partials_.size());
-  const int L = step_streams();
+  const int L = (!chained() || multistep_)
+                    ? 1
+                    : std::max(1, std::min(kGraphSteps, cfg_.step_streams > 0 ? cfg_.step_streams
+                                                                              : kAutoT2Streams));
   // chained launches: a double buffer per chain
   chain_ = DeviceBuffer<double>(2 * static_cast<size_t>(L) * partials_.size());
   for (int l = 1; l < L; ++l) {
@@ -43,18 +50,22 @@ Table2DPlan::Table2DPlan(const Table2DConfig& cfg, int device, const Comm* comm)
     ev_join_.emplace_back(new Event(false));
   }
   fill_unset_slots(partials_.get(), partials_.size(), stream_.get());  // fused kernel's slots
-  bucketed_ = cfg.bucket && comm_ && world_ > 1;
   result_ = DeviceBuffer<double>(kGraphSteps);
+  sync_ = DeviceBuffer<double>(1);
+  MIINT_HIP(hipMemset(sync_.get(), 0, sync_.bytes()));
   ticket_ = DeviceBuffer<unsigned int>(kTicketWords);
   MIINT_HIP(hipMemset(ticket_.get(), 0, ticket_.bytes()));
   host_ = PinnedBuffer<double>(kGraphSteps);
   stream_.sync();
 }
 
-int Table2DPlan::step_streams() const {
-  if (!chained() || multistep_) return 1;
-  return std::max(1, std::min(kGraphSteps, cfg_.step_streams > 0 ? cfg_.step_streams
-                                                                  : kAutoT2Streams));
+// the chains a chained replay actually runs: the plan's stream plus its lane streams
+int Table2DPlan::step_streams() const { return 1 + static_cast<int>(lanes_.size()); }
+
+void Table2DPlan::barrier() {
+  if (!comm_ || world_ <= 1) return;
+  comm_->allreduce_sum(sync_.get(), sync_.get(), 1, stream_.get());
+  wait_with_timeout(stream_.get(), 300.0, comm_);
 }
 
 void Table2DPlan::launch_local(double* out, hipStream_t s) {
@@ -90,8 +101,11 @@ double Table2DPlan::time(int iters, bool graphs) {
   hipStream_t s = stream_.get();
   if (!graphs) {
     enqueue(s);  // warm
+    stream_.sync();
+    barrier();  // no rank's clock starts before every rank is here
     e0_.record(s);
     for (int i = 0; i < iters; ++i) enqueue(s);
+    fault::delay(rank_);
     e1_.record(s);
     stream_.sync();
     return Event::elapsed_ms(e0_, e1_) / iters;
@@ -164,8 +178,11 @@ double Table2DPlan::time(int iters, bool graphs) {
   const double est_replay_ms = kGraphSteps * std::max(3e-3, samples * 5e-10);
   const int warm = std::max(1, static_cast<int>(cfg_.settle_ms / est_replay_ms));
   for (int i = 0; i < warm; ++i) launch_with(gc, graph_, s);
+  stream_.sync();
+  barrier();
   e0_.record(s);
   for (int i = 0; i < launches; ++i) launch_with(gc, graph_, s);
+  fault::delay(rank_);
   e1_.record(s);
   stream_.sync();
   last_batched_ = batched;

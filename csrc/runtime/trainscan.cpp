@@ -3,6 +3,7 @@
 
 #include <algorithm>
 
+#include "miint/fault.hpp"
 #include "miint/integrator.hpp"
 #include "miint/kernels.hpp"
 #include "miint/oracle.hpp"
@@ -17,7 +18,9 @@ constexpr int kCarry = 1;       // [1] look-back carry | [2..3] fused {C1, C2}
 constexpr int kPick = 4;        // [4] pick_global value
 constexpr int kTotals = 5;      // [5..6] fused {T1, T2}, [7] count
 constexpr int kParity = 8;      // [8..9] --parity serial {last, at}
-constexpr int kGather = 10;     // [10 ..) gathered values (3 per rank)
+constexpr int kFlag = 10;       // [10] timeout flag (all-reduced: ranks that timed out)
+constexpr int kSync = 11;       // [11] barrier operand
+constexpr int kGather = 12;     // [12 ..) gathered values (3 per rank)
 }  // namespace
 
 TrainScan::TrainScan(const TrainScanConfig& cfg, int device, const Comm* comm)
@@ -181,8 +184,15 @@ TrainScanResult TrainScan::run() {
   DeviceGuard g(device_);
   hipStream_t s = stream_.get();
   TrainScanResult r;
+  const bool multi = comm_ && world_ > 1;
+  double* sc = scratch_.get();
+  if (multi) {  // barrier: no rank's clock starts before every rank is here
+    comm_->allreduce_sum(sc + kSync, sc + kSync, 1, s);
+    wait_with_timeout(s, 300.0, comm_);
+  }
   e0_.record(s);
   enqueue();
+  fault::delay(rank_);
   e1_.record(s);
   MIINT_HIP(hipStreamSynchronize(s));
   r.device_ms = Event::elapsed_ms(e0_, e1_);
@@ -193,9 +203,24 @@ TrainScanResult TrainScan::run() {
                                   win_lo_, win_hi_};
     r.timeout = trainscan_local_timeout(p, state_.get(), s);
   }
+  if (fault::scan_timeout(rank_)) r.timeout = 1;  // MIINT_FAULT_*: the agreement tests
+  r.timeout_ranks = r.timeout ? 1 : 0;
+  if (multi) {  // a timeout on any rank is every rank's (before anyone enters another collective)
+    host_[1] = r.timeout ? 1.0 : 0.0;
+    MIINT_HIP(hipMemcpyAsync(sc + kFlag, host_.get() + 1, sizeof(double), hipMemcpyHostToDevice, s));
+    comm_->allreduce_sum(sc + kFlag, sc + kFlag, 1, s);
+    MIINT_HIP(hipMemcpyAsync(host_.get() + 1, sc + kFlag, sizeof(double), hipMemcpyDeviceToHost, s));
+    wait_with_timeout(s, 300.0, comm_);
+    r.timeout_ranks = static_cast<int>(host_[1]);
+    r.timeout = r.timeout_ranks > 0 ? 1u : 0u;
+  }
   // a look-back that gave up has poisoned its outputs with NaN: never hand them back
-  MIINT_CHECK(r.timeout == 0, "trainscan: a hand-off spin hit its limit (a predecessor tile or "
-                              "block never published); results are invalid");
+  if (r.timeout)
+    throw ScanTimeout("trainscan: a hand-off spin hit its limit on " +
+                      std::to_string(r.timeout_ranks) + " of " + std::to_string(world_) +
+                      " rank(s) (a predecessor tile or block never published); results are "
+                      "invalid",
+                      r.timeout_ranks);
   // 4main.c:241 prints default_sum[tablelen-2]; the complete integral is element T-1.
   const uint64_t gi = cfg_.parity ? total_ - 2 : total_ - 1;
   r.distance = pick_global(vel_.get(), gi, s) / cfg_.steps_per_sec;

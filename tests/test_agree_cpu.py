@@ -1,0 +1,101 @@
+"""Multi-rank agreement on the CPU: the reported time is the slowest rank's, RCCL's transport is
+read from its INIT log, and the bench's transport check fails a node-local run over a network.
+
+The reference's rank 0 stops its clock only after every worker's MPI_Recv (riemann.cpp:82-93),
+so its "seconds" always covers the slowest worker; these tests hold the native tools to the
+same (a rank made slow with MIINT_FAULT_RANK / MIINT_FAULT_DELAY_MS, miint/fault.hpp).
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(REPO, "build", "bin")
+sys.path.insert(0, REPO)
+
+import bench  # noqa: E402
+
+# Lines as RCCL 2.2x writes them under NCCL_DEBUG=INFO, NCCL_DEBUG_SUBSYS=INIT (the socket
+# ones are from profiles/r3/shared_rccl, two ranks sharing one GPU; the xGMI ones are the
+# format of the P2P transport's connect line).
+NET_LOG = """\
+host:1:1 [0] NCCL INFO NET/Socket : Using [0]lo:127.0.0.1<0>
+host:1:1 [0] NCCL INFO comm 0x5566 rank 0 nRanks 2 nNodes 2 localRanks 1 localRank 0 MNNVL 0
+host:1:1 [0] NCCL INFO Channel 00/0 : 1[0] -> 0[0] [receive] via NET/Socket/0
+host:1:1 [0] NCCL INFO Channel 00/0 : 0[0] -> 1[0] [send] via NET/Socket/0
+host:1:1 [0] NCCL INFO Channel 01/0 : 0[0] -> 1[0] [send] via NET/Socket/0
+host:1:1 [0] NCCL INFO comm 0x5566 rank 0 nranks 2 cudaDev 0 busId 5000 - Init COMPLETE
+"""
+P2P_LOG = """\
+host:7:7 [0] NCCL INFO comm 0x77 rank 0 nRanks 8 nNodes 1 localRanks 8 localRank 0 MNNVL 0
+host:7:7 [0] NCCL INFO Channel 00/0 : 0[0] -> 1[1] via P2P/IPC/read
+host:7:7 [0] NCCL INFO Channel 01/0 : 0[0] -> 1[1] via P2P/IPC/read
+host:7:7 [0] NCCL INFO Channel 00/0 : 7[7] -> 0[0] via P2P/IPC/read
+host:7:7 [0] NCCL INFO Channel 02/0 : 0[0] -> 2[2] via P2P/direct pointer
+host:7:7 [0] NCCL INFO comm 0x77 rank 0 nranks 8 cudaDev 0 busId 1000 - Init COMPLETE
+"""
+
+
+def test_parse_rccl_log_net(native):
+    t = native.parse_rccl_log(NET_LOG)
+    assert t["transport"] == "NET/Socket" and t["uses_net"]
+    assert (t["nranks"], t["nnodes"], t["local_ranks"]) == (2, 2, 1)
+    assert t["connections"] == 3 and t["comms"] == 1
+
+
+def test_parse_rccl_log_p2p(native):
+    t = native.parse_rccl_log(P2P_LOG)
+    assert t["transport"] == "P2P/IPC+P2P/direct" and not t["uses_net"]
+    assert (t["nranks"], t["nnodes"], t["local_ranks"]) == (8, 1, 8)
+    assert t["connections"] == 4
+
+
+def test_parse_rccl_log_empty(native):
+    t = native.parse_rccl_log("")
+    assert t["transport"] == "" and t["nnodes"] == 0 and not t["uses_net"]
+
+
+def test_transport_check(native, monkeypatch):
+    net, p2p = native.parse_rccl_log(NET_LOG), native.parse_rccl_log(P2P_LOG)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
+    # two ranks of one node on distinct GPUs over sockets: the record cannot stand
+    assert "expected P2P" in bench.transport_check(2, False, net)
+    # ... unless they share a GPU (MIINT_OVERSUBSCRIBE: sockets are the transport then)
+    assert bench.transport_check(2, True, net) is None
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    assert bench.transport_check(8, False, p2p) is None
+    assert bench.transport_check(1, False, net) is None
+    assert bench.transport_check(8, False, {}) is None  # no log: unknown, not failed
+    # a multi-node job legitimately crosses nodes over the network
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
+    assert bench.transport_check(2, False, net) is None
+
+
+def _run(args, env):
+    e = dict(os.environ, **env)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
+        e.pop(k, None)
+    p = subprocess.run(args, capture_output=True, text=True, timeout=120, env=e)
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-2000:])
+    return [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+
+
+@pytest.mark.parametrize("prog", ["riemann", "cintegrate"])
+def test_slow_rank_sets_the_reported_time(prog):
+    """Rank 1 of 2 holds its end-of-timing clock back by 400 ms: rank 0's record must report
+    at least that (the max over ranks), and a run without the fault must not."""
+    args = [os.path.join(BIN, "miintrun"), "-np", "2", "--", os.path.join(BIN, prog),
+            "--device", "cpu", "--threads", "1", "--json"]
+    if prog == "riemann":
+        args += ["--integrand", "pi4", "--n", "1e6"]
+    slow = _run(args, {"MIINT_FAULT_RANK": "1", "MIINT_FAULT_DELAY_MS": "400"})
+    fast = _run(args, {})
+    assert len(slow) == 1 and len(fast) == 1  # rank 0 prints
+    assert slow[0]["host_ms"] >= 400.0
+    assert fast[0]["host_ms"] < 400.0
+    assert slow[0]["result"] == fast[0]["result"]

@@ -561,3 +561,48 @@ def test_table2d_multistep_needs_residency(native, cuda):
     plan keeps chained launches (a persistent launch must be resident as a whole)."""
     p = native.Table2DPlan(8192, 1800.0, 0, None, True, True, 0)
     assert not p.multistep and p.step_streams == 2
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_host_direct_off_copies_batch_results(native, cuda, graphs):
+    """a single-GPU plan built with host_direct = false keeps its results in device
+    slots; a multi-step (or chained) batch must still copy them into pinned memory."""
+    m = native
+    cfg = m.RiemannConfig()
+    cfg.integrand, cfg.n, cfg.rule = m.Integrand.pi4, 50_000_017, m.Rule.mid
+    cfg.host_direct = False
+    cfg.slots = 8
+    p = m.RiemannPlan(cfg, 0)
+    assert not p.direct and p.multistep
+    want = p.run()
+    p.run_steps(11, False, graphs)
+    for k in range(8, 11):
+        assert p.host_result(p.host_index_of(k, graphs)) == want, k
+
+
+def test_full_grid_when_batches_never_run_multistep(cuda):
+    """the multi-step residency cap applies only to plans whose batches can run as
+    multi-step launches; an unfused plan keeps the full auto grid."""
+    capped = Integrator("pi4", n=10**9)
+    full = Integrator("pi4", n=10**9, fused=False)
+    assert capped.plan.multistep and not full.plan.multistep and not full.plan.chained
+    assert full.plan.grid > capped.plan.grid and full.plan.grid % 256 == 0
+
+
+@pytest.mark.parametrize("mode", ["direct", "direct_poll", "graph", "graph_poll"])
+def test_time_one_shot(cuda, mode):
+    """One integration per call, launch to pinned result (the reference's timing unit): every
+    form returns the integration's value, and the host interval covers the device span."""
+    it = Integrator("pi4", n=10**9, multistep=False)
+    r = it.plan.time_one_shot(10, mode, 3)
+    assert abs(abs(r["value"] - math.pi) - 1e-9) < 1e-13
+    assert r["reps"] == 10 and 0 < r["device_median_us"] <= r["median_us"] + 1.0
+    assert 20.0 < r["median_us"] < 5000.0
+
+
+def test_cli_riemann_reports_one_shot(cli_built):
+    p = _run([os.path.join(cli_built, "riemann"), "--integrand", "pi4", "--json", "--iters", "20"])
+    assert p.returncode == 0, p.stderr
+    js = json.loads(p.stdout.strip().splitlines()[-1])
+    assert js["ms_one_shot"] > js["device_ms"] * 0.9 and js["ms_one_shot"] < 5.0
+    assert js["comm"] == "none" and js["rccl_world"] == 0 and js["ranks_share_gpus"] is False

@@ -49,6 +49,21 @@ def test_first_failure_ends_the_job():
     assert time.time() - t < 20  # the sleeping ranks were stopped, not waited for
 
 
+def test_agreed_failure_lets_rank0_finish():
+    """A rank that EXITS non-zero gives the others --linger seconds: rank 0, failing the same
+    way a moment later (an agreed failure), still prints its record; a rank that never ends
+    is stopped once the linger is over."""
+    p = subprocess.run([RUN, "-np", "2", "--linger", "3", "sh", "-c",
+                        'if [ "$RANK" = 0 ]; then sleep 0.5; echo record; fi; exit 3'],
+                       capture_output=True, text=True, timeout=60)
+    assert p.returncode == 3 and "record" in p.stdout
+    t = time.time()
+    p = subprocess.run([RUN, "-np", "2", "--linger", "1", "--grace", "5", "sh", "-c",
+                        'if [ "$RANK" = 1 ]; then exit 3; fi; sleep 60'],
+                       capture_output=True, text=True, timeout=60)
+    assert p.returncode == 3 and time.time() - t < 20
+
+
 def test_signals_are_forwarded():
     proc = subprocess.Popen([RUN, "-np", "2", "sleep", "60"])
     time.sleep(0.5)

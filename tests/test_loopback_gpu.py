@@ -286,3 +286,17 @@ def test_cli_riemann_and_table2d_loopback(native, cuda):
     assert many["result"] == pytest.approx(one["result"], rel=1e-15, abs=0)
     t2 = json.loads(_cli([os.path.join(BIN, "miint"), "table2d", "--loopback", "3"])[-1])
     assert t2["rel_err_vs_oracle"] < 1e-14
+
+
+def test_cli_slow_loopback_rank_sets_rank0_time(native, cuda):
+    """Loopback rank 2 of 3 holds its end-of-timing event back by 300 ms (MIINT_FAULT_*): rank
+    0's record reports the slowest rank's time (RankAgree max), not its own."""
+    args = [os.path.join(BIN, "riemann"), "--integrand", "pi4", "--n", "1e8", "--loopback", "3",
+            "--json", "--no-one-shot"]
+    env = dict(os.environ, MIINT_FAULT_RANK="2", MIINT_FAULT_DELAY_MS="300")
+    p = subprocess.run(args, capture_output=True, text=True, timeout=300, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    slow = json.loads(p.stdout.strip().splitlines()[-1])
+    fast = json.loads(_cli(args)[-1])
+    assert slow["device_ms"] >= 300.0 and fast["device_ms"] < 300.0
+    assert slow["comm"] == "loopback" and slow["result"] == fast["result"]

@@ -85,7 +85,7 @@ def parse(argv=None) -> argparse.Namespace:
     p.add_argument("--dtype", default="fp64", choices=["fp64", "fp32", "fp32acc"],
                    help="fp32acc: fp32 samples AND fp32 accumulation to the workgroup partial "
                         "(pi4 only; fp32 folds tile values into fp64)")
-    p.add_argument("--div", default="series", choices=["series", "ieee", "series_direct"])
+    p.add_argument("--div", default="series", choices=["series", "ieee", "series_direct", "series_exact"])
     p.add_argument("--comm", default="native", choices=["native", "torch"],
                    help="native: C++ RCCL communicator captured in the step graph; "
                         "torch: torch.distributed all_reduce of each step's partial")

@@ -88,7 +88,8 @@ inline Rule parse_rule(const std::string& s) {
 inline DivMode parse_div(const std::string& s) {
   if (s == "series") return DivMode::kSeries;
   if (s == "ieee") return DivMode::kIeee;
-  fail("--div must be series or ieee (got " + s + ")", __FILE__, __LINE__);
+  if (s == "series_exact") return DivMode::kSeriesExact;
+  fail("--div must be series, series_exact or ieee (got " + s + ")", __FILE__, __LINE__);
 }
 
 // Print `text` and return true when --help / -h was given (main returns 0 then).

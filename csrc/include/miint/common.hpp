@@ -63,7 +63,10 @@ enum class Rule : int { kLeft = 0, kMid = 1, kRight = 2 };
 //                  pairwise from the tile midpoint, 1/d = s(1+e+e^2)   (default, 3.5 ops)
 //   kIeee          correctly rounded division for every sample (reference path)
 //   kSeriesDirect  the same series with x, d formed explicitly per sample (5 ops; A/B)
-enum class DivMode : int { kSeries = 0, kIeee = 1, kSeriesDirect = 2 };
+//   kSeriesExact   kSeries's residuals without the g = 1/2 + e fold: each sample accumulates
+//                  e + e^2 at e's own precision (3.5 ops; per-point within 1 ulp of IEEE
+//                  division where kSeries is within 5) — the accuracy A/B of the headline
+enum class DivMode : int { kSeries = 0, kIeee = 1, kSeriesDirect = 2, kSeriesExact = 3 };
 
 inline double rule_offset(Rule r) {
   return r == Rule::kLeft ? 0.0 : (r == Rule::kMid ? 0.5 : 1.0);

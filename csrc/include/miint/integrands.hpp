@@ -97,7 +97,7 @@ struct Pi4 : TileDefaults<Pi4> {
 
   template <DivMode M>
   __host__ __device__ static constexpr int tile_len() {
-    return M == DivMode::kSeries ? kSeriesTile : 32;
+    return (M == DivMode::kSeries || M == DivMode::kSeriesExact) ? kSeriesTile : 32;
   }
 
   // Constants held in registers for the whole kernel (see init()). Every fma of the pair
@@ -231,7 +231,21 @@ struct Pi4 : TileDefaults<Pi4> {
   // kSeries tiles are anchored at their midpoint; the lane loop passes x_m directly.
   template <int U, DivMode M>
   __device__ static constexpr double anchor() {
-    return M == DivMode::kSeries ? 0.5 * (U - 1) : 0.0;
+    return (M == DivMode::kSeries || M == DivMode::kSeriesExact) ? 0.5 * (U - 1) : 0.0;
+  }
+
+  // kSeriesExact: the same seed, centres and per-sample residuals as kSeries, without the
+  // 1/2 offset — e_c = e_m + c0 A + (c0^2 + kMeanK2) B, e_{+-k} = e_c + (k^2 - kMeanK2) B
+  // +- k A' — and every sample accumulates f = e + e^2 = fma(e, e, e) at e's own precision
+  // (|e| <= 2e-6: its rounding is ~1e-22 absolute), so the point's value s (1 + f) carries
+  // the roundings of 1 + f and of the product only: within 1 ulp of IEEE division, where
+  // kSeries's g = 1/2 + e rounds every sample at ulp(1/2) (up to 5 ulp). Per pair: c, e+-,
+  // f+- and two adds = 3.5 VALU per sample against kSeries's 2.5
+  // (profiles/r4/accuracy_ab.md).
+  __device__ __forceinline__ Seed seed_exact(double xm, double h) const {
+    const double dm = fma(xm, xm, 1.0);
+    const double s = __builtin_amdgcn_rcp(dm);
+    return {s, fma(-dm, s, 1.0), (-2.0 * h) * xm * s, -(h * h) * s};
   }
 
   template <int U, DivMode M>
@@ -262,9 +276,43 @@ struct Pi4 : TileDefaults<Pi4> {
         }
       }
       return fma(sd.s, t, acc);
+    } else if constexpr (M == DivMode::kSeriesExact) {
+      static_assert(U == kSeriesTile, "series tiles are kSubs sub-tiles of kSub samples");
+      const Seed sd = seed_exact(xa, h);
+      const double b2 = 2.0 * sd.b;
+      double t = 0.0;  // sum of e + e^2 over the tile (|t| <= 4e-4: ulp ~5e-20)
+#pragma unroll
+      for (int q = 0; q < kSubs; ++q) {
+        const double ec = centre_g(sd, q);         // e at the centre (+ mean k^2 B)
+        const double a = centre_slope(sd, b2, q);
+#pragma unroll
+        for (int j = 0; j < kPairs; ++j) {
+          const double c = fma(pk2[j], sd.b, ec);
+          const double ep = fma(pk[j], a, c);
+          const double en = fma(-pk[j], a, c);
+          t += fma(ep, ep, ep);
+          t += fma(en, en, en);
+          asm volatile("" : "+v"(t));
+        }
+      }
+      // U samples of s (1 + f): s U + s t
+      return fma(sd.s, t, fma(sd.s, static_cast<double>(U), acc));
     } else {
       return acc + tile<U, M>(xa, h);
     }
+  }
+
+  // kSeriesExact value of sample u of a full tile (validation kernel): s (1 + e + e^2).
+  __device__ __forceinline__ double series_exact_point(double xm, double h, int u) const {
+    const Seed sd = seed_exact(xm, h);
+    const double b2 = 2.0 * sd.b;
+    const int q = u / kSub, w = u % kSub;
+    const double ec = centre_g(sd, q);
+    const double a = centre_slope(sd, b2, q);
+    const int j = w >= kSub / 2 ? w - kSub / 2 : kSub / 2 - 1 - w;
+    const double c = fma(pk2[j], sd.b, ec);
+    const double e = w >= kSub / 2 ? fma(pk[j], a, c) : fma(-pk[j], a, c);
+    return sd.s * (1.0 + fma(e, e, e));
   }
 
   // Series value of sample u of a full tile, by exactly the operations tile_acc applies to

@@ -37,7 +37,7 @@ inline bool direct_ok(double h) { return kDirectHalfSpan * (h < 0 ? -h : h) <= 2
 // (5 VALU per sample against ~10 for IEEE division); coarser steps use IEEE division.
 inline DivMode effective_div(DivMode d, double h) {
   if (d == DivMode::kIeee) return d;
-  if (d == DivMode::kSeries && series_ok(h)) return d;
+  if ((d == DivMode::kSeries || d == DivMode::kSeriesExact) && series_ok(h)) return d;
   return direct_ok(h) ? DivMode::kSeriesDirect : DivMode::kIeee;
 }
 // Per integrand: the sin / train-velocity series path (angle addition from a per-tile sincos

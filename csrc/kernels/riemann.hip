@@ -488,8 +488,8 @@ __device__ __forceinline__ F make_functor(const RiemannParams& p, const double* 
     F f = Maker<F>::make(p, table, n, lds);
     f.init_series(p.coef_h, p.ncoef, p.h);
     return f;
-  } else if constexpr (__is_same(F, Pi4) && M != DivMode::kSeries) {
-    return Pi4{};  // the register-pinned pair tables (Pi4::init) serve only kSeries
+  } else if constexpr (__is_same(F, Pi4) && M != DivMode::kSeries && M != DivMode::kSeriesExact) {
+    return Pi4{};  // the register-pinned pair tables (Pi4::init) serve only the series tiles
   } else if constexpr (__is_same(F, Table) && M == DivMode::kSeries) {
     Table f{{}, table, n - 1};
     f.init();
@@ -752,6 +752,8 @@ __global__ __launch_bounds__(B) void point_values_kernel(RiemannParams p, const 
     if constexpr (M == DivMode::kSeries && __is_same(F, Pi4)) {
       // exactly the operations Pi4::tile_acc applies to sample u
       v = full ? f.series_point(xm, p.h, u) : f.point(x);
+    } else if constexpr (M == DivMode::kSeriesExact && __is_same(F, Pi4)) {
+      v = full ? f.series_exact_point(xm, p.h, u) : f.point(x);
     } else if constexpr (M == DivMode::kSeries && IsPolyF64<F>::value) {
       v = full ? f.series_point(xm, u) : f.point(x);
     } else if constexpr (M == DivMode::kSeries && __is_same(F, Table)) {
@@ -910,6 +912,7 @@ void dispatch(const RiemannParams& p, DType dtype, DivMode m, A&&... a) {
   switch (f) {
     case Integrand::kPi4:
       if (m == DivMode::kSeries) Op<DivMode::kSeries, Pi4>::run(a...);
+      else if (m == DivMode::kSeriesExact) Op<DivMode::kSeriesExact, Pi4>::run(a...);
       else if (m == DivMode::kSeriesDirect) Op<DivMode::kSeriesDirect, Pi4>::run(a...);
       else if (pi4_narrow(p)) Op<DivMode::kIeee, Pi4>::run(a...);
       else Op<DivMode::kIeee, Pi4Wide>::run(a...);

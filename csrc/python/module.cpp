@@ -80,7 +80,8 @@ PYBIND11_MODULE(_miint, m) {
   py::enum_<DivMode>(m, "DivMode")
       .value("series", DivMode::kSeries)
       .value("ieee", DivMode::kIeee)
-      .value("series_direct", DivMode::kSeriesDirect);
+      .value("series_direct", DivMode::kSeriesDirect)
+      .value("series_exact", DivMode::kSeriesExact);
 
   m.attr("TICKET_WORDS") = kTicketWords;
   m.attr("UNSET_SLOT_WORD") = kUnsetSlotWord;

@@ -596,8 +596,13 @@ def test_time_one_shot(cuda, mode):
     it = Integrator("pi4", n=10**9, multistep=False)
     r = it.plan.time_one_shot(10, mode, 3)
     assert abs(abs(r["value"] - math.pi) - 1e-9) < 1e-13
-    assert r["reps"] == 10 and 0 < r["device_median_us"] <= r["median_us"] + 1.0
-    assert 20.0 < r["median_us"] < 5000.0
+    assert r["reps"] == 10 and 20.0 < r["median_us"] < 5000.0
+    # a synchronised call's host interval covers the device span; a polled one may end before
+    # the kernel (or the graph's closing kernel) has drained and the end event fired
+    if not mode.endswith("_poll"):
+        assert 0 < r["device_median_us"] <= r["median_us"] + 1.0
+    else:
+        assert 0 < r["device_median_us"] <= r["median_us"] + 20.0
 
 
 def test_cli_riemann_reports_one_shot(cli_built):

@@ -20,7 +20,9 @@ EXT_SUFFIX := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_config_
 PY_INC     := $(shell $(PYTHON) -m pybind11 --includes)
 
 COMMON   := -std=c++17 -O3 -fPIC -Icsrc/include -Wall -Wno-unused-function
-DEVFLAGS := $(COMMON) --offload-arch=$(ARCH)
+# ABFLAGS: kernel variants for A/B builds (make cli BUILD=build/ab_x ABFLAGS=-D...; tools/*_ab.sh)
+ABFLAGS  ?=
+DEVFLAGS := $(COMMON) $(ABFLAGS) --offload-arch=$(ARCH)
 HOSTFLAGS:= $(COMMON) -I/opt/rocm/include -D__HIP_PLATFORM_AMD__
 LDLIBS   := -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lrccl -lhiprtc -lamdhip64 -lpthread -ldl
 

@@ -667,25 +667,47 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
     # (2) per-point accuracy of the division the headline used, on one 64 K-sample window
     #     of this rank's slice (rank 0's is reported)
     eff = str(integ.plan.effective_div).split(".")[-1]
-    if pi4 and args.dtype == "fp64" and eff != "ieee":
+    i0 = integ.plan.begin + integ.plan.count // 8 + 12_345
+    w = min(1 << 16, integ.plan.begin + integ.plan.count - i0)
+
+    def ulps(div):  # |value - IEEE value| in ulps of the IEEE value, every point of the window
         import torch
 
-        i0 = integ.plan.begin + integ.plan.count // 8 + 12_345
-        w = min(1 << 16, integ.plan.begin + integ.plan.count - i0)
-        v = kernels.point_values(integ.spec, n_total, rule=args.rule, div=eff, i_begin=i0,
+        v = kernels.point_values(integ.spec, n_total, rule=args.rule, div=div, i_begin=i0,
                                  n_local=w)
         r = kernels.point_values(integ.spec, n_total, rule=args.rule, div="ieee", i_begin=i0,
                                  n_local=w)
         spacing = torch.nextafter(r.abs(), torch.full_like(r, math.inf)) - r.abs()
         u = ((v - r) / spacing).abs()
-        out["per_point"] = {"max_ulp": float(u.max()),
-                            "frac_within_1ulp": float((u <= 1.0).double().mean()),
-                            "frac_within_2ulp": float((u <= 2.0).double().mean()),
-                            "window": [int(i0), int(w)], "bound_max_ulp": 5.0,
-                            "verified": bool(float(u.max()) <= 5.0)}
+        return {"max_ulp": float(u.max()),
+                "frac_within_1ulp": float((u <= 1.0).double().mean()),
+                "frac_within_2ulp": float((u <= 2.0).double().mean()),
+                "window": [int(i0), int(w)]}
+
+    if pi4 and args.dtype == "fp64" and eff != "ieee":
+        pp = ulps(eff)
+        out["per_point"] = dict(pp, bound_max_ulp=5.0, verified=bool(pp["max_ulp"] <= 5.0))
         out["per_point_max_ulp"] = out["per_point"]["max_ulp"]
         out["per_point_frac_within_1ulp"] = out["per_point"]["frac_within_1ulp"]
         out["per_point_window"] = out["per_point"]["window"]
+    # (2b) the same config with the series' residuals kept at their own precision
+    #      (div series_exact: 3.5 VALU per sample instead of 2.5): per point within ~1 ulp of
+    #      IEEE division, where the headline's g = 1/2 + e fold is within 5 — what the
+    #      headline's per-point accuracy costs in speed (profiles/r4/accuracy_ab.md)
+    if pi4 and args.dtype == "fp64" and args.div == "series":
+        ex = Integrator(args.integrand, n=n_total, div="series_exact", **kw)
+        steps = 48
+        ms = _timed_steps(ctx, ex.plan, steps, pipeline, dev)
+        v = ex.plan.host_result(ex.plan.host_index_of(steps - 1, True))
+        e = abs(v - math.pi)
+        pp = ulps("series_exact")
+        out["series_exact_div"] = {
+            "value": n_total / (ms * 1e-3), "ms_per_step": ms, "steps": steps, "result": v,
+            "abs_err": e, "division": str(ex.plan.effective_div).split(".")[-1],
+            "per_point": dict(pp, bound_max_ulp=2.0),
+            "verified": bool(result_ok("pi4", args.rule, args.dtype, n_total, e) and
+                             pp["max_ulp"] <= 2.0)}
+        del ex
     # (3) the headline metric's own config at every GPU count: N = 1e9 IN TOTAL split over
     #     the ranks (riemann.cpp:10,71-73: the reference keeps N fixed and divides it among
     #     its workers), its own graph and timing — equal to the headline at G = 1
@@ -742,6 +764,7 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
             "rel_err_vs_oracle": rel, "rows_this_rank": [p2.row0, p2.row1],
             "bucketed_allreduce": bool(p2.bucketed), "n_gpus": ctx.world,
             "step_streams": p2.step_streams, "multistep": bool(p2.multistep),
+            "phases": p2.phases,
             "verified": bool(rel <= 1e-12)}
         del p2
     # (6) BASELINE config #4: the same integral through the packed-fp32 path. Samples are

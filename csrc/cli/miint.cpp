@@ -230,6 +230,7 @@ constexpr const char* kUsage =
     "       miint sweep [--gpus G]\n"
     "       miint table2d [--grid 4096] [--gpus G] [--slice R/W] [--no-graph]\n"
     "                     [--step-streams S] [--min-wg W] [--settle-ms MS] [--no-multistep]\n"
+    "                     [--phases P]\n"
     "       miint selfcheck\n"
     "       miint comm [--gpus G] [--max-bytes 144e6] [--iters 20]\n"
     "Every record is one JSON line on stdout; --jsonl FILE also appends it to FILE.\n";
@@ -244,9 +245,10 @@ int main(int argc, char** argv) {
       std::printf("miint: %d HIP device(s), RCCL %s\n", nd, nd ? RcclComm::version().c_str() : "-");
       for (int d = 0; d < nd; ++d) {
         const DeviceInfo i = device_info(d);
-        std::printf("  [%d] %s %s  %d CUs  %.1f GHz  %.1f GB  L2 %d KB\n", d, i.name.c_str(),
-                    i.arch.c_str(), i.num_cus, i.clock_khz / 1e6, i.total_mem / 1e9,
-                    i.l2_bytes / 1024);
+        std::printf("  [%d] %s %s  %d CUs  %.1f GHz  %.1f GB  L2 %d KB  LDS %zu KB/CU (%zu KB/block)\n",
+                    d, i.name.c_str(), i.arch.c_str(), i.num_cus, i.clock_khz / 1e6,
+                    i.total_mem / 1e9, i.l2_bytes / 1024, i.lds_per_cu / 1024,
+                    i.lds_per_block / 1024);
       }
       return 0;
     }
@@ -285,6 +287,7 @@ int main(int argc, char** argv) {
       c.min_wg = static_cast<int>(a.integer("min-wg", 0));
       c.settle_ms = a.num("settle-ms", c.settle_ms);
       c.multistep = !a.flag("no-multistep");  // A-B: chained launches per integration
+      c.phases = static_cast<int>(a.integer("phases", 0));  // multi-step step phases (0 auto)
       // --slice R/W: time only rank R's rows of a W-GPU split, on this GPU (no collective)
       const std::string sl = a.str("slice", "");
       if (!sl.empty()) {
@@ -295,7 +298,7 @@ int main(int argc, char** argv) {
       }
       double value = 0.0, timed = 0.0, ms = 0.0;
       bool bucketed = false, chained = false, multistep = false;
-      int streams = 1;
+      int streams = 1, phases = 0, resident = 0;
       cli::RankFacts facts;
       std::mutex mu;
       cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
@@ -312,13 +315,16 @@ int main(int argc, char** argv) {
           chained = plan.chained() && graphs;
           multistep = plan.multistep() && graphs;
           streams = chained ? plan.step_streams() : 1;
+          phases = multistep ? plan.phases() : 0;
+          resident = plan.resident_per_cu();
         }
         if (t > ms) ms = t;
       });
       if (topo.rank0 == 0) {
         cli::JsonRecord r;
         r.add("program", "table2d").add("grid", c.grid);
-        r.add("step_streams", streams).add("multistep", multistep);
+        r.add("step_streams", streams).add("multistep", multistep).add("phases", phases);
+        r.add("resident_per_cu", resident);
         facts.add(r, topo);
         if (c.world > 1) {
           r.add("slice", std::to_string(c.rank) + "/" + std::to_string(c.world))

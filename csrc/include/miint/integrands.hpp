@@ -237,11 +237,10 @@ struct Pi4 : TileDefaults<Pi4> {
   // kSeriesExact: the same seed, centres and per-sample residuals as kSeries, without the
   // 1/2 offset — e_c = e_m + c0 A + (c0^2 + kMeanK2) B, e_{+-k} = e_c + (k^2 - kMeanK2) B
   // +- k A' — and every sample accumulates f = e + e^2 = fma(e, e, e) at e's own precision
-  // (|e| <= 2e-6: its rounding is ~1e-22 absolute), so the point's value s (1 + f) carries
-  // the roundings of 1 + f and of the product only: within 1 ulp of IEEE division, where
-  // kSeries's g = 1/2 + e rounds every sample at ulp(1/2) (up to 5 ulp). Per pair: c, e+-,
-  // f+- and two adds = 3.5 VALU per sample against kSeries's 2.5
-  // (profiles/r4/accuracy_ab.md).
+  // (|e| <= 2e-6: its rounding is ~1e-22 absolute), so the point's value s + s f is rounded
+  // once, where kSeries's g = 1/2 + e rounds every sample at ulp(1/2) (up to 5 ulp from IEEE
+  // division). Per pair: c, e+-, f+- and two adds = 3.5 VALU per sample against kSeries's 2.5:
+  // +37 % time at N = 1e9 (profiles/r4/accuracy_ab.md).
   __device__ __forceinline__ Seed seed_exact(double xm, double h) const {
     const double dm = fma(xm, xm, 1.0);
     const double s = __builtin_amdgcn_rcp(dm);
@@ -302,7 +301,8 @@ struct Pi4 : TileDefaults<Pi4> {
     }
   }
 
-  // kSeriesExact value of sample u of a full tile (validation kernel): s (1 + e + e^2).
+  // kSeriesExact value of sample u of a full tile (validation kernel): s + s (e + e^2), one
+  // rounding — what the tile adds for the sample (s U + s sum f: no 1 + f is ever formed).
   __device__ __forceinline__ double series_exact_point(double xm, double h, int u) const {
     const Seed sd = seed_exact(xm, h);
     const double b2 = 2.0 * sd.b;
@@ -312,7 +312,7 @@ struct Pi4 : TileDefaults<Pi4> {
     const int j = w >= kSub / 2 ? w - kSub / 2 : kSub / 2 - 1 - w;
     const double c = fma(pk2[j], sd.b, ec);
     const double e = w >= kSub / 2 ? fma(pk[j], a, c) : fma(-pk[j], a, c);
-    return sd.s * (1.0 + fma(e, e, e));
+    return fma(sd.s, fma(e, e, e), sd.s);
   }
 
   // Series value of sample u of a full tile, by exactly the operations tile_acc applies to

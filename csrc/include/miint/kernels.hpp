@@ -221,9 +221,19 @@ const char* table2d_path(const Table2DParams& p);
 // closing kernel: outs[s] = integration s, bitwise the chained / fused value. `partials`
 // holds steps x table2d_grid(p) doubles. Only for launches table2d_multistep_ok accepts (the
 // row-stream shape, every workgroup resident at once on num_cus CUs).
+// Step phases: the launch holds `phases` workgroups per row-stream block, workgroup phase f
+// running the steps s = f, f + phases, ... of its block — steps are independent, and a block
+// step is latency-bound (staging, a short row loop, the block reduction) at 2 waves per SIMD,
+// so several steps of one block in flight on different workgroups overlap those latencies.
+// Every partial is still one workgroup's, computed as in the one-phase launch: bitwise the
+// same values. 0 = auto: the most phases (<= kT2MaxPhases, <= steps) that stay resident.
+constexpr int kT2MaxPhases = 4;
 bool table2d_multistep_ok(const Table2DParams& p, int num_cus);
+// Multi-step workgroups resident per CU (hipOccupancy; 0 for a shape without the row stream).
+int table2d_multistep_resident(const Table2DParams& p);
+int table2d_multistep_phases(const Table2DParams& p, int num_cus, int steps, int want = 0);
 void launch_table2d_multistep(const Table2DParams& p, double* partials, int steps, double* outs,
-                              hipStream_t stream);
+                              hipStream_t stream, int phases = 1);
 void launch_table2d_partials(const Table2DParams& p, double* partials, hipStream_t stream);
 // One launch: partials + last-workgroup reduction into out[0] (ticket: kTicketWords words,
 // zero before the first launch; partials: table2d_grid(p) doubles filled with the unset

@@ -31,6 +31,8 @@ struct DeviceInfo {
   size_t total_mem = 0;
   int l2_bytes = 0;
   int max_threads_per_cu = 0;
+  size_t lds_per_cu = 0;     // maxSharedMemoryPerMultiProcessor (160 KB on MI355X)
+  size_t lds_per_block = 0;  // sharedMemPerBlock
 };
 
 int device_count();

@@ -49,6 +49,10 @@ struct Table2DConfig {
   // ramp and tail per replay. Used when the row-stream shape fits the GPU at once; bitwise
   // the same values.
   bool multistep = true;
+  // Multi-step step phases (launch_table2d_multistep): workgroups per row-stream block, each
+  // running every phases-th integration of the replay; 0 = auto (the most that stay
+  // resident, <= kT2MaxPhases), 1 = one workgroup per block (round 3's launch)
+  int phases = 0;
   int min_wg = 0;  // row stream: fewest workgroups its shape aims for (0 = kernel default)
   double settle_ms = 30.0;  // graph time(): untimed warm-up replays first (steady clocks)
 };
@@ -78,6 +82,8 @@ class Table2DPlan {
   void barrier();
   // A chained replay is one multi-step launch (Table2DConfig::multistep, in effect).
   bool multistep() const { return chained() && multistep_; }
+  int phases() const { return multistep() ? phases_ : 0; }  // step phases of a multi-step replay
+  int resident_per_cu() const { return resident_per_cu_; }  // multi-step workgroups per CU
   int row0() const { return row0_; }
   int row1() const { return row1_; }
 
@@ -86,6 +92,8 @@ class Table2DPlan {
   void launch_local(double* out, hipStream_t s);  // this rank's rows -> *out (device ptr)
   Table2DConfig cfg_;
   bool multistep_ = false;
+  int phases_ = 1;
+  int resident_per_cu_ = 0;
   DeviceBuffer<double> ms_partials_;  // multistep: kGraphSteps x workgroups
   int device_;
   const Comm* comm_;

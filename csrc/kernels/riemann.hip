@@ -223,7 +223,7 @@ struct Pi4F32 : TileDefaults<Pi4F32> {
         ecs[p2] = pk_fma(c0v, pk_fma(c0v, bb, aa), emv);
         aqs[p2] = pk_fma(c0v + c0v, bb, aa);
       }
-      f32x2 t;
+      f32x2 t, t1;
 #pragma unroll
       for (int q = 0; q < kSubs; ++q) {
         const float ec = (q & 1) ? ecs[q / 2].y : ecs[q / 2].x;
@@ -235,12 +235,22 @@ struct Pi4F32 : TileDefaults<Pi4F32> {
           const f32x2 k0 = {j + 0.5f, -(j + 0.5f)};
           const f32x2 k1 = {j + 1.5f, -(j + 1.5f)};
           const f32x2 e0 = pk_fma(k0, av, f32x2{cc.x, cc.x});  // (e_{+k_j}, e_{-k_j})
-          t = (q == 0 && j == 0) ? e0 : t + e0;
-          t += pk_fma(k1, av, f32x2{cc.y, cc.y});  // (e_{+k_{j+1}}, e_{-k_{j+1}})
+          const f32x2 e1 = pk_fma(k1, av, f32x2{cc.y, cc.y});  // (e_{+k_{j+1}}, e_{-k_{j+1}})
+          // two running sums: no pk_add waits on the one before it (one sum: a dependent
+          // v_pk_add_f32 chain with 20 s_nop hazard waits per tile; two: none, 39.6 -> 38.8 us
+          // per 1e9, profiles/r4/fp32_ab.md)
+          if (q == 0 && j == 0) {
+            t = e0;
+            t1 = e1;
+          } else {
+            t += e0;
+            t1 += e1;
+          }
           if (j + 2 < kSubLen / 2)
             cc = pk_fma(f32x2{4.0f * j + 6.0f, 4.0f * j + 10.0f}, bb, cc);
         }
       }
+      t += t1;
       // Tile value s (U + sum e) folded in fp64: in fp32, U + sum e (|sum e| ~ U |e_m| ~ 4e-6)
       // rounds at ulp(128) = 1.5e-5 and drops the seed's own correction e_m, leaving every
       // tile at U fl(1/d_m): a -8e-9 relative bias at N = 1e9 (reproduced on the host by a
@@ -305,7 +315,7 @@ struct Pi4F32Acc32 : Pi4F32 {
         ecs[p2] = pk_fma(c0v, pk_fma(c0v, bb, aa), emv);
         aqs[p2] = pk_fma(c0v + c0v, bb, aa);
       }
-      f32x2 t;
+      f32x2 t, t1;
 #pragma unroll
       for (int q = 0; q < kSubs; ++q) {
         const float ec = (q & 1) ? ecs[q / 2].y : ecs[q / 2].x;
@@ -317,12 +327,19 @@ struct Pi4F32Acc32 : Pi4F32 {
           const f32x2 k0 = {j + 0.5f, -(j + 0.5f)};
           const f32x2 k1 = {j + 1.5f, -(j + 1.5f)};
           const f32x2 e0 = pk_fma(k0, av, f32x2{cc.x, cc.x});
-          t = (q == 0 && j == 0) ? e0 : t + e0;
-          t += pk_fma(k1, av, f32x2{cc.y, cc.y});
+          const f32x2 e1 = pk_fma(k1, av, f32x2{cc.y, cc.y});
+          if (q == 0 && j == 0) {  // two running sums, as Pi4F32::tile_acc
+            t = e0;
+            t1 = e1;
+          } else {
+            t += e0;
+            t1 += e1;
+          }
           if (j + 2 < kSubLen / 2)
             cc = pk_fma(f32x2{4.0f * j + 6.0f, 4.0f * j + 10.0f}, bb, cc);
         }
       }
+      t += t1;
       return fmaf(s, static_cast<float>(UU) + (t.x + t.y), acc);  // all fp32
     } else {
       const float x0 = static_cast<float>(xmd);

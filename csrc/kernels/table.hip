@@ -475,14 +475,18 @@ __global__ __launch_bounds__(kB) void table2d_stream_kernel(Table2DParams p, int
 // step's partials in index order — bitwise the chained / fused value. One launch ramp and
 // tail per replay instead of per integration. The table pointer is laundered through an empty
 // asm every step, so no step's loads or arithmetic can be hoisted or shared.
+// Step phases (kernels.hpp): the grid is nb x phases workgroups; workgroup g runs block
+// g % nb for the steps g / nb, g / nb + phases, ...
 template <int SH>
 __global__ __launch_bounds__(kB) void table2d_multistep_kernel(Table2DParams p, int rows_per_wave,
                                                                int gx, double* partials,
-                                                               int steps) {
+                                                               int steps, unsigned nb) {
   __shared__ double tile[SH * kSW];
   __shared__ double red[kB / kWave];
-  const unsigned nb = gridDim.x;
-  const int bx = static_cast<int>(blockIdx.x) % gx, by = static_cast<int>(blockIdx.x) / gx;
+  const unsigned blk = blockIdx.x % nb;
+  const int phases = static_cast<int>(gridDim.x / nb);
+  const int first = static_cast<int>(blockIdx.x / nb);
+  const int bx = static_cast<int>(blk) % gx, by = static_cast<int>(blk) / gx;
   const T2DFoot f = t2d_footprint(p, rows_per_wave, bx, by);
   // Each step loads its own footprint from a table pointer laundered per step (no step's
   // loads are shared or hoisted). Short tiles (the multi-GPU row slices): step st's loads are
@@ -497,15 +501,17 @@ __global__ __launch_bounds__(kB) void table2d_multistep_kernel(Table2DParams p, 
     asm volatile("" : "+s"(t));  // a fresh pointer every step (no instructions)
     t2d_stage_load<SH>(t, p.nx, f, v);
   };
-  if constexpr (kPrefetch) load();
-  for (int st = 0; st < steps; ++st) {
+  if constexpr (kPrefetch) {
+    if (first < steps) load();
+  }
+  for (int st = first; st < steps; st += phases) {
     if constexpr (!kPrefetch) load();
     t2d_stage_store<SH, false>(f, v, tile);
     if constexpr (kPrefetch) {
-      if (st + 1 < steps) load();
+      if (st + phases < steps) load();
     }
     const double val = t2d_stream_rows(p, rows_per_wave, f, tile, red);
-    if (threadIdx.x == 0) partials[static_cast<size_t>(st) * nb + blockIdx.x] = val;
+    if (threadIdx.x == 0) partials[static_cast<size_t>(st) * nb + blk] = val;
     __syncthreads();  // the next step rewrites tile and red
   }
 }
@@ -675,27 +681,47 @@ int t2d_ms_per_cu() {
 }
 }  // namespace
 
-bool table2d_multistep_ok(const Table2DParams& p, int num_cus) {
+int table2d_multistep_resident(const Table2DParams& p) {
   check_table2d(p);
   const Table2DShape sh = table2d_shape(p);
-  if (!sh.stream) return false;
+  if (!sh.stream) return 0;
+  return sh.short_tile ? t2d_ms_per_cu<kSHShort>() : t2d_ms_per_cu<kSH>();
+}
+
+bool table2d_multistep_ok(const Table2DParams& p, int num_cus) {
+  return table2d_multistep_phases(p, num_cus, 1) >= 1;
+}
+
+// Step phases for a launch of `steps`: 0 if not even one phase is resident at once (or the
+// shape is not the row stream); else `want` (an explicit request, e.g. an A/B, even past
+// residency) or, for want = 0, the most phases (<= kT2MaxPhases, <= steps) resident at once.
+int table2d_multistep_phases(const Table2DParams& p, int num_cus, int steps, int want) {
+  check_table2d(p);
+  const Table2DShape sh = table2d_shape(p);
+  if (!sh.stream) return 0;
   const int per_cu = sh.short_tile ? t2d_ms_per_cu<kSHShort>() : t2d_ms_per_cu<kSH>();
-  return static_cast<long>(sh.grid.x) * sh.grid.y <= static_cast<long>(per_cu) * num_cus;
+  const long nb = static_cast<long>(sh.grid.x) * sh.grid.y;
+  const long fit = static_cast<long>(per_cu) * num_cus / nb;
+  if (want > 0) return fit >= 1 ? std::min(want, std::max(1, steps)) : 0;  // as asked (A/B)
+  return static_cast<int>(std::min<long>(fit, std::min(kT2MaxPhases, std::max(1, steps))));
 }
 
 void launch_table2d_multistep(const Table2DParams& p, double* partials, int steps, double* outs,
-                              hipStream_t stream) {
+                              hipStream_t stream, int phases) {
   check_table2d(p);
   MIINT_CHECK(steps >= 1 && steps <= 1024, "table2d multi-step: 1..1024 steps");
+  MIINT_CHECK(phases >= 1 && phases <= kT2MaxPhases, "table2d multi-step: 1..4 step phases");
   const Table2DShape sh = table2d_shape(p);
   MIINT_CHECK(sh.stream, "table2d multi-step runs the row-stream shape only");
   const int nb = static_cast<int>(sh.grid.x * sh.grid.y);
   const int gx = static_cast<int>(sh.grid.x);
+  const unsigned grid = static_cast<unsigned>(nb) * static_cast<unsigned>(phases);
   if (sh.short_tile)
-    table2d_multistep_kernel<kSHShort><<<nb, kB, 0, stream>>>(p, sh.rows_per_wave, gx, partials,
-                                                             steps);
+    table2d_multistep_kernel<kSHShort><<<grid, kB, 0, stream>>>(p, sh.rows_per_wave, gx, partials,
+                                                               steps, static_cast<unsigned>(nb));
   else
-    table2d_multistep_kernel<kSH><<<nb, kB, 0, stream>>>(p, sh.rows_per_wave, gx, partials, steps);
+    table2d_multistep_kernel<kSH><<<grid, kB, 0, stream>>>(p, sh.rows_per_wave, gx, partials,
+                                                          steps, static_cast<unsigned>(nb));
   MIINT_HIP(hipGetLastError());
   table2d_multistep_close_kernel<<<steps, kB, 0, stream>>>(partials, nb, outs);
   MIINT_HIP(hipGetLastError());

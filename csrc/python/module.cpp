@@ -469,8 +469,9 @@ PYBIND11_MODULE(_miint, m) {
   py::class_<Table2DPlan>(m, "Table2DPlan")
       .def(py::init([](int grid, double extent, int device, const Comm* comm, bool bucket,
                        bool chain, int step_streams, int slice_rank, int slice_world,
-                       bool multistep) {
+                       bool multistep, int phases) {
              Table2DConfig c;
+             c.phases = phases;
              c.grid = grid;
              c.extent = extent;
              c.bucket = bucket;
@@ -484,7 +485,8 @@ PYBIND11_MODULE(_miint, m) {
            py::arg("grid") = 4096, py::arg("extent") = 1800.0, py::arg("device") = 0,
            py::arg("comm") = nullptr, py::arg("bucket") = true, py::arg("chain") = true,
            py::arg("step_streams") = 0, py::arg("slice_rank") = 0, py::arg("slice_world") = 1,
-           py::arg("multistep") = true, py::keep_alive<1, 5>())
+           py::arg("multistep") = true, py::arg("phases") = 0, py::keep_alive<1, 5>())
+      .def_property_readonly("phases", &Table2DPlan::phases)
       .def_property_readonly("step_streams",
                              [](const Table2DPlan& p) { return p.step_streams(); })
       .def_property_readonly("multistep", &Table2DPlan::multistep)

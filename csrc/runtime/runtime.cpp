@@ -31,6 +31,8 @@ DeviceInfo device_info(int device) {
   d.total_mem = prop.totalGlobalMem;
   d.l2_bytes = prop.l2CacheSize;
   d.max_threads_per_cu = prop.maxThreadsPerMultiProcessor;
+  d.lds_per_cu = prop.maxSharedMemoryPerMultiProcessor;
+  d.lds_per_block = prop.sharedMemPerBlock;
   return d;
 }
 

@@ -36,9 +36,13 @@ Table2DPlan::Table2DPlan(const Table2DConfig& cfg, int device, const Comm* comm)
   partials_ = DeviceBuffer<double>(static_cast<size_t>(table2d_grid(p)));
   // bucketed_ first: chained() (and so the chain count below) depends on it
   bucketed_ = cfg.bucket && comm_ && world_ > 1;
-  multistep_ = cfg.multistep && row1_ > row0_ &&
-               table2d_multistep_ok(p, device_info(device).num_cus);
-  if (multistep_) ms_partials_ = DeviceBuffer<double>(kGraphSteps * partials_.size());
+  const int cus = device_info(device).num_cus;
+  multistep_ = cfg.multistep && row1_ > row0_ && table2d_multistep_ok(p, cus);
+  resident_per_cu_ = table2d_multistep_resident(p);
+  if (multistep_) {
+    ms_partials_ = DeviceBuffer<double>(kGraphSteps * partials_.size());
+    phases_ = std::max(1, table2d_multistep_phases(p, cus, kGraphSteps, cfg.phases));
+  }
   const int L = (!chained() || multistep_)
                     ? 1
                     : std::max(1, std::min(kGraphSteps, cfg_.step_streams > 0 ? cfg_.step_streams
@@ -128,7 +132,7 @@ double Table2DPlan::time(int iters, bool graphs) {
         const int n = static_cast<int>(oracle::profile_table().size());
         const Table2DParams p{table_.get(), n, n, cfg_.extent, cfg_.extent, cfg_.grid,
                               cfg_.grid, row0_, row1_, cfg_.min_wg};
-        launch_table2d_multistep(p, ms_partials_.get(), kGraphSteps, outs, cs);
+        launch_table2d_multistep(p, ms_partials_.get(), kGraphSteps, outs, cs, phases_);
       } else if (chained()) {
         // integration i runs on chain i % L as that chain's step i / L: launch j of a chain
         // closes the chain's launch j - 1 (its workgroup 0), a finalize closes each chain,

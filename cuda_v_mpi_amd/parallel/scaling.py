@@ -76,6 +76,8 @@ def run_comm(n: int, timeout: float = 600.0) -> dict:
         return {"error": p.stderr[-1000:]}
     rows = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
     out = {}
+    if rows:  # the transport the sweep's collectives used (one process, n devices)
+        out["comm_rccl_transport"] = rows[0].get("rccl_transport")
     for r in rows:
         b = r["bytes"] / (n if r["op"] == "allgather" else 1)  # per-rank payload
         if r["op"] in ("allreduce", "allgather") and (b == 8 or b >= 144e6 * 0.99):
@@ -107,6 +109,11 @@ def sweep(counts: list[int], steps: int = 200, warmup: int = 10, comm: bool = Tr
             "per_rank_spread_ms": b.get("per_rank_spread_ms"),
             "rccl_world": b.get("rccl_world"),
             "rccl_version": b.get("rccl_version"),
+            # what RCCL's INIT log says the ranks' connections use (P2P/IPC over xGMI on one
+            # node), and the record's verdict on it (bench.transport_check)
+            "rccl_transport": b.get("rccl_transport"),
+            "rccl_nnodes": b.get("rccl_nnodes"),
+            "transport_error": b.get("transport_error"),
             "graphs": b["config"]["graphs"],
             "verified": b["verified"],
         }
@@ -124,6 +131,9 @@ def sweep(counts: list[int], steps: int = 200, warmup: int = 10, comm: bool = Tr
         t2 = b.get("baseline5_table2d_4096")
         if t2:
             row["t2d_4096_us"] = t2["ms_per_integration"] * 1e3
+        one = b.get("single_shot_1e9")
+        if one:
+            row["one_shot_1e9_us"] = one["ms_one_shot"] * 1e3
         if comm and n <= have:  # miint comm drives n distinct devices from one process
             row.update(run_comm(n))
         rows.append(row)
@@ -145,7 +155,8 @@ def sweep(counts: list[int], steps: int = 200, warmup: int = 10, comm: bool = Tr
 def markdown(rows: list[dict]) -> str:
     cols = ["n_gpus", "value", "ms_per_step", "weak_eff", "strong_1e9_value", "strong_1e9_ms",
             "strong_1e9_eff", "strong_1e10_value", "strong_eff",
-            "t2d_4096_us", "t2d_strong_eff", "per_rank_spread_ms", "rccl_world", "allreduce_8B_us", "allgather_8B_us",
+            "t2d_4096_us", "t2d_strong_eff", "one_shot_1e9_us", "per_rank_spread_ms", "rccl_world",
+            "rccl_transport", "rccl_nnodes", "allreduce_8B_us", "allgather_8B_us",
             "allreduce_144MB_us", "allgather_144MB_us"]
     out = ["| " + " | ".join(cols) + " |", "|" + "---|" * len(cols)]
     for r in rows:

@@ -39,8 +39,14 @@ same integral through the packed-fp32 path ("baseline4_fp32", tile values folded
 and "baseline4_fp32_accum32", fp32 accumulation to the workgroup partial); #5, the 4096^2
 2-D velocity field with its rows split over the same GPUs ("baseline5_table2d_4096") — and
 the same integral on the node's host cores (the native host engine, the reference's own
-CPU/MPI side: "host_engine"). The record's "verified" is the AND of the headline's and every
-extra's; the exit status follows the headline's.
+CPU/MPI side: "host_engine"). Also: one integration per call, launch to pinned result, the
+reference's own timing unit ("single_shot_1e9"); the headline config with the series'
+residuals at their own precision ("series_exact_div": per point as accurate as IEEE division,
++37 % time); and the reference's own integrands through the same batches ("integrand_sin",
+"integrand_train", "integrand_table", "integrand_poly"). The record's "verified" is the AND of
+the headline's, every extra's and the RCCL transport check ("transport_verified": ranks of one
+node on distinct GPUs must not meet over a network transport); the exit status follows the
+headline's.
 
 One RCCL communicator per rank: with --comm native (default) the torch process group is gloo
 and carries only the control plane (barriers, the settle-count MAX, the per-rank times); the

@@ -208,7 +208,7 @@ constexpr const char* kUsage =
     "usage: riemann [--n 1e9] [--gpus G] [--loopback W] [--integrand sin|pi4|poly|train|table]\n"
     "               [--rule left|mid|right] [--dtype fp64|fp32|fp32acc] [--div series|ieee]\n"
     "               [--iters K] [--block 64..1024] [--grid G] [--a A --b B] [--parity]\n"
-    "               [--no-one-shot]\n"
+    "               [--no-one-shot] [--no-multistep] [--unfused]\n"
     "               [--json] [--jsonl FILE] [--profile FILE]\n"
     "               [--device cpu [--threads T] [--ranks P]]\n"
     "               [--expr EXPR --a A --b B [--analytic V]]\n"
@@ -245,6 +245,7 @@ int main(int argc, char** argv) {
     cfg.dtype = cli::parse_dtype(a.str("dtype", "fp64"));
     cfg.div = cli::parse_div(a.str("div", "series"));
     cfg.fused = !a.flag("unfused");
+    cfg.multistep = !a.flag("no-multistep");  // chained batches, full auto grid
     // --block: threads per workgroup (the reference's SP, cintegrate.cu:17-18); --grid:
     // workgroups (its SM), 0 = auto
     cfg.block = static_cast<int>(a.integer("block", kRiemannBlock));

@@ -31,6 +31,7 @@ for g in G1 G2; do
   run table2d_slice8 $g "${!g}" "$REPO/build/bin/miint" table2d --slice 0/8 --iters 320 --settle-ms 20
   run pi4_ieee $g "${!g}" "$REPO/build/bin/miint" bench --iters 20 --settle 60 --div ieee
   run pi4_fp32 $g "${!g}" "$REPO/build/bin/miint" bench --iters 200 --settle 300 --dtype fp32
+  run pi4_series_exact $g "${!g}" "$REPO/build/bin/miint" bench --iters 200 --settle 300 --div series_exact
   run sin $g "${!g}" "$REPO/build/bin/miint" bench --iters 200 --settle 300 --integrand sin
   run sin_ocml $g "${!g}" "$REPO/build/bin/miint" bench --iters 4 --integrand sin --div ieee \
     --trig-library --settle 16

@@ -16,3 +16,9 @@ for l in open("gpurun_out/r4/t2d_full_phases.jsonl"):
     r=json.loads(l); print(r["phases"], r["resident_per_cu"], r["ms_per_integration"], r["rel_err_vs_oracle"])
 '
 find gpurun_out/prof_oneshot -name "*.csv" | head
+timeout -k 10 300 bash tools/variant_ab.sh gpurun_out/r4/fused_tail_ab.jsonl "riemann --integrand pi4 --json --iters 20 --no-multistep" build/bin build/ab_tail/bin > /dev/null || exit 1
+python3 -c '
+import json
+for l in open("gpurun_out/r4/fused_tail_ab.jsonl"):
+    r=json.loads(l); print(r["build"], r["ms_one_shot"], r["device_ms"], r["grid"], r["result"])
+'

@@ -608,7 +608,9 @@ def single_shot(ctx, kw, args, pipeline, dev, reps: int = 50) -> dict:
         rec["grid"] = p.grid
         ok = True
         for mode in ("direct_poll", "direct", "graph_poll", "graph"):
-            r = p.time_one_shot(reps, mode, 20)
+            # 400 settling calls of the same form first (from idle the clocks need ~250 to
+            # settle: profiles/r4/oneshot_trace.md), then reps timed ones
+            r = p.time_one_shot(reps, mode, 400)
             e = abs(r["value"] - math.pi)
             ok = ok and abs(e - want) <= PI4_TOL
             rec["forms"][mode] = {"median_us": r["median_us"], "min_us": r["min_us"],

@@ -181,8 +181,11 @@ class RiemannPlan {
   // Collective: returns once every rank of the plan's communicator has entered (a 1-double
   // all-reduce, drained under the watchdog). No-op without a collective.
   void barrier();
-  // See OneShotTiming. Single rank only.
-  OneShotTiming time_one_shot(int reps, const std::string& mode, int warmup = 20);
+  // See OneShotTiming. Single rank only. The warm-up calls are timed the same way and
+  // dropped: from idle the clocks need a few hundred one-shot calls to settle (the fused
+  // kernel runs 90 us on the first call and 75.5 us from about the 250th,
+  // profiles/r4/oneshot_trace.md).
+  OneShotTiming time_one_shot(int reps, const std::string& mode, int warmup = 400);
   // The same without synchronisation (bench.py brackets it with its own barrier + device
   // synchronize); call sync() before reading host results.
   void launch_steps(int steps, bool pipeline, bool graphs);

@@ -38,9 +38,6 @@ constexpr int B = kRiemannBlock;  // the default block; validation kernels run a
 // cintegrate.cu:17-18,124-127): 64, 128, 256, 512 or 1024 threads. Everything that depends
 // on it reads blockDim.x; the hot tile loop itself does not.
 constexpr int kMaxBlock = 1024;
-#ifndef MIINT_AB_FUSED_TAIL
-#define MIINT_AB_FUSED_TAIL 0  // A/B builds only (Makefile ABFLAGS, tools/variant_ab.sh)
-#endif
 
 // Wave-uniform 64-bit value read from one lane (two 32-bit v_readlane).
 __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, int lane) {
@@ -605,25 +602,12 @@ __device__ __forceinline__ void fused_body(const RiemannParams& p, const double*
   double s;
   if constexpr (__is_same(Acc, double)) s = block_sum_dyn(lane_sum<M>(p, f, blockIdx.x), red);
   else s = static_cast<double>(block_sum_dyn(lane_sum<M>(p, f, blockIdx.x), red_acc));
-#if MIINT_AB_FUSED_TAIL
-  // A/B: a designated reducer (the last-dispatched workgroup) instead of the ticket
-  const unsigned last = gridDim.x - 1;
-  if (threadIdx.x == 0) slot_store(&partials[blockIdx.x], s);
-  if (blockIdx.x != last) return;
-  (void)ticket;
-  (void)is_last;
-  const double v = ordered_partials<0, true>(partials, static_cast<int>(gridDim.x));
-  rearm_slots<0>(partials, static_cast<int>(gridDim.x));
-  const double tot = block_sum_dyn(v, red);
-  if (threadIdx.x == 0) out[0] = tot * scale;
-#else
   if (!publish_and_ticket(s, partials, ticket, blockIdx.x, gridDim.x, &is_last)) return;
   const double v = ordered_partials<0, true>(partials, static_cast<int>(gridDim.x));
   rearm_slots<0>(partials, static_cast<int>(gridDim.x));
   const double tot = block_sum_dyn(v, red);
   if (threadIdx.x == 0) out[0] = tot * scale;
   rearm_ticket(ticket, gridDim.x);
-#endif
 }
 template <DivMode M, class F>
 __global__ __launch_bounds__(kMaxBlock) void riemann_fused_kernel(RiemannParams p, const double* table,

@@ -393,6 +393,19 @@ __device__ __forceinline__ double t2d_stream_rows(const Table2DParams& p, int ro
 #pragma unroll
   for (int b = 0; b < kSCols; ++b) acc[b] = lc[b] = ln[b] = d[b] = 0.0;
   int cur = -2;
+  // The next table row's LDS pair is read one row change ahead: in flight across the rows
+  // until the change that needs it, instead of waited for at the change (clamped to the
+  // footprint's last row; a read past the rows the wave uses is staged but never used).
+  // 4096^2: 5.99 -> 5.86 us per integration, row slices unchanged (profiles/r4/t2d_pf_ab_*).
+  double n0[kSCols], n1[kSCols];
+  auto fetch = [&](int j) {
+#pragma unroll
+    for (int b = 0; b < kSCols; ++b) {
+      const double* t = tile + (min(j, f.ty1) - f.ty0) * kSW + col[b];
+      n0[b] = t[0];
+      n1[b] = t[1];
+    }
+  };
   for (int k = 0; k < nrows; ++k) {
     const int iy = __builtin_amdgcn_readlane(iyl, k);
     const double fy = readlane_f64(fyl, k);
@@ -401,9 +414,10 @@ __device__ __forceinline__ double t2d_stream_rows(const Table2DParams& p, int ro
 #pragma unroll
         for (int b = 0; b < kSCols; ++b) {
           lc[b] = ln[b];
-          ln[b] = line(iy + 1, b);
+          ln[b] = fma(n1[b] - n0[b], fx[b], n0[b]);  // line(iy + 1, b), read ahead
           d[b] = ln[b] - lc[b];
         }
+        fetch(iy + 2);
       } else {
 #pragma unroll
         for (int b = 0; b < kSCols; ++b) {
@@ -411,6 +425,7 @@ __device__ __forceinline__ double t2d_stream_rows(const Table2DParams& p, int ro
           ln[b] = line(iy + 1, b);
           d[b] = ln[b] - lc[b];
         }
+        fetch(iy + 2);
       }
       cur = iy;
     }

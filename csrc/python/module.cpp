@@ -302,7 +302,7 @@ PYBIND11_MODULE(_miint, m) {
              r["device_min_us"] = t.device_min_us;
              r["value"] = t.value;
              return r;
-           }, py::arg("reps"), py::arg("mode") = "direct", py::arg("warmup") = 20)
+           }, py::arg("reps"), py::arg("mode") = "direct", py::arg("warmup") = 400)
       .def("host_result", &RiemannPlan::host_result)
       .def_property_readonly("host_capacity", &RiemannPlan::host_capacity)
       .def_property_readonly("slots", &RiemannPlan::slots)
@@ -487,6 +487,7 @@ PYBIND11_MODULE(_miint, m) {
            py::arg("step_streams") = 0, py::arg("slice_rank") = 0, py::arg("slice_world") = 1,
            py::arg("multistep") = true, py::arg("phases") = 0, py::keep_alive<1, 5>())
       .def_property_readonly("phases", &Table2DPlan::phases)
+      .def_property_readonly("resident_per_cu", &Table2DPlan::resident_per_cu)
       .def_property_readonly("step_streams",
                              [](const Table2DPlan& p) { return p.step_streams(); })
       .def_property_readonly("multistep", &Table2DPlan::multistep)

@@ -23,6 +23,7 @@ RankAgree::RankAgree(const Comm* comm, double timeout_s)
   const size_t w = static_cast<size_t>(comm_->world());
   MIINT_HIP(hipStreamCreateWithFlags(&s_, hipStreamNonBlocking));
   MIINT_HIP(hipMalloc(&send_, kMaxValues * sizeof(double)));
+  MIINT_HIP(hipMemset(send_, 0, kMaxValues * sizeof(double)));  // the barrier's operand
   MIINT_HIP(hipMalloc(&recv_, w * kMaxValues * sizeof(double)));
   MIINT_HIP(hipHostMalloc(reinterpret_cast<void**>(&host_), w * kMaxValues * sizeof(double),
                           hipHostMallocDefault));

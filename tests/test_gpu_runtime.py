@@ -556,6 +556,32 @@ def test_table2d_multistep_equals_chained(native, cuda, g, sl):
     assert a.last_result() == b.last_result()
 
 
+@pytest.mark.parametrize("g,sl", [(4096, (0, 8)), (4096, (5, 8)), (4096, (1, 4)), (4095, (0, 2)),
+                                  (5000, (3, 8))])
+@pytest.mark.parametrize("phases", [2, 3, 4])
+def test_table2d_multistep_phases_bitwise(native, cuda, g, sl, phases):
+    """Step phases: several workgroups per row-stream block, each running every phases-th
+    integration of the replay (32 integrations: 2, 3 and 4 phases, the last leaving 2 steps
+    for some phases) — every integration's value bitwise the one-phase launch's, and the
+    chained replay's."""
+    a = native.Table2DPlan(g, 1800.0, 0, None, True, True, 1, sl[0], sl[1], multistep=False)
+    one = native.Table2DPlan(g, 1800.0, 0, None, True, True, 1, sl[0], sl[1], phases=1)
+    many = native.Table2DPlan(g, 1800.0, 0, None, True, True, 1, sl[0], sl[1], phases=phases)
+    assert one.multistep and one.phases == 1 and many.phases == phases
+    for p in (a, one, many):
+        p.time(p.graph_steps, True)
+    assert a.last_result() == one.last_result() == many.last_result()
+    assert many.run() == one.run()
+
+
+def test_table2d_multistep_auto_phases(native, cuda):
+    """The auto phase count is the most that keep the launch resident: the 1/8 row slice of
+    4096^2 (512 blocks) runs more than one phase, and never more than kT2MaxPhases."""
+    p = native.Table2DPlan(4096, 1800.0, 0, None, True, True, 1, 0, 8)
+    assert p.multistep and 2 <= p.phases <= 4
+    assert p.phases * 512 <= p.resident_per_cu * native.device_info(0)["num_cus"]
+
+
 def test_table2d_multistep_needs_residency(native, cuda):
     """8192^2 in one piece needs more row-stream workgroups than the GPU holds at once: the
     plan keeps chained launches (a persistent launch must be resident as a whole)."""
@@ -594,7 +620,7 @@ def test_time_one_shot(cuda, mode):
     """One integration per call, launch to pinned result (the reference's timing unit): every
     form returns the integration's value, and the host interval covers the device span."""
     it = Integrator("pi4", n=10**9, multistep=False)
-    r = it.plan.time_one_shot(10, mode, 3)
+    r = it.plan.time_one_shot(10, mode, 50)
     assert abs(abs(r["value"] - math.pi) - 1e-9) < 1e-13
     assert r["reps"] == 10 and 20.0 < r["median_us"] < 5000.0
     # a synchronised call's host interval covers the device span; a polled one may end before

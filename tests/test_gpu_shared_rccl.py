@@ -71,7 +71,7 @@ def test_riemann_ranks_share_gpu_over_rccl(cuda, world):
     assert abs(rec[0]["abs_err"] - 1e-9) < 1e-13
     # W ranks on ONE GPU: barrier before every rank's clock + the slowest rank's time, so the
     # job can never beat the GPU's single-rank rate (round 3 reported 1.7-2.6x it)
-    assert rec[0]["subintervals_per_s"] <= 1.02 * one["subintervals_per_s"], (rec[0], one)
+    assert rec[0]["subintervals_per_s"] <= 1.05 * one["subintervals_per_s"], (rec[0], one)
 
 
 def test_slow_rank_sets_rank0_time_over_rccl(cuda):
@@ -113,7 +113,7 @@ def test_cintegrate_and_miint_ranks_share_gpu(cuda):
     _shared_rccl(b, 2)
     one = _records([os.path.join(BIN, "miint"), "bench", "--integrand", "pi4", "--iters", "20",
                     "--settle", "20"])[0]
-    assert b["subintervals_per_s"] <= 1.02 * one["subintervals_per_s"], (b, one)
+    assert b["subintervals_per_s"] <= 1.05 * one["subintervals_per_s"], (b, one)
 
 
 def test_table2d_two_ranks_reports_the_chains_it_ran(cuda):

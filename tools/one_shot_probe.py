@@ -46,7 +46,7 @@ def main() -> int:
     if hasattr(p, "time_one_shot"):
         for mode in ("direct", "graph", "direct_poll", "graph_poll"):
             try:
-                r = p.time_one_shot(reps, mode)
+                r = p.time_one_shot(reps, mode, 400)
             except Exception as e:  # noqa: BLE001
                 out.append({"form": "native_" + mode, "error": str(e)})
                 continue

@@ -355,6 +355,10 @@ __device__ __forceinline__ void t2d_stage_store(const T2DFoot& f, const double (
 
 // The rows of the workgroup's block from the staged tile (the barrier before them makes every
 // thread's tile writes visible). Returns the block's partial in thread 0.
+// READ_AHEAD (the multi-step kernel): the next table row's LDS pair is read one row change
+// ahead (below). The single-launch kernels keep the plain read: the read-ahead's 16 extra
+// VGPRs would cost them a wave per SIMD (6 -> 5 on the short tile).
+template <bool READ_AHEAD = false>
 __device__ __forceinline__ double t2d_stream_rows(const Table2DParams& p, int rows_per_wave,
                                                   const T2DFoot& f, const double* tile,
                                                   double* red) {
@@ -414,10 +418,11 @@ __device__ __forceinline__ double t2d_stream_rows(const Table2DParams& p, int ro
 #pragma unroll
         for (int b = 0; b < kSCols; ++b) {
           lc[b] = ln[b];
-          ln[b] = fma(n1[b] - n0[b], fx[b], n0[b]);  // line(iy + 1, b), read ahead
+          if constexpr (READ_AHEAD) ln[b] = fma(n1[b] - n0[b], fx[b], n0[b]);  // line(iy + 1)
+          else ln[b] = line(iy + 1, b);
           d[b] = ln[b] - lc[b];
         }
-        fetch(iy + 2);
+        if constexpr (READ_AHEAD) fetch(iy + 2);
       } else {
 #pragma unroll
         for (int b = 0; b < kSCols; ++b) {
@@ -425,7 +430,7 @@ __device__ __forceinline__ double t2d_stream_rows(const Table2DParams& p, int ro
           ln[b] = line(iy + 1, b);
           d[b] = ln[b] - lc[b];
         }
-        fetch(iy + 2);
+        if constexpr (READ_AHEAD) fetch(iy + 2);
       }
       cur = iy;
     }
@@ -525,7 +530,7 @@ __global__ __launch_bounds__(kB) void table2d_multistep_kernel(Table2DParams p, 
     if constexpr (kPrefetch) {
       if (st + phases < steps) load();
     }
-    const double val = t2d_stream_rows(p, rows_per_wave, f, tile, red);
+    const double val = t2d_stream_rows<true>(p, rows_per_wave, f, tile, red);
     if (threadIdx.x == 0) partials[static_cast<size_t>(st) * nb + blk] = val;
     __syncthreads();  // the next step rewrites tile and red
   }

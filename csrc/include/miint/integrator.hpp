@@ -112,7 +112,8 @@ struct StepTiming {
 //                stores (single GPU, host_direct), no stream synchronisation in the interval
 //   graph        a captured 1-step batch (+ its closing kernel) replayed + hipStreamSynchronize
 //   graph_poll   the same replay, host spinning on the pinned result
-// Every call starts from an idle stream; values are checked equal across calls.
+// Every call starts from an idle stream; values are checked equal across calls. Host-timed
+// calls record no events; the device span comes from as many event-timed calls in between.
 struct OneShotTiming {
   std::string mode;
   int reps = 0;

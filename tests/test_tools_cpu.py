@@ -98,3 +98,33 @@ def test_gap_report_csv_trace(tmp_path):
             w.writerow({"Kernel_Name": n, "Start_Timestamp": s, "End_Timestamp": e})
     out = _gap_report(tmp_path, 4)
     assert "gaps: max 0.00 us" in out and "over 4 dispatches" in out
+
+
+def test_shared_rccl_report_flags_records_above_one_rank(tmp_path):
+    """tools/shared_rccl_report.py: a multi-rank record on the shared GPU may not beat its
+    tool's one-rank rate (every tool reports the slowest rank behind a barrier); the report
+    marks one that does and exits 1."""
+    import json
+
+    recs = [
+        {"step": "riemann_np1", "gpus": 1, "comm": "none", "subintervals_per_s": 1.2e13},
+        {"step": "riemann_np2", "gpus": 2, "comm": "rccl", "rccl_world": 2,
+         "rccl_transport": "NET/Socket", "rccl_nnodes": 2, "ranks_share_gpus": True,
+         "subintervals_per_s": 1.1e13},
+        {"step": "miint_bench_np1", "gpus": 1, "subintervals_per_s": 1.3e13},
+        {"step": "miint_bench_np2", "gpus": 2, "subintervals_per_s": 1.9e13},  # impossible
+        {"step": "riemann_parity_np3", "gpus": 3, "subintervals_per_s": 5e12},
+        {"step": "miint_comm_np2", "op": "allreduce", "bytes": 8},
+        {"step": "miint_comm_np2", "op": "allgather", "bytes": 16},
+    ]
+    path = tmp_path / "records.jsonl"
+    path.write_text("".join(json.dumps(r) + "\n" for r in recs))
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "shared_rccl_report.py"),
+                        str(path)], capture_output=True, text=True)
+    assert p.returncode == 1, p.stdout + p.stderr
+    rows = {l.split("|")[1].strip(): l for l in p.stdout.splitlines() if l.startswith("| ")}
+    assert rows["riemann_np2"].rstrip().endswith("| yes |")
+    assert "**NO**" in rows["miint_bench_np2"]
+    assert "NET/Socket" in rows["riemann_np2"]
+    assert p.stdout.count("miint_comm_np2") == 1  # one row per step
+    assert "one-rank rate: 1" in p.stdout

@@ -772,7 +772,7 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
             "rel_err_vs_oracle": rel, "rows_this_rank": [p2.row0, p2.row1],
             "bucketed_allreduce": bool(p2.bucketed), "n_gpus": ctx.world,
             "step_streams": p2.step_streams, "multistep": bool(p2.multistep),
-            "phases": p2.phases,
+            "phases": p2.phases, "workgroups": p2.workgroups,
             "verified": bool(rel <= 1e-12)}
         del p2
     # (6) BASELINE config #4: the same integral through the packed-fp32 path. Samples are

@@ -298,7 +298,7 @@ int main(int argc, char** argv) {
       }
       double value = 0.0, timed = 0.0, ms = 0.0;
       bool bucketed = false, chained = false, multistep = false;
-      int streams = 1, phases = 0, resident = 0;
+      int streams = 1, phases = 0, resident = 0, min_wg = 0, wgs = 0;
       cli::RankFacts facts;
       std::mutex mu;
       cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
@@ -317,6 +317,8 @@ int main(int argc, char** argv) {
           streams = chained ? plan.step_streams() : 1;
           phases = multistep ? plan.phases() : 0;
           resident = plan.resident_per_cu();
+          min_wg = plan.min_wg();
+          wgs = plan.workgroups();
         }
         if (t > ms) ms = t;
       });
@@ -324,7 +326,7 @@ int main(int argc, char** argv) {
         cli::JsonRecord r;
         r.add("program", "table2d").add("grid", c.grid);
         r.add("step_streams", streams).add("multistep", multistep).add("phases", phases);
-        r.add("resident_per_cu", resident);
+        r.add("resident_per_cu", resident).add("min_wg", min_wg).add("workgroups", wgs);
         facts.add(r, topo);
         if (c.world > 1) {
           r.add("slice", std::to_string(c.rank) + "/" + std::to_string(c.world))

@@ -50,10 +50,14 @@ struct Table2DConfig {
   // the same values.
   bool multistep = true;
   // Multi-step step phases (launch_table2d_multistep): workgroups per row-stream block, each
-  // running every phases-th integration of the replay; 0 = auto (the most that stay
-  // resident, <= kT2MaxPhases), 1 = one workgroup per block (round 3's launch)
+  // running every phases-th integration of the replay; 0 = auto (kT2MaxPhases, once one
+  // phase is resident), 1 = one workgroup per block (round 3's launch)
   int phases = 0;
-  int min_wg = 0;  // row stream: fewest workgroups its shape aims for (0 = kernel default)
+  // row stream: fewest workgroups its shape aims for (0 = kernel default, 512 — except in a
+  // multi-step plan, whose step phases supply the parallelism: there 0 means the most rows
+  // per wave that fit the LDS tile, for every launch of the plan, so all its paths still
+  // sum the same partials; 1/8 slice of 4096^2: 1.48 -> 1.23 us, profiles/r4/t2d_slice_shapes)
+  int min_wg = 0;
   double settle_ms = 30.0;  // graph time(): untimed warm-up replays first (steady clocks)
 };
 // 4096^2 on one MI355X, us per integration by chains 1/2/3/4/8 (two runs each, settled
@@ -84,6 +88,8 @@ class Table2DPlan {
   bool multistep() const { return chained() && multistep_; }
   int phases() const { return multistep() ? phases_ : 0; }  // step phases of a multi-step replay
   int resident_per_cu() const { return resident_per_cu_; }  // multi-step workgroups per CU
+  int min_wg() const { return cfg_.min_wg; }  // the row-stream shape's target (after auto)
+  int workgroups() const { return static_cast<int>(partials_.size()); }  // per integration
   int row0() const { return row0_; }
   int row1() const { return row1_; }
 

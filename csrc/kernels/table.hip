@@ -713,8 +713,8 @@ bool table2d_multistep_ok(const Table2DParams& p, int num_cus) {
 }
 
 // Step phases for a launch of `steps`: 0 if not even one phase is resident at once (or the
-// shape is not the row stream); else `want` (an explicit request, e.g. an A/B, even past
-// residency) or, for want = 0, the most phases (<= kT2MaxPhases, <= steps) resident at once.
+// shape is not the row stream); else `want` (an explicit request) or, for want = 0,
+// kT2MaxPhases — both capped by steps.
 int table2d_multistep_phases(const Table2DParams& p, int num_cus, int steps, int want) {
   check_table2d(p);
   const Table2DShape sh = table2d_shape(p);
@@ -722,8 +722,12 @@ int table2d_multistep_phases(const Table2DParams& p, int num_cus, int steps, int
   const int per_cu = sh.short_tile ? t2d_ms_per_cu<kSHShort>() : t2d_ms_per_cu<kSH>();
   const long nb = static_cast<long>(sh.grid.x) * sh.grid.y;
   const long fit = static_cast<long>(per_cu) * num_cus / nb;
-  if (want > 0) return fit >= 1 ? std::min(want, std::max(1, steps)) : 0;  // as asked (A/B)
-  return static_cast<int>(std::min<long>(fit, std::min(kT2MaxPhases, std::max(1, steps))));
+  if (fit < 1) return 0;  // not even one workgroup per block resident: no multi-step
+  // Past residency the later phases' workgroups start as earlier ones finish (each runs
+  // steps / phases steps): 4 phases beat the resident count everywhere measured
+  // (profiles/r4/t2d_phases_explicit.jsonl: 4096^2 5.87 / 5.56 / 5.39 / 5.36 us at 1-4 phases
+  // with 1 resident; the 1/8 slice 1.92 / 1.48 / 1.49 / 1.45 with 2)
+  return std::min(want > 0 ? want : kT2MaxPhases, std::max(1, steps));
 }
 
 void launch_table2d_multistep(const Table2DParams& p, double* partials, int steps, double* outs,

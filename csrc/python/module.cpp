@@ -469,9 +469,10 @@ PYBIND11_MODULE(_miint, m) {
   py::class_<Table2DPlan>(m, "Table2DPlan")
       .def(py::init([](int grid, double extent, int device, const Comm* comm, bool bucket,
                        bool chain, int step_streams, int slice_rank, int slice_world,
-                       bool multistep, int phases) {
+                       bool multistep, int phases, int min_wg) {
              Table2DConfig c;
              c.phases = phases;
+             c.min_wg = min_wg;
              c.grid = grid;
              c.extent = extent;
              c.bucket = bucket;
@@ -485,8 +486,11 @@ PYBIND11_MODULE(_miint, m) {
            py::arg("grid") = 4096, py::arg("extent") = 1800.0, py::arg("device") = 0,
            py::arg("comm") = nullptr, py::arg("bucket") = true, py::arg("chain") = true,
            py::arg("step_streams") = 0, py::arg("slice_rank") = 0, py::arg("slice_world") = 1,
-           py::arg("multistep") = true, py::arg("phases") = 0, py::keep_alive<1, 5>())
+           py::arg("multistep") = true, py::arg("phases") = 0, py::arg("min_wg") = 0,
+           py::keep_alive<1, 5>())
       .def_property_readonly("phases", &Table2DPlan::phases)
+      .def_property_readonly("min_wg", &Table2DPlan::min_wg)
+      .def_property_readonly("workgroups", &Table2DPlan::workgroups)
       .def_property_readonly("resident_per_cu", &Table2DPlan::resident_per_cu)
       .def_property_readonly("step_streams",
                              [](const Table2DPlan& p) { return p.step_streams(); })

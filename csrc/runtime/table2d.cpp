@@ -31,12 +31,21 @@ Table2DPlan::Table2DPlan(const Table2DConfig& cfg, int device, const Comm* comm)
   table_ = DeviceBuffer<double>(static_cast<size_t>(n) * n);
   MIINT_HIP(hipMemcpy(v_.get(), prof.data(), v_.bytes(), hipMemcpyHostToDevice));
   launch_outer_product(v_.get(), n, table_.get(), stream_.get());
-  const Table2DParams p{table_.get(), n, n, cfg.extent, cfg.extent, cfg.grid, cfg.grid,
-                        row0_, std::max(row1_, row0_ + 1), cfg.min_wg};
-  partials_ = DeviceBuffer<double>(static_cast<size_t>(table2d_grid(p)));
-  // bucketed_ first: chained() (and so the chain count below) depends on it
+  // bucketed_ first: chained() (and so the multi-step choice and chain count) depends on it
   bucketed_ = cfg.bucket && comm_ && world_ > 1;
   const int cus = device_info(device).num_cus;
+  const auto params = [&](int min_wg) {
+    return Table2DParams{table_.get(), n, n, cfg.extent, cfg.extent, cfg.grid, cfg.grid,
+                         row0_, std::max(row1_, row0_ + 1), min_wg};
+  };
+  // A multi-step plan takes the most rows per wave that fit (min_wg 1): its step phases give
+  // the parallelism. Every launch of the plan (run(), the replay) uses that same shape, so
+  // all its paths sum the same partials (bitwise equal).
+  if (cfg.multistep && cfg.min_wg == 0 && chained() && row1_ > row0_ &&
+      table2d_multistep_ok(params(1), cus))
+    cfg_.min_wg = 1;
+  const Table2DParams p = params(cfg_.min_wg);
+  partials_ = DeviceBuffer<double>(static_cast<size_t>(table2d_grid(p)));
   multistep_ = cfg.multistep && row1_ > row0_ && table2d_multistep_ok(p, cus);
   resident_per_cu_ = table2d_multistep_resident(p);
   if (multistep_) {

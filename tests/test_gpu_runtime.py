@@ -530,13 +530,14 @@ def test_table2d_step_streams_equal(native, cuda):
     """The 2-D replay on 1, 2 and 4 chained streams and as one multi-step launch: the same 32
     results, bitwise."""
     res = []
+    ms = native.Table2DPlan(4096, 1800.0, 0, None, True, True, 2)
+    assert ms.multistep and ms.step_streams == 1
     for ss in (1, 2, 4):
-        p = native.Table2DPlan(4096, 1800.0, 0, None, True, True, ss, multistep=False)
+        p = native.Table2DPlan(4096, 1800.0, 0, None, True, True, ss, multistep=False,
+                               min_wg=ms.min_wg)
         assert p.step_streams == ss and not p.multistep
         p.time(p.graph_steps, True)
         res.append(p.last_result())
-    ms = native.Table2DPlan(4096, 1800.0, 0, None, True, True, 2)
-    assert ms.multistep and ms.step_streams == 1
     ms.time(ms.graph_steps, True)
     res.append(ms.last_result())
     assert res[0] == res[1] == res[2] == res[3] == native.table2d_oracle(4096)
@@ -547,10 +548,13 @@ def test_table2d_step_streams_equal(native, cuda):
 def test_table2d_multistep_equals_chained(native, cuda, g, sl):
     """Row slices and grids of several shapes: the multi-step replay (every integration
     re-stages its footprint in one persistent launch) gives the chained replay's partial,
-    bitwise."""
-    a = native.Table2DPlan(g, 1800.0, 0, None, True, True, 1, sl[0], sl[1], multistep=False)
+    bitwise (the chained plan given the multi-step plan's shape: a multi-step plan takes the
+    most rows per wave that fit, min_wg 1)."""
     b = native.Table2DPlan(g, 1800.0, 0, None, True, True, 1, sl[0], sl[1])
-    assert b.multistep
+    assert b.multistep and b.min_wg == 1
+    a = native.Table2DPlan(g, 1800.0, 0, None, True, True, 1, sl[0], sl[1], multistep=False,
+                           min_wg=b.min_wg)
+    assert a.workgroups == b.workgroups
     a.time(a.graph_steps, True)
     b.time(b.graph_steps, True)
     assert a.last_result() == b.last_result()
@@ -564,7 +568,8 @@ def test_table2d_multistep_phases_bitwise(native, cuda, g, sl, phases):
     integration of the replay (32 integrations: 2, 3 and 4 phases, the last leaving 2 steps
     for some phases) — every integration's value bitwise the one-phase launch's, and the
     chained replay's."""
-    a = native.Table2DPlan(g, 1800.0, 0, None, True, True, 1, sl[0], sl[1], multistep=False)
+    a = native.Table2DPlan(g, 1800.0, 0, None, True, True, 1, sl[0], sl[1], multistep=False,
+                           min_wg=1)
     one = native.Table2DPlan(g, 1800.0, 0, None, True, True, 1, sl[0], sl[1], phases=1)
     many = native.Table2DPlan(g, 1800.0, 0, None, True, True, 1, sl[0], sl[1], phases=phases)
     assert one.multistep and one.phases == 1 and many.phases == phases
@@ -575,11 +580,21 @@ def test_table2d_multistep_phases_bitwise(native, cuda, g, sl, phases):
 
 
 def test_table2d_multistep_auto_phases(native, cuda):
-    """The auto phase count is the most that keep the launch resident: the 1/8 row slice of
-    4096^2 (512 blocks) runs more than one phase, and never more than kT2MaxPhases."""
+    """Auto: kT2MaxPhases (4) step phases on the most rows per wave that fit (16 rows on
+    4096^2: 16 x 8 = 128 blocks for the 1/8 row slice, 16 x 64 for the whole field) — the
+    fastest measured (profiles/r4/t2d_slice_shapes.jsonl, t2d_phases_explicit.jsonl) — and
+    the same values as one phase."""
     p = native.Table2DPlan(4096, 1800.0, 0, None, True, True, 1, 0, 8)
-    assert p.multistep and 2 <= p.phases <= 4
-    assert p.phases * 512 <= p.resident_per_cu * native.device_info(0)["num_cus"]
+    assert p.multistep and p.phases == 4 and p.min_wg == 1 and p.workgroups == 128
+    full = native.Table2DPlan(4096)
+    assert full.multistep and full.phases == 4 and full.workgroups == 1024
+    one = native.Table2DPlan(4096, phases=1)
+    full.time(full.graph_steps, True)
+    one.time(one.graph_steps, True)
+    assert full.last_result() == one.last_result() == native.table2d_oracle(4096)
+    # an explicit shape target is kept
+    assert native.Table2DPlan(4096, 1800.0, 0, None, True, True, 1, 0, 8,
+                              min_wg=512).workgroups == 512
 
 
 def test_table2d_multistep_needs_residency(native, cuda):

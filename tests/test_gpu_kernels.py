@@ -778,9 +778,9 @@ def test_fp32_accumulation_policy(cuda, rule):
 def test_pi4_series_exact_per_point_accuracy(native, cuda, n):
     """div series_exact (the residual e kept at its own precision, each sample accumulating
     e + e^2): against the true value at the true coordinate (x87 extended precision) every
-    sample is within 2 ulp and the mean error within 0.5 ulp — as accurate as correctly
-    rounded division per sample (profiles/r4/accuracy_ab.md: 1.53 / 0.429 vs IEEE's 1.57 /
-    0.437), where the headline's g = 1/2 + e fold reaches 4 ulp; against the IEEE path's own
+    sample is within 2 ulp, and in every window the max and mean error match correctly
+    rounded division per sample's (profiles/r4/accuracy_ab.md: 1.53 / 0.429 vs IEEE's 1.57 /
+    0.437 over the bench windows), where the headline's g = 1/2 + e fold reaches 4 ulp; against the IEEE path's own
     values (which round the coordinate and 1 + x^2) within 2 ulp, >= 90 % within 1 (96.4 %
     over the bench windows, 93.6 % in the window at x = 0 where 1 + x^2 rounds least). The
     sum equals the IEEE path's to 1e-15 relative."""
@@ -800,9 +800,15 @@ def test_pi4_series_exact_per_point_accuracy(native, cuda, n):
         assert float((u <= 1.0).double().mean()) >= 0.90
         x = (np.arange(1 << 16, dtype=np.longdouble) + np.longdouble(i0)) * h
         true = np.longdouble(4) / (np.longdouble(1) + x * x)
-        ut = np.abs((v.cpu().numpy().astype(np.longdouble) - true) /
-                    np.spacing(true.astype(np.float64)).astype(np.longdouble)).astype(np.float64)
-        assert ut.max() <= 2.0 and ut.mean() <= 0.5
+
+        def vs_true(t):
+            return np.abs((t.cpu().numpy().astype(np.longdouble) - true) /
+                          np.spacing(true.astype(np.float64)).astype(np.longdouble)).astype(np.float64)
+        ut, ui = vs_true(v), vs_true(w)
+        # window by window as accurate as the per-sample IEEE path (whose own mean error is
+        # 0.55 ulp in the window at x -> 1, where the values cross 2)
+        assert ut.max() <= 2.0 and ut.max() <= ui.max() + 0.25, (i0, ut.max(), ui.max())
+        assert ut.mean() <= ui.mean() + 0.02, (i0, ut.mean(), ui.mean())
     ex = Integrator("pi4", n=n, div="series_exact").run().value
     ie = Integrator("pi4", n=n, div="ieee").run().value
     assert ex == pytest.approx(ie, rel=1e-15, abs=0)

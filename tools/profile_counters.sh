@@ -41,6 +41,11 @@ for g in G1 G2; do
   run table2d $g "${!g}" "$REPO/build/bin/miint" table2d --iters 320 --settle-ms 20
   run dpp_selftest $g "${!g}" python3 "$REPO/tools/dpp_probe.py"
 done
+# the 2-D field re-stages its table footprint every integration: bytes fetched past L2
+for g in G3; do
+  run table2d_slice8 $g "${!g}" "$REPO/build/bin/miint" table2d --slice 0/8 --iters 320 --settle-ms 20
+  run table2d $g "${!g}" "$REPO/build/bin/miint" table2d --iters 320 --settle-ms 20
+done
 for g in G1 G2 G3 G4; do
   run trainscan $g "${!g}" "$REPO/build/bin/trainscan"
   run materialize $g "${!g}" "$REPO/build/bin/cintegrate" --materialize

@@ -259,12 +259,21 @@ __global__ __launch_bounds__(kB) void table2d_kernel(Table2DParams p, double* pa
 // counting staging, column setup and the hand-off at 64 samples per lane).
 constexpr int kSCols = 4;                 // columns per lane: a workgroup spans 256 columns
 constexpr int kSW = kWave * kSCols / 2;   // LDS footprint width (cells), 128
-constexpr int kSH = 32;                   // LDS footprint height (cells)
+// LDS footprint height (cells). A/B switch MIINT_T2D_SH (even: kStageRows rows per pass).
+#ifndef MIINT_T2D_SH
+#define MIINT_T2D_SH 32
+#endif
+constexpr int kSH = MIINT_T2D_SH;
+static_assert(kSH % 2 == 0 && kSH >= 16, "kSH: even, >= the short tile");
+// the multi-step row loop's LDS read-ahead (t2d_stream_rows<true>); A/B switch
+#ifndef MIINT_T2D_READ_AHEAD
+#define MIINT_T2D_READ_AHEAD 1
+#endif
 // A launch whose row footprint fits half of it stages a kSH / 2-row tile instead: the
 // branch-free staging loads every tile row whatever the footprint, so the short footprints of
 // the 4-rows-per-wave shapes (multi-GPU row slices) load and write half the rows
 // (profiles/r2/table2d_short_tile.jsonl).
-constexpr int kSHShort = kSH / 2;
+constexpr int kSHShort = 16;
 
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
   const long long bits = __builtin_bit_cast(long long, v);
@@ -291,6 +300,8 @@ __device__ __forceinline__ double fma_sv(double a, double s, double c) {
 struct T2DFoot {
   double sx, sy, cx, cy;
   int c0, r0, r1, tx0, ty0, tx1, ty1;
+  int sy0;  // first staged table row: ty0, moved up at the table's bottom edge so that all
+            // SH staged rows lie inside it (the tile's row j is table row sy0 + j)
 };
 
 __device__ __forceinline__ T2DFoot t2d_footprint(const Table2DParams& p, int rows_per_wave,
@@ -315,23 +326,30 @@ __device__ __forceinline__ T2DFoot t2d_footprint(const Table2DParams& p, int row
       clampi(static_cast<int>(((clast + 0.5) * f.sx) * f.cx), 0, p.nx - 2) + 1);
   f.ty1 = __builtin_amdgcn_readfirstlane(
       clampi(static_cast<int>(((f.r1 - 1 + 0.5) * f.sy) * f.cy), 0, p.ny - 2) + 1);
+  f.sy0 = f.ty0;
   return f;
+}
+template <int SH>
+__device__ __forceinline__ void t2d_stage_rows(const Table2DParams& p, T2DFoot& f) {
+  f.sy0 = min(f.ty0, p.ny - SH);  // the stream shape needs ny >= SH (table2d_shape)
 }
 
 // kSW consecutive lanes per table row, 2 rows per pass; every pass's load in flight before
-// the LDS writes. Branch-free: a lane outside the footprint loads the corner (its LDS slot is
-// never read), and addresses are a uniform base plus 32-bit offsets.
+// the LDS writes. Branch-free and one lane offset for every pass: SH whole table rows from
+// sy0 (inside the table: t2d_stage_rows), a lane right of the footprint loading its last
+// column again (same cache line; its LDS slot is never read) — each pass's address is a
+// uniform base plus the one 32-bit lane offset, which holds 1 VGPR across the step loop
+// instead of one per pass.
 constexpr int kStageRows = kB / kSW;
 template <int SH>
 __device__ __forceinline__ void t2d_stage_load(const double* table, int nx, const T2DFoot& f,
                                                double (&v)[SH / kStageRows]) {
-  const int w = f.tx1 - f.tx0 + 1, hgt = f.ty1 - f.ty0 + 1;
+  const int w = f.tx1 - f.tx0 + 1;
   const int lx = threadIdx.x % kSW, ly = threadIdx.x / kSW;
-  const double* tb = table + static_cast<size_t>(f.ty0) * nx + f.tx0;
+  const unsigned off = static_cast<unsigned>(ly * nx + min(lx, w - 1)) * 8u;
 #pragma unroll
   for (int j = 0; j < SH / kStageRows; ++j) {
-    const int rr = ly + kStageRows * j;
-    const unsigned off = (lx < w && rr < hgt) ? static_cast<unsigned>(rr * nx + lx) * 8u : 0u;
+    const double* tb = table + static_cast<size_t>(f.sy0 + kStageRows * j) * nx + f.tx0;
     v[j] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(tb) + off);
   }
 }
@@ -345,11 +363,13 @@ __device__ __forceinline__ void t2d_stage_store(const T2DFoot& f, const double (
 #pragma unroll
   for (int j = 0; j < SH / kStageRows; ++j) tile[(ly + kStageRows * j) * kSW + lx] = v[j];
   if constexpr (POISON) {
-    const int w = f.tx1 - f.tx0 + 1, hgt = f.ty1 - f.ty0 + 1;
+    const int w = f.tx1 - f.tx0 + 1;
 #pragma unroll
-    for (int j = 0; j < SH / kStageRows; ++j)
-      if (!(lx < w && ly + kStageRows * j < hgt))
+    for (int j = 0; j < SH / kStageRows; ++j) {
+      const int row = f.sy0 + ly + kStageRows * j;
+      if (!(lx < w && row >= f.ty0 && row <= f.ty1))
         tile[(ly + kStageRows * j) * kSW + lx] = __builtin_nan("");
+    }
   }
 }
 
@@ -390,7 +410,7 @@ __device__ __forceinline__ double t2d_stream_rows(const Table2DParams& p, int ro
   }
   __syncthreads();
   auto line = [&](int j, int b) {  // table row j interpolated at column b's x
-    const double* t = tile + (j - f.ty0) * kSW + col[b];
+    const double* t = tile + (j - f.sy0) * kSW + col[b];
     return fma(t[1] - t[0], fx[b], t[0]);
   };
   double acc[kSCols], lc[kSCols], ln[kSCols], d[kSCols];
@@ -405,7 +425,7 @@ __device__ __forceinline__ double t2d_stream_rows(const Table2DParams& p, int ro
   auto fetch = [&](int j) {
 #pragma unroll
     for (int b = 0; b < kSCols; ++b) {
-      const double* t = tile + (min(j, f.ty1) - f.ty0) * kSW + col[b];
+      const double* t = tile + (min(j, f.ty1) - f.sy0) * kSW + col[b];
       n0[b] = t[0];
       n1[b] = t[1];
     }
@@ -452,7 +472,8 @@ template <int SH, bool POISON, class Between>
 __device__ __forceinline__ double table2d_stream_block(const Table2DParams& p, int rows_per_wave,
                                                        int bx, int by, double* tile, double* red,
                                                        Between between) {
-  const T2DFoot f = t2d_footprint(p, rows_per_wave, bx, by);
+  T2DFoot f = t2d_footprint(p, rows_per_wave, bx, by);
+  t2d_stage_rows<SH>(p, f);
   double v[SH / kStageRows];
   t2d_stage_load<SH>(p.table, p.nx, f, v);
   between();
@@ -497,8 +518,17 @@ __global__ __launch_bounds__(kB) void table2d_stream_kernel(Table2DParams p, int
 // asm every step, so no step's loads or arithmetic can be hoisted or shared.
 // Step phases (kernels.hpp): the grid is nb x phases workgroups; workgroup g runs block
 // g % nb for the steps g / nb, g / nb + phases, ...
+// MIINT_T2D_WAVES (A/B): ask the compiler for that many waves per SIMD (register budget)
+#ifndef MIINT_T2D_WAVES
+#define MIINT_T2D_WAVES 0
+#endif
+#if MIINT_T2D_WAVES > 0
+#define MIINT_T2D_MS_ATTR __attribute__((amdgpu_waves_per_eu(MIINT_T2D_WAVES, 8)))
+#else
+#define MIINT_T2D_MS_ATTR
+#endif
 template <int SH>
-__global__ __launch_bounds__(kB) void table2d_multistep_kernel(Table2DParams p, int rows_per_wave,
+__global__ __launch_bounds__(kB) MIINT_T2D_MS_ATTR void table2d_multistep_kernel(Table2DParams p, int rows_per_wave,
                                                                int gx, double* partials,
                                                                int steps, unsigned nb) {
   __shared__ double tile[SH * kSW];
@@ -507,14 +537,18 @@ __global__ __launch_bounds__(kB) void table2d_multistep_kernel(Table2DParams p, 
   const int phases = static_cast<int>(gridDim.x / nb);
   const int first = static_cast<int>(blockIdx.x / nb);
   const int bx = static_cast<int>(blk) % gx, by = static_cast<int>(blk) / gx;
-  const T2DFoot f = t2d_footprint(p, rows_per_wave, bx, by);
+  T2DFoot f = t2d_footprint(p, rows_per_wave, bx, by);
+  t2d_stage_rows<SH>(p, f);
   // Each step loads its own footprint from a table pointer laundered per step (no step's
   // loads are shared or hoisted). Short tiles (the multi-GPU row slices): step st's loads are
   // issued during step st - 1, before its rows, so their latency hides behind the row loop
   // (1/8 slice 2.20 -> 2.04 us, profiles/r3/t2d_prefetch_ab.jsonl). The full tile keeps
   // loading at the top of its step: holding its 16 loads across the rows takes 139 VGPRs, 3
   // waves per SIMD, and the 4096^2 grid would no longer be resident.
-  constexpr bool kPrefetch = SH <= kSHShort;
+#ifndef MIINT_T2D_PREFETCH_FULL
+#define MIINT_T2D_PREFETCH_FULL 0
+#endif
+  constexpr bool kPrefetch = SH <= kSHShort || MIINT_T2D_PREFETCH_FULL;
   double v[SH / kStageRows];
   auto load = [&] {
     const double* t = p.table;
@@ -530,7 +564,7 @@ __global__ __launch_bounds__(kB) void table2d_multistep_kernel(Table2DParams p, 
     if constexpr (kPrefetch) {
       if (st + phases < steps) load();
     }
-    const double val = t2d_stream_rows<true>(p, rows_per_wave, f, tile, red);
+    const double val = t2d_stream_rows<MIINT_T2D_READ_AHEAD != 0>(p, rows_per_wave, f, tile, red);
     if (threadIdx.x == 0) partials[static_cast<size_t>(st) * nb + blk] = val;
     __syncthreads();  // the next step rewrites tile and red
   }
@@ -613,11 +647,14 @@ Table2DShape table2d_shape(const Table2DParams& p) {
   const int rows = p.row1 - p.row0;
   const int gxs = (p.gx + kWave * kSCols - 1) / (kWave * kSCols);
   Table2DShape sh{};
-  // cells spanned by n samples, + 2 for partial cells at both ends, + 1 for the +1 neighbour
-  auto span = [](int n, double step) { return n * step + 3.0; };
-  if (span(kWave * kSCols, step_x) <= kSW) {
+  // table cells n samples touch: their first and last cells floor(a), floor(a + (n-1) step)
+  // are at most floor((n-1) step) + 1 apart, + 1 for the last one's +1 neighbour (the
+  // 1e-9 guards a product that lands a rounding below an integer)
+  auto span = [](int n, double step) { return std::floor((n - 1) * step + 1e-9) + 3.0; };
+  // (a staged tile is SH whole table rows: the table needs at least that many)
+  if (span(kWave * kSCols, step_x) <= kSW && p.ny >= kSHShort) {
     for (int r : {32, 16, 8, 4}) {
-      if (span(4 * r, step_y) > kSH) continue;
+      if (span(4 * r, step_y) > (p.ny >= kSH ? kSH : kSHShort)) continue;
       const long nwg = static_cast<long>(gxs) * ((rows + 4 * r - 1) / (4 * r));
       sh.stream = true;
       sh.rows_per_wave = r;

@@ -50,7 +50,7 @@ struct Table2DConfig {
   // the same values.
   bool multistep = true;
   // Multi-step step phases (launch_table2d_multistep): workgroups per row-stream block, each
-  // running every phases-th integration of the replay; 0 = auto (kT2MaxPhases, once one
+  // running every phases-th integration of the replay; 0 = auto (kT2AutoPhases, once one
   // phase is resident), 1 = one workgroup per block (round 3's launch)
   int phases = 0;
   // row stream: fewest workgroups its shape aims for (0 = kernel default, 512 — except in a

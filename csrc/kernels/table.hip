@@ -751,7 +751,7 @@ bool table2d_multistep_ok(const Table2DParams& p, int num_cus) {
 
 // Step phases for a launch of `steps`: 0 if not even one phase is resident at once (or the
 // shape is not the row stream); else `want` (an explicit request) or, for want = 0,
-// kT2MaxPhases — both capped by steps.
+// kT2AutoPhases — both capped by steps (and an explicit one by kT2MaxPhases).
 int table2d_multistep_phases(const Table2DParams& p, int num_cus, int steps, int want) {
   check_table2d(p);
   const Table2DShape sh = table2d_shape(p);
@@ -764,14 +764,14 @@ int table2d_multistep_phases(const Table2DParams& p, int num_cus, int steps, int
   // steps / phases steps): 4 phases beat the resident count everywhere measured
   // (profiles/r4/t2d_phases_explicit.jsonl: 4096^2 5.87 / 5.56 / 5.39 / 5.36 us at 1-4 phases
   // with 1 resident; the 1/8 slice 1.92 / 1.48 / 1.49 / 1.45 with 2)
-  return std::min(want > 0 ? want : kT2MaxPhases, std::max(1, steps));
+  return std::min(want > 0 ? std::min(want, kT2MaxPhases) : kT2AutoPhases, std::max(1, steps));
 }
 
 void launch_table2d_multistep(const Table2DParams& p, double* partials, int steps, double* outs,
                               hipStream_t stream, int phases) {
   check_table2d(p);
   MIINT_CHECK(steps >= 1 && steps <= 1024, "table2d multi-step: 1..1024 steps");
-  MIINT_CHECK(phases >= 1 && phases <= kT2MaxPhases, "table2d multi-step: 1..4 step phases");
+  MIINT_CHECK(phases >= 1 && phases <= kT2MaxPhases, "table2d multi-step: 1..kT2MaxPhases step phases");
   const Table2DShape sh = table2d_shape(p);
   MIINT_CHECK(sh.stream, "table2d multi-step runs the row-stream shape only");
   const int nb = static_cast<int>(sh.grid.x * sh.grid.y);

@@ -580,7 +580,7 @@ def test_table2d_multistep_phases_bitwise(native, cuda, g, sl, phases):
 
 
 def test_table2d_multistep_auto_phases(native, cuda):
-    """Auto: kT2MaxPhases (4) step phases on the most rows per wave that fit (16 rows on
+    """Auto: kT2AutoPhases (4) step phases on the most rows per wave that fit (16 rows on
     4096^2: 16 x 8 = 128 blocks for the 1/8 row slice, 16 x 64 for the whole field) — the
     fastest measured (profiles/r4/t2d_slice_shapes.jsonl, t2d_phases_explicit.jsonl) — and
     the same values as one phase."""

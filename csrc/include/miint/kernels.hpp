@@ -227,9 +227,9 @@ const char* table2d_path(const Table2DParams& p);
 // so several steps of one block in flight on different workgroups overlap those latencies.
 // Every partial is still one workgroup's, computed as in the one-phase launch: bitwise the
 // same values. 0 = auto: kT2AutoPhases (<= steps) whenever one phase is resident — past
-// residency the later phases' workgroups start as earlier ones finish, and 4 phases measured
-// fastest on every shape (profiles/r4/t2d_phases_explicit.jsonl).
-constexpr int kT2AutoPhases = 4;   // auto
+// residency the later phases' workgroups start as earlier ones finish, and 8 phases measured
+// fastest on every shape (profiles/r4/t2d_phases_explicit.jsonl, t2d_variant_ab.jsonl).
+constexpr int kT2AutoPhases = 8;   // auto
 constexpr int kT2MaxPhases = 16;  // an explicit request
 bool table2d_multistep_ok(const Table2DParams& p, int num_cus);
 // Multi-step workgroups resident per CU (hipOccupancy; 0 for a shape without the row stream).

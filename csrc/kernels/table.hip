@@ -259,9 +259,13 @@ __global__ __launch_bounds__(kB) void table2d_kernel(Table2DParams p, double* pa
 // counting staging, column setup and the hand-off at 64 samples per lane).
 constexpr int kSCols = 4;                 // columns per lane: a workgroup spans 256 columns
 constexpr int kSW = kWave * kSCols / 2;   // LDS footprint width (cells), 128
-// LDS footprint height (cells). A/B switch MIINT_T2D_SH (even: kStageRows rows per pass).
+// LDS footprint height (cells). 30 rows (30 KB tile): 5 workgroups per CU fit the 160 KB of
+// LDS where 32 rows fit 4, and the 16-row-per-wave block of a 4096^2 field touches at most
+// floor(63 x 0.44) + 3 = 30 table rows. Against 32 (profiles/r4/t2d_variant_ab.jsonl, us per
+// integration at 8 step phases): 4096^2 5.34 -> 5.08, 1/2 slice 2.81 -> 2.64, 1/4 1.63 ->
+// 1.58, 1/8 1.045 -> 1.03. A/B switch MIINT_T2D_SH (even: kStageRows rows per pass).
 #ifndef MIINT_T2D_SH
-#define MIINT_T2D_SH 32
+#define MIINT_T2D_SH 30
 #endif
 constexpr int kSH = MIINT_T2D_SH;
 static_assert(kSH % 2 == 0 && kSH >= 16, "kSH: even, >= the short tile");
@@ -761,9 +765,10 @@ int table2d_multistep_phases(const Table2DParams& p, int num_cus, int steps, int
   const long fit = static_cast<long>(per_cu) * num_cus / nb;
   if (fit < 1) return 0;  // not even one workgroup per block resident: no multi-step
   // Past residency the later phases' workgroups start as earlier ones finish (each runs
-  // steps / phases steps): 4 phases beat the resident count everywhere measured
-  // (profiles/r4/t2d_phases_explicit.jsonl: 4096^2 5.87 / 5.56 / 5.39 / 5.36 us at 1-4 phases
-  // with 1 resident; the 1/8 slice 1.92 / 1.48 / 1.49 / 1.45 with 2)
+  // steps / phases steps): more phases won everywhere measured, up to 8
+  // (profiles/r4/t2d_phases_explicit.jsonl, t2d_variant_ab.jsonl: 4096^2 5.87 / 5.56 / 5.39 /
+  // 5.36 us at 1-4 phases with 1 resident, 5.34 at 8; the 1/8 slice 1.92 / 1.48 / 1.49 /
+  // 1.45, and 1.045 at 8 on 16 rows per wave)
   return std::min(want > 0 ? std::min(want, kT2MaxPhases) : kT2AutoPhases, std::max(1, steps));
 }
 

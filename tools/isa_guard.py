@@ -58,15 +58,16 @@ GUARDED = {
     "ms_train_series": ("riemann", MS + r"0ENS_8TrainVelEE", 0),
     "ms_poly7_series": ("riemann", MS + r"0ENS_4PolyILi7EEE", 0),
     "table2d_stream_0_16": ("table", r"table2d_stream_kernelILi0ELi16ELb0EE", 0),
-    "table2d_stream_0_32": ("table", r"table2d_stream_kernelILi0ELi32ELb0EE", 0),
+    "table2d_stream_0_30": ("table", r"table2d_stream_kernelILi0ELi30ELb0EE", 0),
     "table2d_stream_1_16": ("table", r"table2d_stream_kernelILi1ELi16ELb0EE", 0),
-    "table2d_stream_1_32": ("table", r"table2d_stream_kernelILi1ELi32ELb0EE", 0),
+    "table2d_stream_1_30": ("table", r"table2d_stream_kernelILi1ELi30ELb0EE", 0),
     "table2d_stream_2_16": ("table", r"table2d_stream_kernelILi2ELi16ELb0EE", 0),
-    "table2d_stream_2_32": ("table", r"table2d_stream_kernelILi2ELi32ELb0EE", 0),
-    # the 2-D multi-step kernels: the full tile must keep 4 waves per SIMD (at 3 the 4096^2
-    # grid is no longer resident and the plan falls back to chained replays)
+    "table2d_stream_2_30": ("table", r"table2d_stream_kernelILi2ELi30ELb0EE", 0),
+    # the 2-D multi-step kernels: the 30-row tile must keep 5 waves per SIMD (<= 96 VGPRs at
+    # the 5 workgroups per CU its LDS allows; at 3 the 4096^2 grid would no longer be resident
+    # and the plan would fall back to chained replays)
     "table2d_ms_16": ("table", r"table2d_multistep_kernelILi16EE", 0),
-    "table2d_ms_32": ("table", r"table2d_multistep_kernelILi32EE", 0),
+    "table2d_ms_30": ("table", r"table2d_multistep_kernelILi30EE", 0),
 }
 
 

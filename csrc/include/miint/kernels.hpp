@@ -227,10 +227,11 @@ const char* table2d_path(const Table2DParams& p);
 // so several steps of one block in flight on different workgroups overlap those latencies.
 // Every partial is still one workgroup's, computed as in the one-phase launch: bitwise the
 // same values. 0 = auto: kT2AutoPhases (<= steps) whenever one phase is resident — past
-// residency the later phases' workgroups start as earlier ones finish, and 8 phases measured
-// fastest on every shape (profiles/r4/t2d_phases_explicit.jsonl, t2d_variant_ab.jsonl).
-constexpr int kT2AutoPhases = 8;   // auto
-constexpr int kT2MaxPhases = 16;  // an explicit request
+// residency the later phases' workgroups start as earlier ones finish, and 16 phases measured
+// fastest or level on every shape (profiles/r4/t2d_phases_explicit.jsonl, t2d_variant_ab.jsonl,
+// t2d_shape_sweep.jsonl).
+constexpr int kT2AutoPhases = 16;  // auto
+constexpr int kT2MaxPhases = 32;  // an explicit request (32: one step per workgroup)
 bool table2d_multistep_ok(const Table2DParams& p, int num_cus);
 // Multi-step workgroups resident per CU (hipOccupancy; 0 for a shape without the row stream).
 int table2d_multistep_resident(const Table2DParams& p);

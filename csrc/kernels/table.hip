@@ -765,10 +765,10 @@ int table2d_multistep_phases(const Table2DParams& p, int num_cus, int steps, int
   const long fit = static_cast<long>(per_cu) * num_cus / nb;
   if (fit < 1) return 0;  // not even one workgroup per block resident: no multi-step
   // Past residency the later phases' workgroups start as earlier ones finish (each runs
-  // steps / phases steps): more phases won everywhere measured, up to 8
-  // (profiles/r4/t2d_phases_explicit.jsonl, t2d_variant_ab.jsonl: 4096^2 5.87 / 5.56 / 5.39 /
-  // 5.36 us at 1-4 phases with 1 resident, 5.34 at 8; the 1/8 slice 1.92 / 1.48 / 1.49 /
-  // 1.45, and 1.045 at 8 on 16 rows per wave)
+  // steps / phases steps): more phases won or tied everywhere measured, up to 16
+  // (profiles/r4/t2d_phases_explicit.jsonl, t2d_variant_ab.jsonl, t2d_shape_sweep.jsonl, us
+  // per integration; 4096^2: 5.87 / 5.56 / 5.39 / 5.36 at 1-4 phases on 32-row tiles, 5.13 /
+  // 5.07 at 8 / 16 on 30-row tiles; the 1/8 slice 1.92 / 1.48 / 1.49 / 1.45, then 1.01 / 0.97)
   return std::min(want > 0 ? std::min(want, kT2MaxPhases) : kT2AutoPhases, std::max(1, steps));
 }
 

@@ -562,7 +562,7 @@ def test_table2d_multistep_equals_chained(native, cuda, g, sl):
 
 @pytest.mark.parametrize("g,sl", [(4096, (0, 8)), (4096, (5, 8)), (4096, (1, 4)), (4095, (0, 2)),
                                   (5000, (3, 8))])
-@pytest.mark.parametrize("phases", [2, 3, 4])
+@pytest.mark.parametrize("phases", [2, 3, 4, 16, 32])
 def test_table2d_multistep_phases_bitwise(native, cuda, g, sl, phases):
     """Step phases: several workgroups per row-stream block, each running every phases-th
     integration of the replay (32 integrations: 2, 3 and 4 phases, the last leaving 2 steps
@@ -580,14 +580,14 @@ def test_table2d_multistep_phases_bitwise(native, cuda, g, sl, phases):
 
 
 def test_table2d_multistep_auto_phases(native, cuda):
-    """Auto: kT2AutoPhases (8) step phases on the most rows per wave that fit (16 rows on
+    """Auto: kT2AutoPhases (16) step phases on the most rows per wave that fit (16 rows on
     4096^2: 16 x 8 = 128 blocks for the 1/8 row slice, 16 x 64 for the whole field) — the
     fastest measured (profiles/r4/t2d_slice_shapes.jsonl, t2d_phases_explicit.jsonl) — and
     the same values as one phase."""
     p = native.Table2DPlan(4096, 1800.0, 0, None, True, True, 1, 0, 8)
-    assert p.multistep and p.phases == 8 and p.min_wg == 1 and p.workgroups == 128
+    assert p.multistep and p.phases == 16 and p.min_wg == 1 and p.workgroups == 128
     full = native.Table2DPlan(4096)
-    assert full.multistep and full.phases == 8 and full.workgroups == 1024
+    assert full.multistep and full.phases == 16 and full.workgroups == 1024
     one = native.Table2DPlan(4096, phases=1)
     full.time(full.graph_steps, True)
     one.time(one.graph_steps, True)

@@ -339,22 +339,28 @@ __device__ __forceinline__ void t2d_stage_rows(const Table2DParams& p, T2DFoot& 
 }
 
 // kSW consecutive lanes per table row, 2 rows per pass; every pass's load in flight before
-// the LDS writes. Branch-free and one lane offset for every pass: SH whole table rows from
+// the LDS writes. Branch-free, and one lane offset for every pass: SH whole table rows from
 // sy0 (inside the table: t2d_stage_rows), a lane right of the footprint loading its last
-// column again (same cache line; its LDS slot is never read) — each pass's address is a
-// uniform base plus the one 32-bit lane offset, which holds 1 VGPR across the step loop
-// instead of one per pass.
+// column again (same cache line; its LDS slot is never read). Buffer loads: the table's
+// resource in SGPRs, the one lane offset in a VGPR and each pass's row offset in an SGPR
+// (soffset) — no per-pass address arithmetic on the VALU and no per-pass address VGPRs (a
+// global / flat load would take a 64-bit VGPR address per pass: 15 v_lshl_add_u64 and 30
+// VGPRs a step).
 constexpr int kStageRows = kB / kSW;
+// buffer resource word 3 on gfx9 (CDNA): raw (untyped) access, 32-bit data format
+constexpr int kBufferRsrcWord3 = 0x00020000;
 template <int SH>
-__device__ __forceinline__ void t2d_stage_load(const double* table, int nx, const T2DFoot& f,
-                                               double (&v)[SH / kStageRows]) {
+__device__ __forceinline__ void t2d_stage_load(const double* table, int nx, int ny,
+                                               const T2DFoot& f, double (&v)[SH / kStageRows]) {
   const int w = f.tx1 - f.tx0 + 1;
   const int lx = threadIdx.x % kSW, ly = threadIdx.x / kSW;
   const unsigned off = static_cast<unsigned>(ly * nx + min(lx, w - 1)) * 8u;
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<double*>(table), static_cast<short>(0), nx * ny * 8, kBufferRsrcWord3);
 #pragma unroll
   for (int j = 0; j < SH / kStageRows; ++j) {
-    const double* tb = table + static_cast<size_t>(f.sy0 + kStageRows * j) * nx + f.tx0;
-    v[j] = *reinterpret_cast<const double*>(reinterpret_cast<const char*>(tb) + off);
+    const int soff = ((f.sy0 + kStageRows * j) * nx + f.tx0) * 8;
+    v[j] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rsrc, off, soff, 0));
   }
 }
 
@@ -479,7 +485,7 @@ __device__ __forceinline__ double table2d_stream_block(const Table2DParams& p, i
   T2DFoot f = t2d_footprint(p, rows_per_wave, bx, by);
   t2d_stage_rows<SH>(p, f);
   double v[SH / kStageRows];
-  t2d_stage_load<SH>(p.table, p.nx, f, v);
+  t2d_stage_load<SH>(p.table, p.nx, p.ny, f, v);
   between();
   t2d_stage_store<SH, POISON>(f, v, tile);
   return t2d_stream_rows(p, rows_per_wave, f, tile, red);
@@ -557,7 +563,7 @@ __global__ __launch_bounds__(kB) MIINT_T2D_MS_ATTR void table2d_multistep_kernel
   auto load = [&] {
     const double* t = p.table;
     asm volatile("" : "+s"(t));  // a fresh pointer every step (no instructions)
-    t2d_stage_load<SH>(t, p.nx, f, v);
+    t2d_stage_load<SH>(t, p.nx, p.ny, f, v);
   };
   if constexpr (kPrefetch) {
     if (first < steps) load();
@@ -687,6 +693,8 @@ const char* table2d_path(const Table2DParams& p) {
 
 static void check_table2d(const Table2DParams& p) {
   MIINT_CHECK(p.nx >= 2 && p.ny >= 2 && p.gx >= 1 && p.gy >= 1, "table2d dims");
+  // the row stream's buffer loads address the table with 32-bit byte offsets
+  MIINT_CHECK(static_cast<long long>(p.nx) * p.ny * 8 < (1LL << 31), "table2d: table over 2 GB");
   MIINT_CHECK(p.row0 >= 0 && p.row1 <= p.gy && p.row0 < p.row1, "table2d row range");
 }
 

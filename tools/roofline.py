@@ -14,7 +14,15 @@ For every (workload, kernel) whose median dispatch is at least --min-us long:
                  streaming kernel reaches, profiles/r1 and r2 trainscan rows), when collected
   sol            max(bounds) / measured median dispatch time: the fraction of the tighter
                  roofline the kernel reaches
-  valu_per_sample, when the workload's sample count is known (Riemann workloads: 1e9)
+  valu_per_sample, when the workload's sample count is known (Riemann workloads: 1e9; the
+                 2-D multi-step dispatch runs 32 integrations of its field)
+  clock_ghz      GRBM_GUI_ACTIVE / 8 XCDs / measured median: the shader clock the dispatch
+                 actually ran at (the counter sums the 8 XCDs' busy cycles; its window runs a
+                 few us past the dispatch, so only dispatches >= 500 us get a clock)
+  valu_at_clock  the VALU bound priced at that clock / measured: issue efficiency with the
+                 clock taken out (packed-fp32 kernels run at ~2.1 GHz under the power limit
+                 where fp64 runs at ~2.3: at 2.4 GHz pricing they look 10 points worse than
+                 their issue rate is)
 Counters of one workload come from several runs (one counter group each); per counter the
 median over that workload's dispatches of the kernel is used.
 """
@@ -87,8 +95,8 @@ def main() -> None:
     a = ap.parse_args()
     ctr, dur = collect(a.root)
     print("| workload | kernel | median us | VALU insts | VALU/sample | VALU bound us | "
-          "HBM bytes | HBM bound us | speed of light |")
-    print("|---|---|---|---|---|---|---|---|---|")
+          "HBM bytes | HBM bound us | speed of light | clock GHz | VALU issue at that clock |")
+    print("|---|---|---|---|---|---|---|---|---|---|---|")
     for (w, kname), cs in sorted(ctr.items()):
         if "rocclr" in kname or not dur[(w, kname)]:
             continue
@@ -105,14 +113,20 @@ def main() -> None:
             nbytes = (med.get("FETCH_SIZE", 0.0) + med.get("WRITE_SIZE", 0.0)) * 1024
         hb = nbytes / HBM_BPS * 1e6 if nbytes else None
         bound = max(b for b in (vb, hb, 0.0) if b is not None)
-        per = f"{valu * 64 / SAMPLES[w]:.2f}" if valu and w in SAMPLES else "—"
+        samples = SAMPLES.get(w, 0) * (32 if w.startswith("table2d") and "multistep" in kname else 1)
+        per = f"{valu * 64 / samples:.2f}" if valu and samples else "—"
+        grbm = med.get("GRBM_GUI_ACTIVE")
+        # the counter window spans a few us past the dispatch: only long dispatches give a clock
+        ghz = grbm / 8 / (t_us * 1e-6) / 1e9 if grbm and t_us >= 500 else None
+        at_clock = (f"{vb * CLOCK_HZ / (ghz * 1e9) / t_us:.0%}" if ghz and vb else "—")
+        tail = f" {'—' if ghz is None else f'{ghz:.2f}'} | {at_clock} |"
         print(f"| {w} | `{kname}` | {t_us:.1f} | {valu:.3g} | {per} | "
               f"{vb:.1f} | {'—' if nbytes is None else f'{nbytes:.3g}'} | "
-              f"{'—' if hb is None else f'{hb:.1f}'} | {bound / t_us:.0%} |"
+              f"{'—' if hb is None else f'{hb:.1f}'} | {bound / t_us:.0%} |" + tail
               if valu else
               f"| {w} | `{kname}` | {t_us:.1f} | — | — | — | "
               f"{'—' if nbytes is None else f'{nbytes:.3g}'} | {'—' if hb is None else f'{hb:.1f}'} | "
-              f"{bound / t_us:.0%} |")
+              f"{bound / t_us:.0%} |" + tail)
 
 
 if __name__ == "__main__":

@@ -217,6 +217,14 @@ int table2d_grid(const Table2DParams& p);
 // Which kernel a launch runs: "stream" (LDS footprint + row streaming, fine grids) or
 // "tile" (coarse grids, table read from global memory).
 const char* table2d_path(const Table2DParams& p);
+// The launch shape table2d_* pick (host only; tests check the footprint bound against it):
+// row stream or tile, rows per wave, staged tile rows (kSH or the short tile), tile width,
+// grid, and for the tile kernel its square size.
+struct Table2DShapeInfo {
+  bool stream;
+  int rows_per_wave, tile_rows, tile_cols, grid_x, grid_y, tile;
+};
+Table2DShapeInfo table2d_shape_info(const Table2DParams& p);
 // Multi-step row stream: `steps` integrations in one launch of resident workgroups, then one
 // closing kernel: outs[s] = integration s, bitwise the chained / fused value. `partials`
 // holds steps x table2d_grid(p) doubles. Only for launches table2d_multistep_ok accepts (the

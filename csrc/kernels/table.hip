@@ -686,6 +686,13 @@ int table2d_grid(const Table2DParams& p) {
   return static_cast<int>(sh.grid.x * sh.grid.y);
 }
 
+Table2DShapeInfo table2d_shape_info(const Table2DParams& p) {
+  const Table2DShape sh = table2d_shape(p);
+  return {sh.stream, sh.stream ? sh.rows_per_wave : 0,
+          sh.stream ? (sh.short_tile ? kSHShort : kSH) : 0, sh.stream ? kSW : 0,
+          static_cast<int>(sh.grid.x), static_cast<int>(sh.grid.y), sh.stream ? 0 : sh.tile};
+}
+
 const char* table2d_path(const Table2DParams& p) {
   const Table2DShape sh = table2d_shape(p);
   return sh.stream ? "stream" : "tile";

@@ -417,6 +417,20 @@ PYBIND11_MODULE(_miint, m) {
     Table2DParams p{nullptr, nx, ny, X, Y, gx, gy, row0, row1};
     return std::string(table2d_path(p));
   });
+  m.def("table2d_shape_info", [](int nx, int ny, double X, double Y, int gx, int gy, int row0,
+                                 int row1, int min_wg) {
+    Table2DParams p{nullptr, nx, ny, X, Y, gx, gy, row0, row1, min_wg};
+    const Table2DShapeInfo i = table2d_shape_info(p);
+    py::dict d;
+    d["stream"] = i.stream;
+    d["rows_per_wave"] = i.rows_per_wave;
+    d["tile_rows"] = i.tile_rows;
+    d["tile_cols"] = i.tile_cols;
+    d["grid"] = py::make_tuple(i.grid_x, i.grid_y);
+    d["tile"] = i.tile;
+    return d;
+  }, py::arg("nx"), py::arg("ny"), py::arg("X"), py::arg("Y"), py::arg("gx"), py::arg("gy"),
+     py::arg("row0"), py::arg("row1"), py::arg("min_wg") = 0);
   m.def("launch_table2d_partials", [](uintptr_t table, int nx, int ny, double X, double Y, int gx,
                                       int gy, int row0, int row1, uintptr_t partials, uintptr_t s) {
     Table2DParams p{ptr<const double>(table), nx, ny, X, Y, gx, gy, row0, row1};

@@ -593,8 +593,9 @@ def single_shot(ctx, kw, args, pipeline, dev, reps: int = 50) -> dict:
     fused launch whose last workgroup stores the value straight into pinned host memory), and
     RiemannPlan.time_one_shot times four forms in C++: direct (fused launch + stream sync),
     direct_poll (the same launch, the host spinning on the pinned result word), graph /
-    graph_poll (a captured 1-step batch replayed). Several GPUs: one step per call through
-    the rank's collective plan (barrier, launch, all-reduce, copy, sync), slowest rank."""
+    graph_poll (a captured 1-step batch replayed). Several GPUs (or --force-collective): one
+    step per call through the rank's collective plan (barrier, launch, all-reduce, copy,
+    sync), slowest rank."""
     import torch
 
     from cuda_v_mpi_amd import Integrator
@@ -602,7 +603,7 @@ def single_shot(ctx, kw, args, pipeline, dev, reps: int = 50) -> dict:
     n1 = 10**9
     want = pi4_expected_abs_err(args.rule, n1)
     rec: dict = {"N": n1, "reps": reps, "n_gpus": ctx.world, "forms": {}}
-    if ctx.world == 1:
+    if ctx.world == 1 and not args.force_collective:
         one = Integrator("pi4", n=n1, div=args.div, **dict(kw, dtype="fp64", multistep=False))
         p = one.plan
         rec["grid"] = p.grid

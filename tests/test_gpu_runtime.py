@@ -433,6 +433,7 @@ def test_bench_force_collective_graph(native, cuda, bucket):
     assert p.returncode == 0, p.stderr[-2000:]
     js = json.loads(p.stdout.strip().splitlines()[-1])
     bad = [k for k, v in js.items() if isinstance(v, dict) and v.get("verified") is False]
+    assert "extras_error" not in js, js["extras_error"]
     assert js["verified"] and not bad, bad
     assert js["config"]["graphs"] and js["config"]["pipeline"]
     assert js["config"]["bucketed_allreduce"] == bucket

@@ -11,7 +11,7 @@ mkdir -p "$(dirname "$out")"
 : > "$out"
 for rep in 1 2; do
   for slice in "" 0/2 0/4 0/8; do
-    for ph in 4 8; do
+    for ph in ${PHASES:-4 8}; do
       for dir in "$@"; do
         extra=(); [ -n "$slice" ] && extra=(--slice "$slice")
         line=$(timeout -k 10 60 "$dir/miint" table2d --grid 4096 --iters 640 --phases $ph "${extra[@]}" | grep '^{' | tail -1) || {

@@ -269,10 +269,6 @@ constexpr int kSW = kWave * kSCols / 2;   // LDS footprint width (cells), 128
 #endif
 constexpr int kSH = MIINT_T2D_SH;
 static_assert(kSH % 2 == 0 && kSH >= 16, "kSH: even, >= the short tile");
-// A/B: every table-row change computes both lines afresh (no carried next line)
-#ifndef MIINT_T2D_FRESH_LINES
-#define MIINT_T2D_FRESH_LINES 0
-#endif
 // the multi-step row loop's LDS read-ahead (t2d_stream_rows<true>); A/B switch
 #ifndef MIINT_T2D_READ_AHEAD
 #define MIINT_T2D_READ_AHEAD 1
@@ -448,11 +444,7 @@ __device__ __forceinline__ double t2d_stream_rows(const Table2DParams& p, int ro
     const int iy = __builtin_amdgcn_readlane(iyl, k);
     const double fy = readlane_f64(fyl, k);
     if (iy != cur) {  // wave-uniform
-#if MIINT_T2D_FRESH_LINES
-      if (false) {
-#else
       if (iy == cur + 1) {
-#endif
 #pragma unroll
         for (int b = 0; b < kSCols; ++b) {
           lc[b] = ln[b];

@@ -783,7 +783,9 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
     #     the all-fp32 variant is measured in profiles/r3/fp32_accum.jsonl)
     if pi4 and args.dtype == "fp64":
         f32 = Integrator("pi4", n=n_total, div=args.div, **dict(kw, dtype="fp32"))
-        steps = 40
+        # two full 48-step batches: a batch's fixed cost (~28 us: launch, ramp, tail, close,
+        # syncs; profiles/r4/replay_overhead.jsonl) is 1.8 % of a 40-step fp32 batch
+        steps = 96
         ms = _timed_steps(ctx, f32.plan, steps, pipeline, dev)
         v = f32.plan.host_result(f32.plan.host_index_of(steps - 1, True))
         ref = integ.plan.host_result(integ.plan.host_index_of(0, True))

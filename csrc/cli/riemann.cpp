@@ -329,9 +329,16 @@ int main(int argc, char** argv) {
         double shot = 0.0;
         if (!a.flag("no-one-shot")) {
           if (!plan.collective()) {
-            // 400 settling calls first: from idle the clocks take ~250 calls to settle
-            shot = plan.time_one_shot(50, plan.direct() ? "direct_poll" : "direct", 400)
-                       .median_us * 1e-3;
+            // 400 settling calls first: from idle the clocks take ~250 calls to settle. A
+            // 1-step graph replay with the host polling the pinned result: the fastest form
+            // (profiles/r4/one_shot_grid_settled.jsonl: 78.4-79 us against 80.1 direct_poll)
+            try {
+              shot = plan.time_one_shot(50, plan.direct() ? "graph_poll" : "direct", 400)
+                         .median_us * 1e-3;
+            } catch (const Error&) {  // no 1-step graph for this plan: the direct launch
+              shot = plan.time_one_shot(50, plan.direct() ? "direct_poll" : "direct", 400)
+                         .median_us * 1e-3;
+            }
           } else {
             std::vector<double> v1;
             for (int k = 0; k < 10; ++k) v1.push_back(plan.run_steps(1, true, false).wall_s * 1e3);

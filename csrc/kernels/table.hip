@@ -778,7 +778,12 @@ int table2d_multistep_phases(const Table2DParams& p, int num_cus, int steps, int
   const int per_cu = sh.short_tile ? t2d_ms_per_cu<kSHShort>() : t2d_ms_per_cu<kSH>();
   const long nb = static_cast<long>(sh.grid.x) * sh.grid.y;
   const long fit = static_cast<long>(per_cu) * num_cus / nb;
-  if (fit < 1) return 0;  // not even one workgroup per block resident: no multi-step
+#ifndef MIINT_T2D_MS_ANY
+#define MIINT_T2D_MS_ANY 0
+#endif
+  // not even one workgroup per block resident: no multi-step (A/B MIINT_T2D_MS_ANY: the
+  // kernel's workgroups never wait on each other, so a launch past residency is still correct)
+  if (fit < 1 && !MIINT_T2D_MS_ANY) return 0;
   // Past residency the later phases' workgroups start as earlier ones finish (each runs
   // steps / phases steps): more phases won or tied everywhere measured, up to 16
   // (profiles/r4/t2d_phases_explicit.jsonl, t2d_variant_ab.jsonl, t2d_shape_sweep.jsonl, us

@@ -225,19 +225,18 @@ struct Table2DShapeInfo {
   int rows_per_wave, tile_rows, tile_cols, grid_x, grid_y, tile;
 };
 Table2DShapeInfo table2d_shape_info(const Table2DParams& p);
-// Multi-step row stream: `steps` integrations in one launch of resident workgroups, then one
-// closing kernel: outs[s] = integration s, bitwise the chained / fused value. `partials`
-// holds steps x table2d_grid(p) doubles. Only for launches table2d_multistep_ok accepts (the
-// row-stream shape, every workgroup resident at once on num_cus CUs).
+// Multi-step row stream: `steps` integrations in one launch, then one closing kernel:
+// outs[s] = integration s, bitwise the chained / fused value. `partials` holds steps x
+// table2d_grid(p) doubles. Only for launches table2d_multistep_ok accepts (the row-stream
+// shape; residency is not required: no workgroup waits on another).
 // Step phases: the launch holds `phases` workgroups per row-stream block, workgroup phase f
 // running the steps s = f, f + phases, ... of its block — steps are independent, and a block
 // step is latency-bound (staging, a short row loop, the block reduction) at 2 waves per SIMD,
 // so several steps of one block in flight on different workgroups overlap those latencies.
 // Every partial is still one workgroup's, computed as in the one-phase launch: bitwise the
-// same values. 0 = auto: kT2AutoPhases (<= steps) whenever one phase is resident — past
-// residency the later phases' workgroups start as earlier ones finish, and 16 phases measured
-// fastest or level on every shape (profiles/r4/t2d_phases_explicit.jsonl, t2d_variant_ab.jsonl,
-// t2d_shape_sweep.jsonl).
+// same values. 0 = auto: kT2AutoPhases (<= steps) — past residency the later phases'
+// workgroups start as earlier ones finish, and 16 phases measured fastest or level on every
+// shape (profiles/r4/t2d_phases_explicit.jsonl, t2d_variant_ab.jsonl, t2d_shape_sweep.jsonl).
 constexpr int kT2AutoPhases = 16;  // auto
 constexpr int kT2MaxPhases = 32;  // an explicit request (32: one step per workgroup)
 bool table2d_multistep_ok(const Table2DParams& p, int num_cus);

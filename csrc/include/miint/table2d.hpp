@@ -46,12 +46,12 @@ struct Table2DConfig {
   int step_streams = 0;
   // Chained graph timing as ONE multi-step launch of resident workgroups for the replay's
   // kGraphSteps integrations plus one closing kernel (launch_table2d_multistep): one launch
-  // ramp and tail per replay. Used when the row-stream shape fits the GPU at once; bitwise
-  // the same values.
+  // ramp and tail per replay. Used for every row-stream shape (resident or not); bitwise the
+  // same values.
   bool multistep = true;
   // Multi-step step phases (launch_table2d_multistep): workgroups per row-stream block, each
-  // running every phases-th integration of the replay; 0 = auto (kT2AutoPhases, once one
-  // phase is resident), 1 = one workgroup per block (round 3's launch)
+  // running every phases-th integration of the replay; 0 = auto (kT2AutoPhases), 1 = one
+  // workgroup per block (round 3's launch)
   int phases = 0;
   // row stream: fewest workgroups its shape aims for (0 = kernel default, 512 — except in a
   // multi-step plan, whose step phases supply the parallelism: there 0 means the most rows

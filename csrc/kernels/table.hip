@@ -768,22 +768,16 @@ bool table2d_multistep_ok(const Table2DParams& p, int num_cus) {
   return table2d_multistep_phases(p, num_cus, 1) >= 1;
 }
 
-// Step phases for a launch of `steps`: 0 if not even one phase is resident at once (or the
-// shape is not the row stream); else `want` (an explicit request) or, for want = 0,
-// kT2AutoPhases — both capped by steps (and an explicit one by kT2MaxPhases).
+// Step phases for a launch of `steps`: 0 if the shape is not the row stream; else `want` (an
+// explicit request) or, for want = 0, kT2AutoPhases — both capped by steps (and an explicit
+// one by kT2MaxPhases). Residency is not required: the kernel's workgroups never wait on each
+// other, and past it the multi-step replay still beats chained launches
+// (profiles/r4/t2d_ms_any_ab.jsonl: 6144^2 10.5 -> 9.15 us, 8192^2 13.3 -> 12.2 us, where
+// not one phase is resident).
 int table2d_multistep_phases(const Table2DParams& p, int num_cus, int steps, int want) {
   check_table2d(p);
-  const Table2DShape sh = table2d_shape(p);
-  if (!sh.stream) return 0;
-  const int per_cu = sh.short_tile ? t2d_ms_per_cu<kSHShort>() : t2d_ms_per_cu<kSH>();
-  const long nb = static_cast<long>(sh.grid.x) * sh.grid.y;
-  const long fit = static_cast<long>(per_cu) * num_cus / nb;
-#ifndef MIINT_T2D_MS_ANY
-#define MIINT_T2D_MS_ANY 0
-#endif
-  // not even one workgroup per block resident: no multi-step (A/B MIINT_T2D_MS_ANY: the
-  // kernel's workgroups never wait on each other, so a launch past residency is still correct)
-  if (fit < 1 && !MIINT_T2D_MS_ANY) return 0;
+  (void)num_cus;
+  if (!table2d_shape(p).stream) return 0;
   // Past residency the later phases' workgroups start as earlier ones finish (each runs
   // steps / phases steps): more phases won or tied everywhere measured, up to 16
   // (profiles/r4/t2d_phases_explicit.jsonl, t2d_variant_ab.jsonl, t2d_shape_sweep.jsonl, us

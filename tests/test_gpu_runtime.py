@@ -600,11 +600,20 @@ def test_table2d_multistep_auto_phases(native, cuda):
                               min_wg=512).workgroups == 512
 
 
-def test_table2d_multistep_needs_residency(native, cuda):
-    """8192^2 in one piece needs more row-stream workgroups than the GPU holds at once: the
-    plan keeps chained launches (a persistent launch must be resident as a whole)."""
+def test_table2d_multistep_past_residency(native, cuda):
+    """8192^2 in one piece: more row-stream workgroups than the GPU holds at once. The
+    multi-step replay needs no residency (no workgroup waits on another): the plan runs it,
+    and every value is bitwise the chained replay's at the same shape."""
     p = native.Table2DPlan(8192, 1800.0, 0, None, True, True, 0)
-    assert not p.multistep and p.step_streams == 2
+    assert p.multistep and p.phases == 16 and p.step_streams == 1
+    assert p.workgroups > p.resident_per_cu * native.device_info(0)["num_cus"]
+    c = native.Table2DPlan(8192, 1800.0, 0, None, True, True, 1, multistep=False,
+                           min_wg=p.min_wg)
+    assert not c.multistep and c.workgroups == p.workgroups
+    p.time(p.graph_steps, True)
+    c.time(c.graph_steps, True)
+    assert p.last_result() == c.last_result()
+    assert abs(p.last_result() - native.table2d_oracle(8192)) <= 1e-12 * native.table2d_oracle(8192)
 
 
 @pytest.mark.parametrize("graphs", [False, True])

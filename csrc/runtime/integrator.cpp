@@ -243,10 +243,10 @@ void RiemannPlan::enqueue_chain_streams(hipStream_t cs, int nsteps) {
 
 void RiemannPlan::enqueue_batch(hipStream_t cs, hipStream_t rs, int nsteps, bool overlap) {
   if (chained()) {
-    if (multistep_ && nsteps == 1)
+    if (nsteps == 1)
       // a 1-step batch (a one-shot graph, a remainder): the fused launch, one kernel instead
-      // of a 1-step persistent launch + its close kernel (the same partials, the same order:
-      // bitwise the same value; one-shot graph replay 80.3 -> ~78 us)
+      // of a 1-step persistent launch + its close kernel, or a chained launch + its finalize
+      // (the same partials, the same order: bitwise the same value)
       launch_riemann_fused(params_, cfg_.dtype, cfg_.div, shape_, table_.get(),
                            static_cast<int>(cfg_.table.size()), slots_.get(), ticket_.get(),
                            scale_, result_ptr(0), cs);

@@ -1,14 +1,16 @@
 #!/usr/bin/env python3
-"""Headline benchmark: Riemann subintervals/s of 4/(1+x^2) on [0,1], N=1e9 fp64 per GPU.
+"""Headline benchmark: Riemann subintervals/s of 4/(1+x^2) on [0,1], N=1e9 fp64.
 
 Metric and config come from BASELINE.json ("Riemann subintervals/sec at N=1e9 fp64; |error|
-vs analytic pi"). One step = one complete integration of N samples per GPU: gfx950 kernel
-(every sample evaluated, fp64) -> in-kernel DPP/LDS reduction -> RCCL all-reduce of the
-per-GPU partial over xGMI -> D2H into pinned memory. Steps are hipGraph replays of batches
-of --slots (48) steps plus one replay of a remainder-sized batch (every graph is captured
-before the warmup, so the timed region only replays); with >1 GPU each batch ends in ONE
-all-reduce of its step results (bucketed: every step still gets its own global sum;
---no-bucket = one 8-byte all-reduce per step, overlapped on a side stream).
+vs analytic pi"). One step = one complete integration of N = 1e9 samples IN TOTAL, split over
+the G GPUs as the reference splits its fixed STEPS over its workers (riemann.cpp:10,71-73:
+strong scaling, so the record at every G is the metric's own config): gfx950 kernel (every
+sample evaluated, fp64) -> in-kernel DPP/LDS reduction -> RCCL all-reduce of the per-GPU
+partial over xGMI -> D2H into pinned memory. Steps are hipGraph replays of batches of --slots
+(48) steps plus one replay of a remainder-sized batch (every graph is captured before the
+warmup, so the timed region only replays); with >1 GPU each batch ends in ONE all-reduce of its
+step results (bucketed: every step still gets its own global sum; --no-bucket = one 8-byte
+all-reduce per step, overlapped on a side stream).
 
 Launch (the reference's `mpirun -np P ./riemann`, riemann.cpp:62-86: one command, P ranks,
 one gathered result):
@@ -25,28 +27,27 @@ Warmup: the W warmup steps, then untimed repeats of the timed K-step pattern for
 --settle-ms (60) so the timed region starts at steady clocks (from idle the GPU ramps from
 ~90 to 76.8 us per step over ~25 ms); the JSON line reports those as "warmup_settle_steps".
 
-Weak scaling: every GPU integrates its own 1e9-sample slice of a global N = 1e9 x n_gpus
-(N = 8e9 on 8 GPUs). The results of the last batch of timed steps (every rank holds the
-global sums) are checked on the host against the rule's closed-form truncation error. After
-the timed region (outside it) the same ranks also measure, each with its own graphs, timing
-and pass/fail ("verified"): the metric's own config, N = 1e9 IN TOTAL split over the GPUs as
-the reference splits its fixed STEPS over its workers ("strong_1e9", riemann.cpp:10,71-73);
-the same config with IEEE division per sample ("ieee_div"); the series path's per-point
-error against IEEE division on a 64 K-sample window ("per_point"); and the other BASELINE
-configs: #1, the serial CPU sum at N = 1e6 on one host thread ("baseline1_serial_cpu_1e6");
-#3, N = 1e10 in total strong-scaled over the same GPUs ("baseline3_strong_1e10"); #4, the
-same integral through the packed-fp32 path ("baseline4_fp32", tile values folded in fp64,
-and "baseline4_fp32_accum32", fp32 accumulation to the workgroup partial); #5, the 4096^2
-2-D velocity field with its rows split over the same GPUs ("baseline5_table2d_4096") — and
-the same integral on the node's host cores (the native host engine, the reference's own
-CPU/MPI side: "host_engine"). Also: one integration per call, launch to pinned result, the
-reference's own timing unit ("single_shot_1e9"); the headline config with the series'
-residuals at their own precision ("series_exact_div": per point as accurate as IEEE division,
-+37 % time); and the reference's own integrands through the same batches ("integrand_sin",
-"integrand_train", "integrand_table", "integrand_poly"). The record's "verified" is the AND of
-the headline's, every extra's and the RCCL transport check ("transport_verified": ranks of one
-node on distinct GPUs must not meet over a network transport); the exit status follows the
-headline's.
+Scaling: the headline is strong (N = 1e9 in total; --scaling weak makes --samples a per-GPU
+count instead). The results of the last batch of timed steps (every rank holds the global
+sums) are checked on the host against the rule's closed-form truncation error. After the timed
+region (outside it) the same ranks also measure, each with its own graphs, timing and
+pass/fail ("verified"): the weak-scaling form, 1e9 samples PER GPU (N = 1e9 x G,
+"weak_1e9_per_gpu"); the same config with IEEE division per sample ("ieee_div"); the series
+path's per-point error against IEEE division on a 64 K-sample window ("per_point"); and the
+other BASELINE configs: #1, the serial CPU sum at N = 1e6 on one host thread
+("baseline1_serial_cpu_1e6"); #3, N = 1e10 in total strong-scaled over the same GPUs
+("baseline3_strong_1e10"); #4, the same integral through the packed-fp32 path
+("baseline4_fp32", tile values folded in fp64, and "baseline4_fp32_accum32", fp32 accumulation
+to the workgroup partial); #5, the 4096^2 2-D velocity field with its rows split over the same
+GPUs ("baseline5_table2d_4096") — and the same integral on the node's host cores (the native
+host engine, the reference's own CPU/MPI side: "host_engine"). Also: one integration per call,
+launch to pinned result, the reference's own timing unit ("single_shot_1e9"); the headline
+config with the series' residuals at their own precision ("series_exact_div"); and the
+reference's own integrands through the same batches ("integrand_sin", "integrand_train",
+"integrand_table", "integrand_poly"). The record's "verified" is the AND of the headline's,
+every extra's and the RCCL transport check ("transport_verified": ranks of one node on distinct
+GPUs must be SEEN to meet over xGMI peer-to-peer; a network transport or no transport evidence
+at all fails it); the exit status follows the headline's.
 
 One RCCL communicator per rank: with --comm native (default) the torch process group is gloo
 and carries only the control plane (barriers, the settle-count MAX, the per-rank times); the
@@ -84,8 +85,10 @@ def parse(argv=None) -> argparse.Namespace:
                         "for at least this long so the timed steps run at steady clocks (0 = off)")
     # (--n is a prefix of torchrun's own --nnodes/--nproc-per-node: use --samples under torchrun)
     p.add_argument("--samples", "--n", dest="n", type=float, default=1e9,
-                   help="samples per GPU (weak) or total (strong)")
-    p.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+                   help="samples in total (strong, the default: the metric's N = 1e9 split "
+                        "over the GPUs) or per GPU (--scaling weak)")
+    p.add_argument("--scaling", choices=["weak", "strong"], default="strong",
+                   help="strong: N fixed in total (riemann.cpp:10,71-73); weak: N per GPU")
     p.add_argument("--integrand", default="pi4")
     p.add_argument("--rule", default="left", choices=["left", "mid", "right"])
     p.add_argument("--dtype", default="fp64", choices=["fp64", "fp32", "fp32acc"],
@@ -398,7 +401,7 @@ def main(argv=None) -> int:
         if world > 1:
             transport = native().rccl_transport()
     share = mdist.ranks_share_devices() and world > 1
-    transport_error = transport_check(world, share, transport)
+    transport_error = transport_check(world, share, transport, rccl=not cpu)
     if transport_error:
         print(f"bench.py: {transport_error}", file=sys.stderr)
     extras = {}
@@ -468,7 +471,8 @@ def main(argv=None) -> int:
                 "model": f"riemann_{args.integrand}_{args.dtype}",
                 "integrand": "4/(1+x^2) on [0,1]" if args.integrand == "pi4" else args.integrand,
                 "N": n_total,
-                "n_per_gpu": n_total // world,
+                # rank 0's share (ranks differ by at most one sample when G does not divide N)
+                "n_per_gpu": plan.count if plan is not None else n_total // world,
                 "rule": args.rule,
                 "division": str(plan.effective_div).split(".")[-1] if plan is not None else "ieee",
                 "global_batch": n_total,
@@ -499,17 +503,23 @@ def main(argv=None) -> int:
     return 0 if ok else 1
 
 
-def transport_check(world: int, share: bool, transport: dict) -> str | None:
+def transport_check(world: int, share: bool, transport: dict, rccl: bool = True) -> str | None:
     """None, or why the multi-GPU record cannot stand: ranks of ONE node on distinct GPUs must
-    meet over xGMI peer-to-peer, not a network transport (a silent fallback — P2P disabled, a
-    leaked NCCL_HOSTID splitting the node into W "hosts" — would corrupt the scaling curve).
-    Ranks sharing a GPU (MIINT_OVERSUBSCRIBE) legitimately use sockets; an unknown transport
-    (no RCCL log) is recorded as null, not failed."""
-    if world <= 1 or share or not transport or not transport.get("transport"):
+    be seen to meet over xGMI peer-to-peer, not a network transport (a silent fallback — P2P
+    disabled, a leaked NCCL_HOSTID splitting the node into W "hosts" — would corrupt the scaling
+    curve). Fail-closed: no transport evidence at all (RCCL's INIT log missing or without a
+    single peer connection) fails too, since it cannot tell xGMI from sockets. Ranks sharing a
+    GPU (MIINT_OVERSUBSCRIBE) legitimately use sockets; gloo-only runs (rccl=False) have no
+    RCCL transport to check."""
+    if world <= 1 or share or not rccl:
         return None
     local = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
     if local != world:  # a multi-node job: NET between nodes is expected
         return None
+    if not transport or not transport.get("transport"):
+        where = (transport or {}).get("log") or "no RCCL log captured"
+        return (f"RCCL transport unknown between {world} ranks on distinct local GPUs (no peer "
+                f"connection in {where}): P2P over xGMI cannot be confirmed")
     if transport.get("uses_net"):
         return (f"RCCL transport is {transport['transport']} (nNodes {transport.get('nnodes')}) "
                 f"between {world} ranks on distinct local GPUs: expected P2P over xGMI")
@@ -717,21 +727,23 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
             "verified": bool(result_ok("pi4", args.rule, args.dtype, n_total, e) and
                              pp["max_ulp"] <= 2.0)}
         del ex
-    # (3) the headline metric's own config at every GPU count: N = 1e9 IN TOTAL split over
-    #     the ranks (riemann.cpp:10,71-73: the reference keeps N fixed and divides it among
-    #     its workers), its own graph and timing — equal to the headline at G = 1
+    # (3) the headline config in its other scaling form. Strong headline (the default: N = 1e9
+    #     IN TOTAL, riemann.cpp:10,71-73): the weak form, 1e9 samples PER GPU (N = 1e9 x G,
+    #     "weak_1e9_per_gpu"). Weak headline (--scaling weak): the metric's fixed N = 1e9 split
+    #     over the ranks ("strong_1e9"). Own graph and timing; equal configs at G = 1.
     if pi4:
-        n1 = 10**9
+        weak_extra = args.scaling == "strong"
+        key, n1 = ("weak_1e9_per_gpu", 10**9 * ctx.world) if weak_extra else ("strong_1e9", 10**9)
         st = Integrator("pi4", n=n1, div=args.div, **dict(kw, dtype="fp64"))
         steps = 48
         ms = _timed_steps(ctx, st.plan, steps, pipeline, dev)
         v = st.plan.host_result(st.plan.host_index_of(steps - 1, True))
         e = abs(v - math.pi)
-        out["strong_1e9"] = {"N": n1, "value": n1 / (ms * 1e-3), "ms_per_step": ms,
-                             "steps": steps, "result": v, "abs_err": e,
-                             "n_per_gpu": st.plan.count, "grid": st.plan.grid,
-                             "scaling": "strong", "n_gpus": ctx.world,
-                             "verified": result_ok("pi4", args.rule, "fp64", n1, e)}
+        out[key] = {"N": n1, "value": n1 / (ms * 1e-3), "ms_per_step": ms,
+                    "steps": steps, "result": v, "abs_err": e,
+                    "n_per_gpu": st.plan.count, "grid": st.plan.grid,
+                    "scaling": "weak" if weak_extra else "strong", "n_gpus": ctx.world,
+                    "verified": result_ok("pi4", args.rule, "fp64", n1, e)}
         del st
     # (4) BASELINE config #3: N = 1e10 in total over the same GPUs (strong scaling)
     if pi4:
@@ -816,7 +828,7 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
     # (6c) the reference's own integrands (sin: riemann.cpp:37, cintegrate.cu:68; the table
     #      interpolant: cintegrate.cu:36-44; the analytic train model: riemann.cpp:103-116) and
     #      the random-coefficient polynomial, each one timed 48-step graph batch of the same
-    #      shape as the headline (N per GPU, weak), checked against its analytic value
+    #      shape as the headline (the headline's N), checked against its analytic value
     if pi4:
         for name in ("sin", "train", "table", "poly"):
             it = Integrator(name, n=n_total, **dict(kw, dtype="fp64"))

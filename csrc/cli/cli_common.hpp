@@ -305,6 +305,16 @@ struct RankFacts {
     r.add("rccl_world", rccl_world);
     const RcclTransport tr = rccl_world > 0 ? rccl_transport() : RcclTransport{};
     r.add("rccl_transport", tr.transport).add("rccl_nnodes", tr.nnodes);
+    // fail-closed: RCCL ranks of one node on distinct GPUs must be SEEN meeting
+    // over P2P/xGMI; no evidence, sockets or a multi-node count is recorded as an error
+    std::string err;
+    if (comm == "rccl") {
+      const int local_world = t.multiproc ? env_int("LOCAL_WORLD_SIZE", t.world) : t.world;
+      err = transport_error(tr, t.world, local_world, ranks_share_devices() && t.world > 1);
+      if (!err.empty()) std::fprintf(stderr, "transport check: %s\n", err.c_str());
+    }
+    r.add("transport_verified", err.empty());
+    if (!err.empty()) r.add("transport_error", err);
   }
 };
 

@@ -198,6 +198,11 @@ int comm_sweep(const cli::Args& a, const cli::Topology& topo, double max_bytes, 
   if (topo.rank0 != 0) return 0;
   const double P = topo.world;
   const RcclTransport tr = rccl_transport();  // the connections the sweep's collectives used
+  const bool share = ranks_share_devices() && topo.world > 1;
+  const std::string terr = transport_error(
+      tr, topo.world, topo.multiproc ? cli::env_int("LOCAL_WORLD_SIZE", topo.world) : topo.world,
+      share);
+  if (!terr.empty()) std::fprintf(stderr, "miint comm: transport check: %s\n", terr.c_str());
   for (size_t k = 0; k < counts.size(); ++k)
     for (int op = 0; op < 3; ++op) {
       const double bytes = counts[k] * 8.0 * (op == 1 ? P : 1.0);
@@ -213,7 +218,8 @@ int comm_sweep(const cli::Args& a, const cli::Topology& topo, double max_bytes, 
                        .add("busbw_GBps", alg * factor)
                        .add("ranks_share_gpus", ranks_share_devices() && topo.world > 1)
                        .add("rccl_transport", tr.transport)
-                       .add("rccl_nnodes", tr.nnodes),
+                       .add("rccl_nnodes", tr.nnodes)
+                       .add("transport_verified", terr.empty()),
                 true);
     }
   return 0;

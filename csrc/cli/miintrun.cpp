@@ -133,10 +133,16 @@ int main(int argc, char** argv) {
         rc = code;
         std::fprintf(stderr, "miintrun: a rank exited with %d; stopping the others\n", code);
       }
-      if (code != 0 && !stopping && !lingering && WIFEXITED(st) && linger > 0) {
-        lingering = true;  // an exit status: the peers may be finishing the same failure
-        t_linger = std::chrono::steady_clock::now();
-      } else if (code != 0 && !stopping) {
+      if (code != 0 && !stopping && WIFEXITED(st) && linger > 0) {
+        // an exit status: the peers may be finishing the same agreed failure (every rank
+        // exits 3 after a scan timeout anywhere). The first one starts the linger; further
+        // exits with a status during it only set rc — stopping now could cut rank 0 off
+        // before it prints its record, which is what the linger is for.
+        if (!lingering) {
+          lingering = true;
+          t_linger = std::chrono::steady_clock::now();
+        }
+      } else if (code != 0 && !stopping) {  // a signal (crash), or no linger: stop at once
         stopping = true;
         t_stop = std::chrono::steady_clock::now();
         signal_all(SIGTERM);

@@ -124,6 +124,8 @@ int main(int argc, char** argv) {
     TrainScanResult res;
     std::string timeout_what;
     cli::RankFacts facts;
+    ReplicaDigest digest;
+    bool replicas_identical = true;
     std::mutex mu;
     cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
       TrainScan ts(cfg, dev, comm);
@@ -146,10 +148,23 @@ int main(int argc, char** argv) {
         timeout_what = e.what();
       }
       if (!r.timeout) r.device_ms = agree.max(r.device_ms);  // the slowest rank's time
+      // --replicate (4main.c:157: every rank ends holding the whole table): fingerprint each
+      // rank's copy; the hashes are gathered, so rank 0 can say whether all copies are equal
+      ReplicaDigest dg;
+      bool identical = true;
+      if (cfg.replicate && !r.timeout) {
+        dg = ts.replica_digest();
+        const double hi = static_cast<double>(dg.hash >> 32), lo = static_cast<double>(dg.hash & 0xffffffffu);
+        const std::vector<double> all = agree.gather({hi, lo});
+        for (size_t q = 0; q + 1 < all.size(); q += 2)
+          identical = identical && all[q] == hi && all[q + 1] == lo;
+      }
       std::lock_guard<std::mutex> lk(mu);
       if (rank == topo.rank0) {
         res = r;
         facts.note(comm);
+        digest = dg;
+        replicas_identical = identical;
       }
       if (r.timeout) res.timeout = 1;
     });
@@ -162,6 +177,22 @@ int main(int argc, char** argv) {
     cli::JsonRecord rec;
     rec.add("program", "trainscan").add("gpus", topo.world);
     facts.add(rec, topo);
+    if (cfg.replicate) {
+      char hex[24];
+      std::snprintf(hex, sizeof hex, "%016llx", static_cast<unsigned long long>(digest.hash));
+      std::string at = "[";
+      for (int k = 0; k < 5; ++k) {
+        char b[40];
+        std::snprintf(b, sizeof b, "%s%.17g", k ? ", " : "", digest.at[k]);
+        at += b;
+      }
+      rec.add("replicate", true)
+          .add("replica_n", static_cast<double>(digest.n))
+          .add("replica_hash", std::string(hex))
+          .add("replica_sum", digest.sum)
+          .add_raw("replica_at", at + "]")
+          .add("replicas_identical", replicas_identical);
+    }
     cli::emit(a, rec.add("distance", res.distance)
                      .add("sum_of_sums", res.sum_of_sums)
                      .add("device_ms", res.device_ms)

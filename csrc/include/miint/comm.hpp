@@ -297,6 +297,14 @@ struct RcclTransport {
   bool uses_net() const { return transport.find("NET/") != std::string::npos; }
 };
 RcclTransport parse_rccl_log(const std::string& text);
+// "" or why a multi-rank record cannot stand (bench.py's transport_check, same rules): ranks
+// of ONE node on distinct GPUs must be seen meeting over P2P (xGMI). Fail-closed: a network
+// transport, more than one node counted, or no connection evidence at all is an error. Ranks
+// sharing a GPU (share), one rank, and multi-node jobs (local_world != world) are exempt.
+std::string transport_error(const RcclTransport& t, int world, int local_world, bool share);
+// A user's own NCCL_DEBUG_FILE is honoured (read, never overwritten or deleted; "%h"/"%p"
+// expanded as RCCL does); a user's own NCCL_DEBUG level below INFO still gets the INIT lines
+// captured, and the WARN lines are echoed to stderr at exit (the user asked to see them).
 void capture_rccl_log();
 std::string rccl_log_path();  // "" when not capturing
 RcclTransport rccl_transport();

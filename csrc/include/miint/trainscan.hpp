@@ -104,6 +104,18 @@ unsigned trainscan_onepass_timeout(const void* ws, hipStream_t s);
 // totals are then NaN); 0 for the 3-kernel path. Synchronises.
 unsigned trainscan_local_timeout(const TrainScanKernelParams& p, const void* ws, hipStream_t s);
 
+// A host-side fingerprint of a replicated table (--replicate, 4main.c:157's "every rank holds
+// the whole table"): FNV-1a over the fp64 bit patterns (equal on every rank iff the copies are
+// bitwise equal), a compensated sum and samples at fixed fractions of the table (comparable
+// to the one-GPU table within roundoff: the carries round differently from one scan).
+struct ReplicaDigest {
+  uint64_t hash = 0;
+  uint64_t n = 0;
+  double sum = 0.0;
+  double at[5] = {0, 0, 0, 0, 0};  // elements 0, n/4, n/2, 3n/4, n-1
+};
+ReplicaDigest digest_table(const double* host, uint64_t n);
+
 class TrainScan {
  public:
   TrainScan(const TrainScanConfig& cfg, int device, const Comm* comm = nullptr);
@@ -117,6 +129,9 @@ class TrainScan {
   const double* velocity() const { return vel_.get(); }
   const double* position() const { return pos_.get(); }
   const double* replicated() const { return full_.get(); }
+  // Copy the replicated table to the host and fingerprint it (--replicate only; synchronises;
+  // not part of any timed region)
+  ReplicaDigest replica_digest();
   hipStream_t stream() const { return stream_.get(); }
 
  private:

@@ -216,6 +216,13 @@ PYBIND11_MODULE(_miint, m) {
         "route RCCL's INIT log into a per-process file (call before the first RCCL call)");
   m.def("rccl_log_path", &rccl_log_path);
   m.def("rccl_transport", [transport_dict]() { return transport_dict(rccl_transport()); });
+  m.def(
+      "transport_error",
+      [](const std::string& log_text, int world, int local_world, bool share) {
+        return transport_error(parse_rccl_log(log_text), world, local_world, share);
+      },
+      "the native CLIs' fail-closed transport verdict on an RCCL INIT log (\"\" = ok)",
+      py::arg("log_text"), py::arg("world"), py::arg("local_world"), py::arg("share"));
 
   // ------------------------------------------------------------------ Riemann plan
   py::class_<RiemannConfig>(m, "RiemannConfig")

@@ -102,11 +102,40 @@ int int_after(const std::string& line, const char* key) {
 std::mutex g_log_mu;
 std::string g_log_path;  // set once per process by capture_rccl_log
 bool g_log_done = false;
+bool g_log_ours = false;  // our file (deleted at exit) vs the user's NCCL_DEBUG_FILE
+bool g_echo_warn = false;  // the user set NCCL_DEBUG below INFO: WARN lines go to stderr
 
-void remove_log() {
+void finish_log() {
+  if (g_log_path.empty()) return;
+  if (g_echo_warn) {  // what the user's level would have shown them on stderr
+    std::ifstream f(g_log_path);
+    std::string line;
+    while (std::getline(f, line))
+      if (line.find(" WARN ") != std::string::npos) std::fprintf(stderr, "%s\n", line.c_str());
+  }
   const char* keep = std::getenv("MIINT_RCCL_LOG_KEEP");
-  if (!g_log_path.empty() && !(keep && *keep && std::strcmp(keep, "0") != 0))
+  if (g_log_ours && !(keep && *keep && std::strcmp(keep, "0") != 0))
     std::remove(g_log_path.c_str());
+}
+
+// RCCL's NCCL_DEBUG_FILE substitutions: %h = hostname, %p = pid
+std::string expand_debug_file(const std::string& pat) {
+  std::string out;
+  for (size_t i = 0; i < pat.size(); ++i) {
+    if (pat[i] == '%' && i + 1 < pat.size() && (pat[i + 1] == 'h' || pat[i + 1] == 'p')) {
+      if (pat[i + 1] == 'p') {
+        out += std::to_string(static_cast<long>(::getpid()));
+      } else {
+        char host[256] = {0};
+        ::gethostname(host, sizeof(host) - 1);
+        out += host;
+      }
+      ++i;
+    } else {
+      out += pat[i];
+    }
+  }
+  return out;
 }
 
 }  // namespace
@@ -155,23 +184,52 @@ void capture_rccl_log() {
   g_log_done = true;
   const char* off = std::getenv("MIINT_RCCL_LOG");
   if (off && std::strcmp(off, "0") == 0) return;
-  const char* tmp = std::getenv("TMPDIR");
-  g_log_path = std::string(tmp && *tmp ? tmp : "/tmp") + "/miint_rccl." +
-               std::to_string(static_cast<long>(::getpid())) + ".log";
-  std::remove(g_log_path.c_str());  // a stale file of a recycled pid
-  // INFO lines of the INIT subsystem (comm topology + one line per peer connection) into
-  // the file; whatever else the caller asked RCCL to log goes there too
-  ::setenv("NCCL_DEBUG_FILE", g_log_path.c_str(), 1);
+  const char* user_file = std::getenv("NCCL_DEBUG_FILE");
   const char* lvl = std::getenv("NCCL_DEBUG");
-  if (!lvl || (std::strcmp(lvl, "INFO") != 0 && std::strcmp(lvl, "TRACE") != 0))
-    ::setenv("NCCL_DEBUG", "INFO", 1);
+  const bool info = lvl && (std::strcmp(lvl, "INFO") == 0 || std::strcmp(lvl, "TRACE") == 0);
+  if (user_file && *user_file) {
+    // the user's file: read it, never overwrite or delete it. Without a level of their own
+    // RCCL would write nothing into it, so INFO (INIT lines) is added in that case only.
+    g_log_path = expand_debug_file(user_file);
+    g_log_ours = false;
+    if (!lvl || !*lvl) ::setenv("NCCL_DEBUG", "INFO", 1);
+  } else {
+    const char* tmp = std::getenv("TMPDIR");
+    g_log_path = std::string(tmp && *tmp ? tmp : "/tmp") + "/miint_rccl." +
+                 std::to_string(static_cast<long>(::getpid())) + ".log";
+    std::remove(g_log_path.c_str());  // a stale file of a recycled pid
+    g_log_ours = true;
+    ::setenv("NCCL_DEBUG_FILE", g_log_path.c_str(), 1);
+    // INFO lines of the INIT subsystem (comm topology + one line per peer connection) into
+    // the file. A level the user chose below INFO (WARN, VERSION) loses nothing: its WARN
+    // lines are echoed to stderr at exit.
+    g_echo_warn = lvl && *lvl && !info;
+    if (!info) ::setenv("NCCL_DEBUG", "INFO", 1);
+  }
   const char* sub = std::getenv("NCCL_DEBUG_SUBSYS");
   if (!sub || !*sub) {
     ::setenv("NCCL_DEBUG_SUBSYS", "INIT", 1);
   } else if (sub[0] != '^' && !std::strstr(sub, "INIT") && !std::strstr(sub, "ALL")) {
     ::setenv("NCCL_DEBUG_SUBSYS", (std::string(sub) + ",INIT").c_str(), 1);
   }
-  std::atexit(remove_log);
+  std::atexit(finish_log);
+}
+
+std::string transport_error(const RcclTransport& t, int world, int local_world, bool share) {
+  if (world <= 1 || share || local_world != world) return "";
+  if (t.transport.empty())
+    return "RCCL transport unknown between " + std::to_string(world) +
+           " ranks on distinct local GPUs (no peer connection in " +
+           (t.log.empty() ? std::string("no RCCL log captured") : t.log) +
+           "): P2P over xGMI cannot be confirmed";
+  if (t.uses_net())
+    return "RCCL transport is " + t.transport + " (nNodes " + std::to_string(t.nnodes) +
+           ") between " + std::to_string(world) +
+           " ranks on distinct local GPUs: expected P2P over xGMI";
+  if (t.nnodes > 1)
+    return "RCCL counted " + std::to_string(t.nnodes) + " nodes for " + std::to_string(world) +
+           " ranks of one node";
+  return "";
 }
 
 std::string rccl_log_path() {

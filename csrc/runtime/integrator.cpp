@@ -464,7 +464,21 @@ OneShotTiming RiemannPlan::time_one_shot(int reps, const std::string& mode, int 
     else enqueue(cs, 0, 0);
     if (events) ev_t1_.record(cs);
     if (poll) {
-      while (*word == kSentinel) {
+      // bounded spin: past 50 ms (a healthy call takes ~80 us) the stream is
+      // asked whether it finished or failed without storing the result; past the plan's
+      // timeout (or 60 s) the call is abandoned
+      const double limit = cfg_.timeout_s > 0 ? cfg_.timeout_s : 60.0;
+      for (uint32_t spin = 1; *word == kSentinel; ++spin) {
+        if ((spin & 1023u) != 0) continue;
+        const double waited = wall_seconds() - t0;
+        if (waited < 0.05) continue;
+        const hipError_t q = hipStreamQuery(cs);
+        if (q != hipErrorNotReady && *word == kSentinel) {
+          MIINT_HIP(q);  // an asynchronous kernel failure surfaces here
+          throw Error("time_one_shot: the stream finished but the result word was never stored");
+        }
+        if (waited > limit)
+          throw Error("time_one_shot: no result after " + std::to_string(limit) + " s (" + mode + ")");
       }
     } else {
       MIINT_HIP(hipStreamSynchronize(cs));

@@ -2,6 +2,9 @@
 #include "miint/trainscan.hpp"
 
 #include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
 
 #include "miint/fault.hpp"
 #include "miint/integrator.hpp"
@@ -178,6 +181,41 @@ void TrainScan::enqueue() {
                                hipMemcpyDeviceToDevice, s));
     }
   }
+}
+
+ReplicaDigest digest_table(const double* host, uint64_t n) {
+  ReplicaDigest d;
+  d.n = n;
+  uint64_t h = 1469598103934665603ull;  // FNV-1a 64
+  double sum = 0.0, c = 0.0;            // Neumaier
+  for (uint64_t i = 0; i < n; ++i) {
+    uint64_t bits;
+    std::memcpy(&bits, &host[i], sizeof bits);
+    for (int b = 0; b < 8; ++b) {
+      h ^= (bits >> (8 * b)) & 0xffu;
+      h *= 1099511628211ull;
+    }
+    const double x = host[i], t = sum + x;
+    c += std::fabs(sum) >= std::fabs(x) ? (sum - t) + x : (x - t) + sum;
+    sum = t;
+  }
+  d.hash = h;
+  d.sum = sum + c;
+  if (n > 0) {
+    const uint64_t idx[5] = {0, n / 4, n / 2, 3 * (n / 4), n - 1};
+    for (int k = 0; k < 5; ++k) d.at[k] = host[idx[k]];
+  }
+  return d;
+}
+
+ReplicaDigest TrainScan::replica_digest() {
+  MIINT_CHECK(cfg_.replicate, "replica_digest needs --replicate");
+  DeviceGuard g(device_);
+  std::vector<double> h(total_);
+  MIINT_HIP(hipMemcpyAsync(h.data(), full_.get(), total_ * sizeof(double), hipMemcpyDeviceToHost,
+                           stream_.get()));
+  MIINT_HIP(hipStreamSynchronize(stream_.get()));
+  return digest_table(h.data(), total_);
 }
 
 TrainScanResult TrainScan::run() {

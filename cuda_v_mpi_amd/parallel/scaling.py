@@ -5,16 +5,18 @@ The reference measures its decomposition by re-running ``mpirun -np P`` by hand
 every GPU count the node has,
 
   * ``bench.py --gpus N`` (one process per GPU, spawned by bench.py itself; RCCL over xGMI):
-    the weak-scaling headline (1e9 samples per GPU) and, from the same run, the metric's own
-    fixed-N point (``strong_1e9``: N = 1e9 in total over the N GPUs, as the reference splits
-    its fixed STEPS over its workers, riemann.cpp:10,71-73), BASELINE #3's strong-scaling
-    point (N = 1e10 in total) and BASELINE #5's 2-D field (4096^2 samples in total, rows
-    split over the N GPUs);
+    the headline, which is the metric's own config at every N (N = 1e9 samples IN TOTAL over
+    the N GPUs, as the reference splits its fixed STEPS over its workers,
+    riemann.cpp:10,71-73: strong scaling) and, from the same run, the weak form
+    (``weak_1e9_per_gpu``: 1e9 samples per GPU), BASELINE #3's strong-scaling point (N = 1e10
+    in total) and BASELINE #5's 2-D field (4096^2 samples in total, rows split over the N
+    GPUs);
   * ``miint comm --gpus N`` (one process driving N GPUs, ncclCommInitAll): all-reduce and
     all-gather latency at 8 B (the Riemann payload, riemann.cpp:76) and 144 MB (4main.c:157's
     broadcast table),
 
-and derives weak- and strong-scaling efficiency against the N = 1 row. Counts the node
+and derives strong- (the headline ``value``) and weak-scaling efficiency against the N = 1
+row. Counts the node
 cannot run get an explicit ``skipped`` row instead of a number.
 
     python -m cuda_v_mpi_amd scale --gpus 1,2,4,8 [--steps 200] [--jsonl FILE] [--md FILE]
@@ -119,11 +121,18 @@ def sweep(counts: list[int], steps: int = 200, warmup: int = 10, comm: bool = Tr
         }
         if n > have:
             row["ranks_share_gpus"] = True
-        s1 = b.get("strong_1e9")
-        if s1:
-            row["strong_1e9_value"] = s1["value"]
-            row["strong_1e9_ms"] = s1["ms_per_step"]
-            row["strong_1e9_verified"] = s1.get("verified")
+        # the headline is the metric's fixed N = 1e9 (strong); a record from --scaling weak
+        # names its strong point "strong_1e9" and carries the weak figure at the top
+        strong = b.get("scaling", "strong") == "strong"
+        if not strong and b.get("strong_1e9"):
+            w = {"value": b["value"], "ms_per_step": b["ms_per_step"], "verified": b["verified"]}
+            row.update(value=b["strong_1e9"]["value"], ms_per_step=b["strong_1e9"]["ms_per_step"])
+        else:
+            w = b.get("weak_1e9_per_gpu")
+        if w:
+            row["weak_1e9_value"] = w["value"]
+            row["weak_1e9_ms"] = w["ms_per_step"]
+            row["weak_1e9_verified"] = w.get("verified")
         s = b.get("baseline3_strong_1e10")
         if s:
             row["strong_1e10_value"] = s["value"]
@@ -142,9 +151,9 @@ def sweep(counts: list[int], steps: int = 200, warmup: int = 10, comm: bool = Tr
         if base is None or "value" not in r or r.get("ranks_share_gpus"):
             continue
         n = r["n_gpus"]
-        r["weak_eff"] = r["value"] / (n * base["value"])
-        if "strong_1e9_value" in r and "strong_1e9_value" in base:  # the metric's own N
-            r["strong_1e9_eff"] = r["strong_1e9_value"] / (n * base["strong_1e9_value"])
+        r["strong_1e9_eff"] = r["value"] / (n * base["value"])  # the metric's own N
+        if "weak_1e9_value" in r and "weak_1e9_value" in base:
+            r["weak_eff"] = r["weak_1e9_value"] / (n * base["weak_1e9_value"])
         if "strong_1e10_value" in r and "strong_1e10_value" in base:
             r["strong_eff"] = r["strong_1e10_value"] / (n * base["strong_1e10_value"])
         if "t2d_4096_us" in r and "t2d_4096_us" in base:  # fixed total work: strong
@@ -153,8 +162,8 @@ def sweep(counts: list[int], steps: int = 200, warmup: int = 10, comm: bool = Tr
 
 
 def markdown(rows: list[dict]) -> str:
-    cols = ["n_gpus", "value", "ms_per_step", "weak_eff", "strong_1e9_value", "strong_1e9_ms",
-            "strong_1e9_eff", "strong_1e10_value", "strong_eff",
+    cols = ["n_gpus", "value", "ms_per_step", "strong_1e9_eff", "weak_1e9_value", "weak_1e9_ms",
+            "weak_eff", "strong_1e10_value", "strong_eff",
             "t2d_4096_us", "t2d_strong_eff", "one_shot_1e9_us", "per_rank_spread_ms", "rccl_world",
             "rccl_transport", "rccl_nnodes", "allreduce_8B_us", "allgather_8B_us",
             "allreduce_144MB_us", "allgather_144MB_us"]

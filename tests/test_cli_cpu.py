@@ -106,7 +106,9 @@ def test_bench_spawns_ranks_without_torchrun():
     assert js["n_gpus"] == 2 and js["launcher"] == "spawn"
     assert js["parent_imported_torch"] is False
     assert len(js["per_rank_ms"]) == 2 and js["per_rank_spread_ms"] >= 0
-    assert js["config"]["N"] == 40_000 and js["config"]["parallelism"] == "dp2"
+    # strong scaling (the metric's form): --samples is the TOTAL N, split over the 2 ranks
+    assert js["scaling"] == "strong" and js["config"]["parallelism"] == "dp2"
+    assert js["config"]["N"] == 20_000 and js["config"]["n_per_gpu"] == 10_000
     assert js["verified"] and abs(js["result"] - math.pi) < 1e-3
 
 
@@ -131,18 +133,21 @@ def test_scale_sweep_rows_and_efficiency(monkeypatch):
     monkeypatch.setattr(scaling, "visible_gpus", lambda: 2)
     fake = {1: 1.0e13, 2: 1.9e13}
     monkeypatch.setattr(scaling, "run_bench", lambda n, s, w: {
-        "value": fake[n], "ms_per_step": 0.075, "per_rank_spread_ms": 0.001,
+        "value": fake[n], "ms_per_step": 0.075, "per_rank_spread_ms": 0.001, "scaling": "strong",
         "rccl_world": n if n > 1 else None, "config": {"graphs": True}, "verified": True,
         "baseline3_strong_1e10": {"value": fake[n] * 1.05, "ms_per_step": 0.7},
-        "strong_1e9": {"value": fake[n] * 0.9, "ms_per_step": 0.08, "verified": True},
+        "weak_1e9_per_gpu": {"value": fake[n] * 1.02, "ms_per_step": 0.08, "verified": True},
         "baseline5_table2d_4096": {"ms_per_integration": 0.009 / n ** 0.8}})
     monkeypatch.setattr(scaling, "run_comm", lambda n: {"allreduce_8B_us": 10.0 * n})
     rows = scaling.sweep([1, 2, 4, 8])
     assert [r["n_gpus"] for r in rows] == [1, 2, 4, 8]
     assert rows[2]["skipped"] == "only 2 devices" and rows[3]["skipped"] == "only 2 devices"
-    assert rows[0]["weak_eff"] == 1.0 and abs(rows[1]["weak_eff"] - 0.95) < 1e-12
-    assert abs(rows[1]["strong_eff"] - 0.95) < 1e-12
+    # the row's value is the metric's own config (N = 1e9 in total: strong); weak a column
+    assert rows[1]["value"] == 1.9e13
     assert rows[0]["strong_1e9_eff"] == 1.0 and abs(rows[1]["strong_1e9_eff"] - 0.95) < 1e-12
+    assert rows[0]["weak_eff"] == 1.0 and abs(rows[1]["weak_eff"] - 0.95) < 1e-12
+    assert rows[1]["weak_1e9_value"] == pytest.approx(1.9e13 * 1.02)
+    assert abs(rows[1]["strong_eff"] - 0.95) < 1e-12
     assert abs(rows[1]["t2d_4096_us"] - 9.0 / 2 ** 0.8) < 1e-9
     assert abs(rows[1]["t2d_strong_eff"] - 2 ** 0.8 / 2) < 1e-12
     md = scaling.markdown(rows)
@@ -154,8 +159,8 @@ def test_scale_sweep_rows_and_efficiency(monkeypatch):
     rows = scaling.sweep([1, 2, 4, 8])
     assert all("skipped" not in r for r in rows)
     assert [bool(r.get("ranks_share_gpus")) for r in rows] == [False, False, True, True]
-    assert "weak_eff" not in rows[2] and "allreduce_8B_us" not in rows[3]
-    assert "weak_eff" in rows[1] and "allreduce_8B_us" in rows[1]
+    assert "strong_1e9_eff" not in rows[2] and "allreduce_8B_us" not in rows[3]
+    assert "strong_1e9_eff" in rows[1] and "allreduce_8B_us" in rows[1]
 
 
 def test_bench_driver_launch_form_json_contract():
@@ -183,7 +188,7 @@ def test_bench_driver_launch_form_json_contract():
     for k in ("model", "global_batch", "seq_len", "parallelism"):
         assert k in js["config"], k
     assert js["n_gpus"] == 2 and js["steps"] == 3 and js["warmup"] == 1
-    assert js["launcher"] == "torchrun" and js["scaling"] == "weak"
+    assert js["launcher"] == "torchrun" and js["scaling"] == "strong"
     assert js["comm_fallback"] is None
     assert js["metric"].startswith("Riemann subintervals/sec at N=1e9 fp64")
     assert js["ms_per_step"] == pytest.approx(max(js["per_rank_ms"]))
@@ -230,14 +235,32 @@ def test_bench_verification_bounds():
 
 def test_bench_eight_rank_rehearsal():
     """The driver's 8-GPU scaling run, rehearsed on the CPU: 8 spawned rank processes, the gloo
-    control plane (no torch RCCL group), one time per rank, MAX over ranks, weak N = 8 x
-    per-rank samples, every rank's result verified."""
+    control plane (no torch RCCL group), one time per rank, MAX over ranks, the metric's
+    fixed total N split 8 ways (strong), every rank's result verified."""
     p = _bench("--gpus", "8", "--device", "cpu", "--samples", "8e4", "--steps", "2",
                "--warmup", "1", "--settle-ms", "0", timeout=600)
     assert p.returncode == 0, p.stderr[-3000:]
     js = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
     assert js["n_gpus"] == 8 and len(js["per_rank_ms"]) == 8
     assert js["control_plane"] == "gloo" and js["torch_nccl_groups"] == 0
-    assert js["config"]["N"] == 8 * 80_000 and js["config"]["parallelism"] == "dp8"
+    assert js["config"]["N"] == 80_000 and js["config"]["parallelism"] == "dp8"
+    assert js["config"]["n_per_gpu"] == 10_000 and js["scaling"] == "strong"
     assert js["ms_per_step"] == pytest.approx(max(js["per_rank_ms"]))
     assert js["verified"]
+
+
+def test_bench_multi_rank_record_is_the_metric_config():
+    """VERDICT r4 Next #1: at G > 1 the top-level record IS the metric's config, N = 1e9 in
+    total split over the ranks (riemann.cpp:10,71-73), not a weak N = G x 1e9 figure printed
+    under the N = 1e9 metric string. CPU form (gloo, torch fp64 evaluation): 2 ranks, 5e8
+    samples each, the left-rule truncation of N = 1e9 (h - h^2/6) checked to 1e-13."""
+    p = _bench("--gpus", "2", "--device", "cpu", "--steps", "1", "--warmup", "1",
+               "--settle-ms", "0", timeout=600)
+    assert p.returncode == 0, p.stderr[-3000:]
+    js = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
+    assert js["metric"] == "Riemann subintervals/sec at N=1e9 fp64; |error| vs analytic π"
+    assert js["scaling"] == "strong" and js["n_gpus"] == 2
+    assert js["config"]["N"] == 10**9 and js["config"]["n_per_gpu"] == 5 * 10**8
+    assert js["config"]["global_batch"] == 10**9
+    assert js["verified"] and abs(js["abs_err"] - (1e-9 - 1e-18 / 6)) <= 1e-13
+    assert js["value"] == pytest.approx(10**9 / (js["ms_per_step"] * 1e-3))

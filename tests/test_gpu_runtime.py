@@ -269,6 +269,28 @@ def test_cli_riemann_format(cli_built):
     assert float(lines[1].rsplit(" ", 1)[1]) == pytest.approx(2.0, abs=1e-11)
 
 
+def test_cli_riemann_default_is_one_run(cli_built, tmp_path):
+    """VERDICT r4 Next #5: the default program is the reference's single run (riemann.cpp:
+    49-51,90-96): one cold + one timed integration, then exactly the two §2.6 lines — the
+    one-integration-per-call harness (~450 extra integrations) runs only with --json or
+    --one-shot. The --jsonl side record shows it did not run."""
+    rec = tmp_path / "r.jsonl"
+    p = _run([os.path.join(cli_built, "riemann"), "--jsonl", str(rec)])
+    assert p.returncode == 0, p.stderr
+    lines = p.stdout.strip().splitlines()
+    assert len(lines) == 2 and lines[0].endswith(" seconds")
+    assert lines[1].startswith("The integral of f(x) from 0.0 to 3.14159265358979 with ")
+    js = json.loads(rec.read_text().strip().splitlines()[-1])
+    assert js["one_shot"] is False and "ms_one_shot" not in js
+    # the whole program (process start to print) is far below what the harness would add
+    # (~450 integrations of 1e9 samples ~ 35 ms of GPU time alone)
+    assert js["seconds_wall"] > 0
+    q = _run([os.path.join(cli_built, "riemann"), "--one-shot", "--jsonl", str(rec)])
+    assert q.returncode == 0, q.stderr
+    js = json.loads(rec.read_text().strip().splitlines()[-1])
+    assert js["one_shot"] is True and 0 < js["ms_one_shot"] < 5.0
+
+
 def test_cli_riemann_parity_single_rank_is_zero(cli_built):
     p = _run([os.path.join(cli_built, "riemann"), "--parity", "--n", "1e6"])
     assert p.returncode == 0, p.stderr
@@ -365,7 +387,8 @@ def test_bench_two_ranks_share_one_gpu_over_gloo():
     assert len(rows) == 1
     js = rows[0]
     assert js["verified"] and js["n_gpus"] == 2 and js["config"]["comm"] == "torch"
-    assert js["config"]["N"] == 2 * 10**9 and js["config"]["n_per_gpu"] == 10**9
+    # the metric's N = 1e9 in total, split over the two ranks (strong)
+    assert js["config"]["N"] == 10**9 and js["config"]["n_per_gpu"] == 5 * 10**8
 
 
 def test_cli_comm_sweep(cli_built):
@@ -405,12 +428,13 @@ def test_bench_torchrun_single_rank(native, cuda):
 
 def test_bench_two_ranks_shared_gpu_torch_comm(native, cuda):
     """Two processes on one GPU: rank slicing + torch.distributed (gloo) all_reduce of the
-    per-rank kernel partials; weak scaling doubles N."""
+    per-rank kernel partials; --samples is the total N, halved per rank."""
     p = _torchrun(2, [os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo",
                       "--comm", "torch", "--steps", "12", "--warmup", "2", "--samples", "2e8"])
     assert p.returncode == 0, p.stderr[-3000:]
     js = json.loads(p.stdout.strip().splitlines()[-1])
-    assert js["n_gpus"] == 2 and js["config"]["N"] == 400_000_000 and js["verified"]
+    assert js["n_gpus"] == 2 and js["config"]["N"] == 200_000_000 and js["verified"]
+    assert js["config"]["n_per_gpu"] == 100_000_000
 
 
 def test_bench_native_comm_failure_falls_back_to_torch(native, cuda):

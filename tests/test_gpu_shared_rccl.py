@@ -57,6 +57,8 @@ def _shared_rccl(rec, world):
     assert rec["comm"] == "rccl" and rec["rccl_world"] == world
     assert rec["ranks_share_gpus"] is True
     assert rec["rccl_transport"].startswith("NET/Socket") and rec["rccl_nnodes"] == world
+    # sockets are this setup's transport, so the fail-closed check exempts it (and says so)
+    assert rec["transport_verified"] is True and "transport_error" not in rec
 
 
 @pytest.mark.parametrize("world", [2, 4])
@@ -137,7 +139,8 @@ def test_bench_two_ranks_native_rccl_one_gpu(cuda):
     assert r["rccl_transport"] == "NET/Socket" and r["rccl_nnodes"] == 2
     assert r["transport_verified"] and r["transport_error"] is None
     assert r["comm_fallback"] is None and r["graph_replays_timed"] == 1
-    assert r["config"]["bucketed_allreduce"] and r["config"]["N"] == 2 * 10**9
+    assert r["config"]["bucketed_allreduce"] and r["config"]["N"] == 10**9
+    assert r["config"]["n_per_gpu"] == 5 * 10**8 and r["scaling"] == "strong"
 
 
 def test_bench_driver_launch_form_two_ranks(cuda):
@@ -194,3 +197,28 @@ def test_riemann_parity_is_a_distributed_master_worker_run(cuda, world):
     for w in range(W):
         exact = math.cos(w * math.pi / W) - math.cos((w + 1) * math.pi / W)
         assert abs(parts[w + 1] - exact) < 1e-7
+
+
+def test_trainscan_replicate_ranks_share_gpu(cuda):
+    """trainscan --replicate under 2 RCCL ranks (4main.c:157): the 144 MB allgather leaves
+    both ranks with bitwise-equal copies that match the one-rank table within roundoff."""
+    one = _records([os.path.join(BIN, "trainscan"), "--replicate", "--json"])[0]
+    assert one["replicate"] and one["replicas_identical"] and one["replica_n"] == 18_000_000
+    two = _records(_np(2, os.path.join(BIN, "trainscan"), "--replicate", "--json"))[0]
+    _shared_rccl(two, 2)
+    assert two["replicas_identical"] is True and two["replica_n"] == 18_000_000
+    assert two["replica_sum"] == pytest.approx(one["replica_sum"], rel=1e-12)
+    for x, y in zip(two["replica_at"], one["replica_at"]):
+        assert x == pytest.approx(y, rel=1e-12, abs=1e-9)
+
+
+def test_miint_comm_ranks_share_gpu(cuda):
+    """miint comm as 2 RCCL processes on the one GPU: every collective size reports a time,
+    the transport is the sockets this setup uses, and the record names it."""
+    p = _proc(_np(2, os.path.join(BIN, "miint"), "comm", "--max-bytes", "1e6", "--iters", "3"))
+    assert p.returncode == 0, (p.stdout[-2000:], p.stderr[-2000:])
+    rows = [json.loads(l) for l in p.stdout.splitlines() if l.startswith("{")]
+    assert {r["op"] for r in rows} == {"allreduce", "allgather", "broadcast"}
+    for r in rows:
+        assert r["gpus"] == 2 and r["us"] > 0 and r["ranks_share_gpus"] is True
+        assert r["rccl_transport"].startswith("NET/Socket") and r["transport_verified"]

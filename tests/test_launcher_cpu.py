@@ -57,6 +57,13 @@ def test_agreed_failure_lets_rank0_finish():
                         'if [ "$RANK" = 0 ]; then sleep 0.5; echo record; fi; exit 3'],
                        capture_output=True, text=True, timeout=60)
     assert p.returncode == 3 and "record" in p.stdout
+    # with 3+ ranks, the 2nd and 3rd agreed exits during the linger must not stop
+    # the ranks still finishing — rank 0 exits last and its record is still printed
+    p = subprocess.run([RUN, "-np", "4", "--linger", "3", "sh", "-c",
+                        'if [ "$RANK" = 0 ]; then sleep 1; echo record; fi; '
+                        'if [ "$RANK" = 2 ]; then sleep 0.3; fi; exit 3'],
+                       capture_output=True, text=True, timeout=60)
+    assert p.returncode == 3 and "record" in p.stdout, p.stderr
     t = time.time()
     p = subprocess.run([RUN, "-np", "2", "--linger", "1", "--grace", "5", "sh", "-c",
                         'if [ "$RANK" = 1 ]; then exit 3; fi; sleep 60'],

@@ -30,7 +30,7 @@ def test_scale_sweep_one_gpu_row_matches_bench(native, cuda):
         else:
             assert r["verified"] and r["graphs"] and r["value"] > 1e12
     one = rows[0]
-    assert one["weak_eff"] == 1.0 and one["strong_eff"] == 1.0
+    assert one["strong_1e9_eff"] == 1.0 and one["weak_eff"] == 1.0 and one["strong_eff"] == 1.0
     assert one["allreduce_8B_us"] > 0 and one["allgather_144MB_us"] > 0
     b = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--steps", "200",
                         "--warmup", "10", "--no-extras"], cwd=REPO, capture_output=True,

@@ -94,7 +94,7 @@ def parse(argv=None) -> argparse.Namespace:
     p.add_argument("--dtype", default="fp64", choices=["fp64", "fp32", "fp32acc"],
                    help="fp32acc: fp32 samples AND fp32 accumulation to the workgroup partial "
                         "(pi4 only; fp32 folds tile values into fp64)")
-    p.add_argument("--div", default="series", choices=["series", "ieee", "series_direct", "series_exact"])
+    p.add_argument("--div", default="series_exact", choices=["series", "ieee", "series_direct", "series_exact"])
     p.add_argument("--comm", default="native", choices=["native", "torch"],
                    help="native: C++ RCCL communicator captured in the step graph; "
                         "torch: torch.distributed all_reduce of each step's partial")
@@ -400,8 +400,15 @@ def main(argv=None) -> int:
         rccl_version = native().Comm.version()
         if world > 1:
             transport = native().rccl_transport()
-    share = mdist.ranks_share_devices() and world > 1
-    transport_error = transport_check(world, share, transport, rccl=not cpu)
+    native_rccl = int(comm is not None and getattr(comm, "kind", "") == "rccl")
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    # ranks share GPUs: MIINT_OVERSUBSCRIBE, or simply more local ranks than devices (gloo
+    # rehearsals on one GPU map rank r to device r % count)
+    share = world > 1 and (mdist.ranks_share_devices() or
+                           (not cpu and local_world > torch.cuda.device_count()))
+    # the transport check applies only where RCCL carried the ranks' collectives
+    transport_error = transport_check(world, share, transport,
+                                      rccl=not cpu and bool(native_rccl or ctx.nccl_groups))
     if transport_error:
         print(f"bench.py: {transport_error}", file=sys.stderr)
     extras = {}
@@ -457,7 +464,7 @@ def main(argv=None) -> int:
             # the control plane (gloo unless --comm torch), torch RCCL groups counted here
             "control_plane": ctx.backend,
             "torch_nccl_groups": ctx.nccl_groups,
-            "native_rccl_comms": int(comm is not None and getattr(comm, "kind", "") == "rccl"),
+            "native_rccl_comms": native_rccl,
             # MIINT_OVERSUBSCRIBE: ranks share GPUs and RCCL runs over loopback sockets — a
             # correctness run of the multi-rank path, not a scaling number
             "ranks_share_gpus": share,
@@ -683,49 +690,75 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
                            "verified": result_ok("pi4", args.rule, args.dtype, n_total, e)}
         out["ieee_div_value"] = out["ieee_div"]["value"]
         del ie
-    # (2) per-point accuracy of the division the headline used, on one 64 K-sample window
-    #     of this rank's slice (rank 0's is reported)
+    # (2) per-point accuracy of the division the headline used, on two 64 K-sample windows of
+    #     this rank's slice (its first samples, and 1/8 in; rank 0's are reported): against
+    #     the IEEE path's own values, and against the true value 4/(1 + x^2) at the true
+    #     coordinate in x87 extended precision (profiles/r5/accuracy_ab.md)
     eff = str(integ.plan.effective_div).split(".")[-1]
-    i0 = integ.plan.begin + integ.plan.count // 8 + 12_345
-    w = min(1 << 16, integ.plan.begin + integ.plan.count - i0)
+    b0, cnt = integ.plan.begin, integ.plan.count
+    w = min(1 << 16, cnt)
+    windows = [b0, b0 + cnt // 8 + 12_345] if cnt >= 8 * w else [b0]
 
-    def ulps(div):  # |value - IEEE value| in ulps of the IEEE value, every point of the window
+    def ulps(div):  # every point of the windows: |value - reference| in ulps
+        import numpy as np
         import torch
 
-        v = kernels.point_values(integ.spec, n_total, rule=args.rule, div=div, i_begin=i0,
-                                 n_local=w)
-        r = kernels.point_values(integ.spec, n_total, rule=args.rule, div="ieee", i_begin=i0,
-                                 n_local=w)
-        spacing = torch.nextafter(r.abs(), torch.full_like(r, math.inf)) - r.abs()
-        u = ((v - r) / spacing).abs()
-        return {"max_ulp": float(u.max()),
-                "frac_within_1ulp": float((u <= 1.0).double().mean()),
-                "frac_within_2ulp": float((u <= 2.0).double().mean()),
-                "window": [int(i0), int(w)]}
+        u_all, t_all, per = [], [], []
+        h = np.longdouble(integ.spec.b - integ.spec.a) / np.longdouble(n_total)
+        off = {"left": 0.0, "mid": 0.5, "right": 1.0}[args.rule]
+        for i0 in windows:
+            v = kernels.point_values(integ.spec, n_total, rule=args.rule, div=div, i_begin=i0,
+                                     n_local=w)
+            r = kernels.point_values(integ.spec, n_total, rule=args.rule, div="ieee",
+                                     i_begin=i0, n_local=w)
+            spacing = torch.nextafter(r.abs(), torch.full_like(r, math.inf)) - r.abs()
+            u = ((v - r) / spacing).abs().cpu().numpy()
+            x = np.longdouble(integ.spec.a) + (np.arange(w, dtype=np.longdouble) +
+                                               np.longdouble(i0) + np.longdouble(off)) * h
+            true = np.longdouble(4) / (np.longdouble(1) + x * x)
+            t = np.abs((v.cpu().numpy().astype(np.longdouble) - true) /
+                       np.spacing(true.astype(np.float64)).astype(np.longdouble)).astype(np.float64)
+            u_all.append(u)
+            t_all.append(t)
+            per.append({"i0": int(i0), "max_ulp": float(u.max()), "vs_true_max_ulp": float(t.max()),
+                        "vs_true_mean_ulp": float(t.mean())})
+        u, t = np.concatenate(u_all), np.concatenate(t_all)
+        return {"max_ulp": float(u.max()), "frac_within_1ulp": float((u <= 1.0).mean()),
+                "frac_within_2ulp": float((u <= 2.0).mean()),
+                "vs_true_max_ulp": float(t.max()), "vs_true_mean_ulp": float(t.mean()),
+                "vs_true_frac_within_1ulp": float((t <= 1.0).mean()),
+                "window": [int(windows[-1]), int(w)], "windows": per}
 
+    # per-point bounds against the IEEE path's values: series_exact is exact-grade (within 2,
+    # both sides round), the g-fold of series within 5
+    bound = {"series_exact": 2.0}.get(eff, 5.0)
     if pi4 and args.dtype == "fp64" and eff != "ieee":
         pp = ulps(eff)
-        out["per_point"] = dict(pp, bound_max_ulp=5.0, verified=bool(pp["max_ulp"] <= 5.0))
+        out["per_point"] = dict(pp, division=eff, bound_max_ulp=bound,
+                                verified=bool(pp["max_ulp"] <= bound))
         out["per_point_max_ulp"] = out["per_point"]["max_ulp"]
         out["per_point_frac_within_1ulp"] = out["per_point"]["frac_within_1ulp"]
+        out["per_point_vs_true_max_ulp"] = out["per_point"]["vs_true_max_ulp"]
         out["per_point_window"] = out["per_point"]["window"]
-    # (2b) the same config with the series' residuals kept at their own precision
-    #      (div series_exact: 3.5 VALU per sample instead of 2.5): per point within ~1 ulp of
-    #      IEEE division, where the headline's g = 1/2 + e fold is within 5 — what the
-    #      headline's per-point accuracy costs in speed (profiles/r4/accuracy_ab.md)
-    if pi4 and args.dtype == "fp64" and args.div == "series":
-        ex = Integrator(args.integrand, n=n_total, div="series_exact", **kw)
+    # (2b) the same config with the other series form: under the default series_exact
+    #      headline (per point as accurate as IEEE division), the g = 1/2 + e fold ("series":
+    #      one square per sample rounded at ulp(1/2), up to 5 ulp per point) — what the
+    #      headline's exact-grade points cost in speed; under --div series, series_exact.
+    if pi4 and args.dtype == "fp64" and args.div in ("series", "series_exact"):
+        alt = "series" if args.div == "series_exact" else "series_exact"
+        ex = Integrator(args.integrand, n=n_total, div=alt, **kw)
         steps = 48
         ms = _timed_steps(ctx, ex.plan, steps, pipeline, dev)
         v = ex.plan.host_result(ex.plan.host_index_of(steps - 1, True))
         e = abs(v - math.pi)
-        pp = ulps("series_exact")
-        out["series_exact_div"] = {
+        ab = {"series_exact": 2.0}.get(alt, 5.0)
+        pp = ulps(alt)
+        out[f"{alt}_div"] = {
             "value": n_total / (ms * 1e-3), "ms_per_step": ms, "steps": steps, "result": v,
             "abs_err": e, "division": str(ex.plan.effective_div).split(".")[-1],
-            "per_point": dict(pp, bound_max_ulp=2.0),
+            "per_point": dict(pp, bound_max_ulp=ab),
             "verified": bool(result_ok("pi4", args.rule, args.dtype, n_total, e) and
-                             pp["max_ulp"] <= 2.0)}
+                             pp["max_ulp"] <= ab)}
         del ex
     # (3) the headline config in its other scaling form. Strong headline (the default: N = 1e9
     #     IN TOTAL, riemann.cpp:10,71-73): the weak form, 1e9 samples PER GPU (N = 1e9 x G,

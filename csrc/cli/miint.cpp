@@ -2,7 +2,7 @@
 //
 //   ./miint info
 //   ./miint bench [--integrand pi4] [--n 1e9] [--dtype fp64] [--rule left] [--iters 200]
-//                 [--gpus G] [--div series|ieee] [--unfused] [--no-graph]      (JSON lines)
+//                 [--gpus G] [--div series_exact|series|ieee] [--unfused] [--no-graph]      (JSON lines)
 //   ./miint sweep [--gpus G]     N in {1e6,1e9,1e10} x dtype {fp64,fp32} x integrand
 //   ./miint table2d [--grid 4096] [--gpus G] [--slice R/W] [--no-graph]
 //                                2-D velocity-field integral (BASELINE #5); timed as
@@ -230,7 +230,7 @@ int comm_sweep(const cli::Args& a, const cli::Topology& topo, double max_bytes, 
 constexpr const char* kUsage =
     "usage: miint info\n"
     "       miint bench [--integrand pi4] [--n 1e9] [--dtype fp64|fp32|fp32acc] [--rule left]\n"
-    "                   [--iters 200] [--gpus G] [--div series|ieee] [--unfused] [--no-graph]\n"
+    "                   [--iters 200] [--gpus G] [--div series_exact|series|ieee] [--unfused] [--no-graph]\n"
     "                   [--block B] [--grid G] [--step-streams S] [--trig-library] [--settle N]\n"
     "                   [--no-multistep] [--slots K]\n"
     "       miint sweep [--gpus G]\n"
@@ -264,7 +264,7 @@ int main(int argc, char** argv) {
     const bool graphs = !a.flag("no-graph");
     if (cmd == "bench") {
       RiemannConfig c = make_cfg(a.str("integrand", "pi4"), a.num("n", 1e9), a.str("dtype", "fp64"),
-                                 a.str("rule", "left"), a.str("div", "series"));
+                                 a.str("rule", "left"), a.str("div", "series_exact"));
       c.fused = !a.flag("unfused");
       c.grid = static_cast<int>(a.integer("grid", 0));
       c.block = static_cast<int>(a.integer("block", kRiemannBlock));

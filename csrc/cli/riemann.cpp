@@ -207,7 +207,7 @@ int run_expr(const cli::Args& a, const RiemannConfig& cfg, double nd, int iters)
 
 constexpr const char* kUsage =
     "usage: riemann [--n 1e9] [--gpus G] [--loopback W] [--integrand sin|pi4|poly|train|table]\n"
-    "               [--rule left|mid|right] [--dtype fp64|fp32|fp32acc] [--div series|ieee]\n"
+    "               [--rule left|mid|right] [--dtype fp64|fp32|fp32acc] [--div series_exact|series|ieee]\n"
     "               [--iters K] [--block 64..1024] [--grid G] [--a A --b B] [--parity]\n"
     "               [--one-shot | --no-one-shot] [--no-multistep] [--unfused]\n"
     "               [--json] [--jsonl FILE] [--profile FILE]\n"
@@ -244,7 +244,7 @@ int main(int argc, char** argv) {
     cfg.n = n;
     cfg.rule = cli::parse_rule(a.str("rule", "left"));
     cfg.dtype = cli::parse_dtype(a.str("dtype", "fp64"));
-    cfg.div = cli::parse_div(a.str("div", "series"));
+    cfg.div = cli::parse_div(a.str("div", "series_exact"));
     cfg.fused = !a.flag("unfused");
     cfg.multistep = !a.flag("no-multistep");  // chained batches, full auto grid
     // --block: threads per workgroup (the reference's SP, cintegrate.cu:17-18); --grid:

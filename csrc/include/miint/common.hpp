@@ -60,12 +60,16 @@ enum class Rule : int { kLeft = 0, kMid = 1, kRight = 2 };
 
 // How the Pi4 kernels divide (see integrands.hpp for the derivation):
 //   kSeries        per-tile v_rcp_f64 seed, per-sample exact residual e = 1 - d*s evaluated
-//                  pairwise from the tile midpoint, 1/d = s(1+e+e^2)   (default, 3.5 ops)
+//                  pairwise from the tile midpoint, 1/d = s(3/4 + g^2), g = 1/2 + e
+//                  (2.65 VALU per sample; per point up to 4 ulp from the true value)
 //   kIeee          correctly rounded division for every sample (reference path)
 //   kSeriesDirect  the same series with x, d formed explicitly per sample (5 ops; A/B)
-//   kSeriesExact   kSeries's residuals without the g = 1/2 + e fold: each sample accumulates
-//                  e + e^2 at e's own precision (3.5 ops; per-point within 1 ulp of IEEE
-//                  division where kSeries is within 5) — the accuracy A/B of the headline
+//   kSeriesExact   kSeries's residuals without the g = 1/2 + e fold: each sample's value is
+//                  s (1 + e + e^2) at e's own precision, the seed residual from the exact
+//                  d_m (2.68 VALU per sample; per point max 1.34 ulp / mean 0.27 ulp from the
+//                  true value, where IEEE division per sample is 1.57 / 0.45): the headline
+//                  division since round 5 (profiles/r5/accuracy_ab.md). For the other
+//                  integrands (and fp32) it selects their series path.
 enum class DivMode : int { kSeries = 0, kIeee = 1, kSeriesDirect = 2, kSeriesExact = 3 };
 
 inline double rule_offset(Rule r) {

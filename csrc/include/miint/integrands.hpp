@@ -94,6 +94,10 @@ struct Pi4 : TileDefaults<Pi4> {
   // 192 deals 9.93 tiles per lane of the 2048 x 256 grid, as even as 128's 14.9).
   static constexpr int kSubs = 6;
   static constexpr int kSeriesTile = kSub * kSubs;  // 192 samples per seed
+  // sum over a series tile's samples of k_u^2, k_u = u - (U-1)/2: 2 sum_{j<U/2} (j + 1/2)^2
+  static constexpr double kSumK2 = (kSeriesTile / 2) * (kSeriesTile / 2 - 1) * (kSeriesTile - 1) / 3.0 +
+                                   (kSeriesTile / 2) * (kSeriesTile / 2 - 1) + kSeriesTile / 4.0;
+  static_assert(kSumK2 == 589808.0, "sum of squared midpoint offsets of a 192-sample tile");
 
   template <DivMode M>
   __host__ __device__ static constexpr int tile_len() {
@@ -236,15 +240,30 @@ struct Pi4 : TileDefaults<Pi4> {
 
   // kSeriesExact: the same seed, centres and per-sample residuals as kSeries, without the
   // 1/2 offset — e_c = e_m + c0 A + (c0^2 + kMeanK2) B, e_{+-k} = e_c + (k^2 - kMeanK2) B
-  // +- k A' — and every sample accumulates f = e + e^2 = fma(e, e, e) at e's own precision
-  // (|e| <= 2e-6: its rounding is ~1e-22 absolute), so the point's value s + s f is rounded
-  // once, where kSeries's g = 1/2 + e rounds every sample at ulp(1/2) (up to 5 ulp from IEEE
-  // division). Per pair: c, e+-, f+- and two adds = 3.5 VALU per sample against kSeries's 2.5:
-  // +37 % time at N = 1e9 (profiles/r4/accuracy_ab.md).
+  // +- k A' — and every sample's value is s (1 + e + e^2) at e's own precision (|e| <= 2e-6:
+  // its rounding is ~1e-22 absolute), rounded once, where kSeries's g = 1/2 + e rounds every
+  // sample at ulp(1/2) (up to 5 ulp from IEEE division).
+  // Cost (round 5): each sample forms its own residual e+-k and adds its
+  // own e^2 with one fma, exactly as kSeries forms g+-k and adds g^2 (whose square carries
+  // the linear term g^2 = 1/4 + e + e^2). The residuals' LINEAR terms are not added sample by
+  // sample: over the tile, e_u = e_m + k_u A + k_u^2 B with offsets k_u = u - (U-1)/2
+  // symmetric about the midpoint, so sum_u e_u = U e_m + B sum_u k_u^2 exactly (the A terms
+  // cancel) — one fma per tile, exact where per-sample adds would round. Per pair: c, e+, e-,
+  // two fma = 2.5 VALU per sample, kSeries's count (the first form, f = fma(e, e, e) and
+  // t += f per sample, was 3.5: +37 % time).
+  // The seed's residual e_m = 1 - (1 + x_m^2) s is formed from the exact d_m (x_m s split
+  // into q + qe by an fma): from the rounded d_m = fma(x_m, x_m, 1) it carried d_m's
+  // rounding (up to ulp(1)/2 relative) into every sample of the tile — the 1.49-ulp maximum
+  // near x = 0 of round 4 (profiles/r4/accuracy_ab.md).
   __device__ __forceinline__ Seed seed_exact(double xm, double h) const {
     const double dm = fma(xm, xm, 1.0);
     const double s = __builtin_amdgcn_rcp(dm);
-    return {s, fma(-dm, s, 1.0), (-2.0 * h) * xm * s, -(h * h) * s};
+    const double q = xm * s;
+    const double qe = fma(xm, s, -q);  // xm s = q + qe exactly
+    // 1 - s is exact for s in [1/2, 2] (d in [1/2, 2]: x in [0, 1]); elsewhere the rounding
+    // is no worse than 1 - d_m s's
+    const double em = fma(-xm, qe, fma(-xm, q, 1.0 - s));
+    return {s, em, (-2.0 * h) * xm * s, -(h * h) * s};
   }
 
   template <int U, DivMode M>
@@ -279,7 +298,8 @@ struct Pi4 : TileDefaults<Pi4> {
       static_assert(U == kSeriesTile, "series tiles are kSubs sub-tiles of kSub samples");
       const Seed sd = seed_exact(xa, h);
       const double b2 = 2.0 * sd.b;
-      double t = 0.0;  // sum of e + e^2 over the tile (|t| <= 4e-4: ulp ~5e-20)
+      // sum_u e_u (U e_m + B sum k^2), then every sample's e^2 on top (|t| <= ~1e-12)
+      double t = fma(kSumK2, sd.b, static_cast<double>(U) * sd.em);
 #pragma unroll
       for (int q = 0; q < kSubs; ++q) {
         const double ec = centre_g(sd, q);         // e at the centre (+ mean k^2 B)
@@ -287,14 +307,14 @@ struct Pi4 : TileDefaults<Pi4> {
 #pragma unroll
         for (int j = 0; j < kPairs; ++j) {
           const double c = fma(pk2[j], sd.b, ec);
-          const double ep = fma(pk[j], a, c);
-          const double en = fma(-pk[j], a, c);
-          t += fma(ep, ep, ep);
-          t += fma(en, en, en);
-          asm volatile("" : "+v"(t));
+          const double ep = fma(pk[j], a, c);   // sample kSub/2 + j's residual
+          const double en = fma(-pk[j], a, c);  // sample kSub/2 - 1 - j's
+          t = fma(ep, ep, t);
+          t = fma(en, en, t);
+          asm volatile("" : "+v"(t));  // program order, as kSeries
         }
       }
-      // U samples of s (1 + f): s U + s t
+      // U samples of s (1 + e + e^2): s U + s (sum e + sum e^2)
       return fma(sd.s, t, fma(sd.s, static_cast<double>(U), acc));
     } else {
       return acc + tile<U, M>(xa, h);

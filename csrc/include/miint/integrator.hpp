@@ -52,7 +52,7 @@ struct RiemannConfig {
   uint64_t n = 1000000000ull;  // total samples over all ranks
   Rule rule = Rule::kLeft;
   DType dtype = DType::kF64;
-  DivMode div = DivMode::kSeries;
+  DivMode div = DivMode::kSeriesExact;  // exact-grade per point (common.hpp); --div series: the g-fold
   std::vector<double> coef;    // Integrand::kPoly
   double p0 = 0.0, p1 = 0.0;   // Integrand::kTrainVel (ts, vs)
   std::vector<double> table;   // Integrand::kTable (host copy, uploaded once)

@@ -42,10 +42,12 @@ inline DivMode effective_div(DivMode d, double h) {
 }
 // Per integrand: the sin / train-velocity series path (angle addition from a per-tile sincos
 // seed) and the table's segment-line tiles are exact for any h, so only the series/ieee
-// choice applies; integrands without a series path run kIeee.
+// choice applies (kSeriesExact, the exact-grade request, is their series path); integrands
+// without a series path run kIeee.
+inline bool series_request(DivMode d) { return d == DivMode::kSeries || d == DivMode::kSeriesExact; }
 inline DivMode effective_div(DivMode d, double h, Integrand f) {
   if (f == Integrand::kSin || f == Integrand::kTrainVel || f == Integrand::kTable)
-    return d == DivMode::kSeries ? DivMode::kSeries : DivMode::kIeee;
+    return series_request(d) ? DivMode::kSeries : DivMode::kIeee;
   if (f != Integrand::kPi4) return DivMode::kIeee;
   return effective_div(d, h);
 }
@@ -64,8 +66,8 @@ inline DivMode effective_div(DivMode d, double h, Integrand f, DType t, int ncoe
       return (ncoef >= 1 && ncoef <= kPolySeriesMaxCoeffs) ? DivMode::kSeries : DivMode::kIeee;
     return DivMode::kSeries;  // sin, train velocity, table: exact for any h
   }
-  if (f == Integrand::kPoly)
-    return (d == DivMode::kSeries && ncoef >= 1 && ncoef <= kPolySeriesMaxCoeffs)
+  if (f == Integrand::kPoly)  // the Taylor-pair tiles are exact-grade: kSeriesExact runs them
+    return (series_request(d) && ncoef >= 1 && ncoef <= kPolySeriesMaxCoeffs)
                ? DivMode::kSeries
                : DivMode::kIeee;
   return effective_div(d, h, f);

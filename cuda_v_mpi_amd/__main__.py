@@ -289,7 +289,7 @@ def main(argv=None) -> int:
         sp.add_argument("--n", type=float, default=1e9)
         sp.add_argument("--rule", default="left", choices=["left", "mid", "right"])
         sp.add_argument("--dtype", default="fp64", choices=["fp64", "fp32", "fp32acc"])
-        sp.add_argument("--div", default="series", choices=["series", "ieee", "series_direct", "series_exact"])
+        sp.add_argument("--div", default="series_exact", choices=["series", "ieee", "series_direct", "series_exact"])
         sp.add_argument("--block", type=int, default=256, choices=[64, 128, 256, 512, 1024],
                         help="threads per workgroup (the reference's SP)")
         sp.add_argument("--backend", default="hip", choices=["hip", "host", "cpu"])

@@ -65,7 +65,7 @@ class IntegrationResult:
 
 class Integrator:
     def __init__(self, integrand: str | integrands.IntegrandSpec = "pi4", n: int = 10**9,
-                 rule: str = "left", dtype: str = "fp64", div: str = "series",
+                 rule: str = "left", dtype: str = "fp64", div: str = "series_exact",
                  backend: str = "hip", ctx: DistContext | None = None, comm: str = "native",
                  fused: bool = True, grid: int = 0, slots: int = 16, a: float | None = None,
                  b: float | None = None, force_collective: bool = False, bucket: bool = True,

@@ -49,7 +49,7 @@ def default_grid() -> int:
 
 
 def riemann_partials(spec: IntegrandSpec, n: int, rule: str = "left", dtype: str = "fp64",
-                     div: str = "series", grid: int | None = None, i_begin: int = 0,
+                     div: str = "series_exact", grid: int | None = None, i_begin: int = 0,
                      n_local: int | None = None) -> torch.Tensor:
     """Per-workgroup unscaled partial sums of f over samples [i_begin, i_begin+n_local)."""
     m = native()
@@ -109,7 +109,7 @@ class FusedWorkspace:
 
 
 def riemann(spec: IntegrandSpec, n: int, rule: str = "left", dtype: str = "fp64",
-            div: str = "series", grid: int | None = None, i_begin: int = 0,
+            div: str = "series_exact", grid: int | None = None, i_begin: int = 0,
             n_local: int | None = None, out: torch.Tensor | None = None,
             workspace: FusedWorkspace | None = None, fused: bool = True) -> torch.Tensor:
     """h * scale * sum f over this launch's samples, as a 1-element fp64 device tensor."""

@@ -22,7 +22,7 @@ from .dist import DistContext
 
 class TorchStepper:
     def __init__(self, spec: IntegrandSpec, n_total: int, ctx: DistContext, rule: str = "left",
-                 dtype: str = "fp64", div: str = "series", grid: int | None = None,
+                 dtype: str = "fp64", div: str = "series_exact", grid: int | None = None,
                  capacity: int = 4096, group=None):
         self.spec, self.n, self.ctx = spec, int(n_total), ctx
         self.rule, self.dtype, self.div = rule, dtype, div

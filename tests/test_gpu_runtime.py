@@ -55,14 +55,14 @@ def test_chained_batches_equal_fused_bitwise(cuda, name, collective):
 
 
 @pytest.mark.parametrize("name", ["pi4", "pi4_fp32", "pi4_fp32acc", "sin", "poly", "train",
-                                  "sin_ieee", "pi4_fp32_ieee"])
+                                  "sin_ieee", "pi4_fp32_ieee", "pi4_exact"])
 def test_multistep_batches_equal_chained_bitwise(cuda, name):
     """A graph batch as ONE persistent multi-step launch + a closing kernel (workgroups rotate
     over virtual blocks from step to step) gives every step the chained batch's value, bit for
     bit: 47 steps = two 20-step replays + a 7-step one, and 1-step batches."""
     parts = name.split("_")
     dtype = parts[1] if len(parts) > 1 and parts[1].startswith("fp") else "fp64"
-    div = "ieee" if name.endswith("_ieee") else "series"
+    div = {"ieee": "ieee", "exact": "series_exact"}.get(parts[-1], "series")
     kw = dict(n=60_000_011, rule="mid", dtype=dtype, div=div)
     ms = Integrator(parts[0], slots=20, **kw)
     ch = Integrator(parts[0], slots=20, multistep=False, grid=ms.plan.grid, **kw)
@@ -477,7 +477,11 @@ def test_bench_contract(native, cuda):
     assert js["config"]["graphs"] is True
     # the record carries what the headline rests on: IEEE-division speed and per-point ulp
     assert js["ieee_div_value"] > 1e11 and js["ieee_div"]["abs_err"] < 2e-9
-    assert js["per_point_max_ulp"] <= 5.0
+    # the headline division (series_exact): per point within 2 ulp of the IEEE path's own
+    # values, within 1.5 of the true value; the faster g-fold (series) rides along as an extra
+    assert js["config"]["division"] == "series_exact" and js["per_point"]["division"] == "series_exact"
+    assert js["per_point_max_ulp"] <= 2.0 and js["per_point_vs_true_max_ulp"] <= 1.5
+    assert js["series_div"]["verified"] and js["series_div"]["per_point"]["max_ulp"] <= 5.0
     b3 = js["baseline3_strong_1e10"]
     assert b3["N"] == 10**10 and abs(b3["abs_err"] - 1e-10) < 1e-13 and b3["value"] > 1e11
     assert js["rccl_version"] and js["per_rank_ms"] and js["launcher"] == "single"
@@ -686,5 +690,7 @@ def test_cli_riemann_reports_one_shot(cli_built):
     p = _run([os.path.join(cli_built, "riemann"), "--integrand", "pi4", "--json", "--iters", "20"])
     assert p.returncode == 0, p.stderr
     js = json.loads(p.stdout.strip().splitlines()[-1])
-    assert js["ms_one_shot"] > js["device_ms"] * 0.9 and js["ms_one_shot"] < 5.0
+    # the one-shot is timed after 400 settling calls, the 20 steps from a cold clock (~25 ms
+    # of ramp, profiles/r4/oneshot_trace.md): the same order, not the same clock
+    assert js["ms_one_shot"] > js["device_ms"] * 0.6 and js["ms_one_shot"] < 5.0
     assert js["comm"] == "none" and js["rccl_world"] == 0 and js["ranks_share_gpus"] is False

@@ -35,7 +35,9 @@ def main() -> int:
     n = 10**9
     steps = 48
     spec = Integrator("pi4", n=n, backend="cpu").spec
-    windows = [int(f * n) + 12_345 for f in (0.01, 0.3, 0.6, 0.95)]
+    # the window at x = 0 (values just under 4: where 1 + x^2 rounds least, round 4's worst
+    # for series_exact) and four spread across [0, 1]
+    windows = [0] + [int(f * n) + 12_345 for f in (0.01, 0.3, 0.6, 0.95)]
     w = 1 << 16
     ref = {i0: kernels.point_values(spec, n, rule="left", div="ieee", i_begin=i0, n_local=w)
            for i0 in windows}
@@ -57,6 +59,7 @@ def main() -> int:
         hist = {"<=0.5": 0, "<=1": 0, "<=2": 0, "<=3": 0, "<=5": 0, ">5": 0}
         umax, total = 0.0, 0
         tmax, tsum, t1 = 0.0, 0.0, 0
+        per_window = []
         for i0 in windows:
             val = kernels.point_values(spec, n, rule="left", div=div, i_begin=i0, n_local=w)
             tv = truth[i0]
@@ -64,6 +67,8 @@ def main() -> int:
                         np.spacing(tv.astype(np.float64)).astype(np.longdouble)).astype(np.float64)
             tmax = max(tmax, float(ut.max()))
             tsum += float(ut.sum())
+            per_window.append({"i0": i0, "x0": i0 / n, "vs_true_max_ulp": float(ut.max()),
+                               "vs_true_mean_ulp": float(ut.mean())})
             t1 += int((ut <= 1.0).sum())
             r = ref[i0]
             spacing = torch.nextafter(r.abs(), torch.full_like(r, math.inf)) - r.abs()
@@ -85,7 +90,7 @@ def main() -> int:
             "points": total, "max_ulp": umax, "frac_within_1ulp": cum1,
             "frac_within_2ulp": cum2, "ulp_hist": hist,
             "vs_true_max_ulp": tmax, "vs_true_mean_ulp": tsum / total,
-            "vs_true_frac_within_1ulp": t1 / total}), flush=True)
+            "vs_true_frac_within_1ulp": t1 / total, "windows": per_window}), flush=True)
         del it, p
     return 0
 

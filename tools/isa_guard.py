@@ -41,6 +41,7 @@ MS = r"riemann_multistep_kernel(?:_o8)?ILNS_7DivModeE"
 GUARDED = {
     "pi4_series": ("riemann", CH + r"0ENS_3Pi4EE", 192),
     "pi4_ieee": ("riemann", CH + r"1ENS_3Pi4EE", 32),
+    "pi4_series_exact": ("riemann", CH + r"3ENS_3Pi4EE", 192),
     "sin_series": ("riemann", CH + r"0ENS_3SinEE", 192),
     "sin_ieee": ("riemann", CH + r"1ENS_3SinEE", 32),
     "train_series": ("riemann", CH + r"0ENS_8TrainVelEE", 128),
@@ -52,6 +53,7 @@ GUARDED = {
     # the multi-step kernels (graph batches by default): the hot loop found is the step loop
     # around a tile, so no per-sample figure; max_block_valu is one tile's straight line
     "ms_pi4_series": ("riemann", MS + r"0ENS_3Pi4EE", 0),
+    "ms_pi4_series_exact": ("riemann", MS + r"3ENS_3Pi4EE", 0),
     "ms_pi4f32_series": ("riemann", MS + r"0ENS0_6Pi4F32EE", 0),
     "ms_sin_series": ("riemann", MS + r"0ENS_3SinEE", 0),
     "ms_sin_ieee": ("riemann", MS + r"1ENS_3SinEE", 0),

@@ -362,6 +362,12 @@ def main(argv=None) -> int:
     g0 = plan.graph_launches if plan is not None else 0
     d0 = plan.direct_steps if plan is not None else 0
     ctx.barrier()
+    if plan is not None and not cpu:
+        # then a device barrier through the rank's RCCL communicator (an 8-byte all-reduce on
+        # the compute stream, polled): ranks leave a host barrier up to tens of us apart,
+        # and the early ones would count that skew as step time inside the batch's
+        # all-reduce; an all-reduce completes on every rank within ~us (no-op on one GPU)
+        plan.barrier()
     sync_dev()
     t0 = time.perf_counter()
     launch(args.steps)
@@ -593,6 +599,7 @@ def _timed_steps(ctx, plan, steps, pipeline, dev) -> float:
         plan.launch_steps(steps, pipeline, True)
     plan.sync()
     ctx.barrier()
+    plan.barrier()  # device barrier (see main's timed region)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     plan.launch_steps(steps, pipeline, True)

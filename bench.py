@@ -533,7 +533,9 @@ def transport_check(world: int, share: bool, transport: dict, rccl: bool = True)
         where = (transport or {}).get("log") or "no RCCL log captured"
         return (f"RCCL transport unknown between {world} ranks on distinct local GPUs (no peer "
                 f"connection in {where}): P2P over xGMI cannot be confirmed")
-    if transport.get("uses_net"):
+    if transport.get("uses_net") or not all(t.startswith("P2P")
+                                            for t in transport["transport"].split("+")):
+        # a network transport, or shared host memory (SHM: P2P disabled) — not xGMI
         return (f"RCCL transport is {transport['transport']} (nNodes {transport.get('nnodes')}) "
                 f"between {world} ranks on distinct local GPUs: expected P2P over xGMI")
     if transport.get("nnodes", 1) not in (0, 1):

@@ -208,7 +208,8 @@ void capture_rccl_log() {
   }
   const char* sub = std::getenv("NCCL_DEBUG_SUBSYS");
   if (!sub || !*sub) {
-    ::setenv("NCCL_DEBUG_SUBSYS", "INIT", 1);
+    // the peer-connection lines ("... via P2P/IPC") are INIT|P2P / INIT|NET messages
+    ::setenv("NCCL_DEBUG_SUBSYS", "INIT,P2P", 1);
   } else if (sub[0] != '^' && !std::strstr(sub, "INIT") && !std::strstr(sub, "ALL")) {
     ::setenv("NCCL_DEBUG_SUBSYS", (std::string(sub) + ",INIT").c_str(), 1);
   }
@@ -222,7 +223,16 @@ std::string transport_error(const RcclTransport& t, int world, int local_world, 
            " ranks on distinct local GPUs (no peer connection in " +
            (t.log.empty() ? std::string("no RCCL log captured") : t.log) +
            "): P2P over xGMI cannot be confirmed";
-  if (t.uses_net())
+  // every connection P2P: a network transport or shared host memory (SHM: P2P disabled) is
+  // not xGMI
+  bool all_p2p = true;
+  for (size_t p = 0; p <= t.transport.size();) {
+    size_t q = t.transport.find('+', p);
+    if (q == std::string::npos) q = t.transport.size();
+    all_p2p = all_p2p && t.transport.compare(p, 3, "P2P") == 0 && q - p >= 3;
+    p = q + 1;
+  }
+  if (t.uses_net() || !all_p2p)
     return "RCCL transport is " + t.transport + " (nNodes " + std::to_string(t.nnodes) +
            ") between " + std::to_string(world) +
            " ranks on distinct local GPUs: expected P2P over xGMI";

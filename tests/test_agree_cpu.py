@@ -80,6 +80,10 @@ def test_transport_check(native, monkeypatch):
     assert bench.transport_check(8, True, {}) is None
     assert bench.transport_check(1, False, {}) is None
     assert bench.transport_check(8, False, {}, rccl=False) is None
+    # shared host memory between ranks on distinct GPUs (P2P disabled) is not xGMI either
+    shm = native.parse_rccl_log(P2P_LOG.replace("via P2P/IPC", "via SHM/direct/direct"))
+    assert shm["transport"].startswith("SHM") and not shm["uses_net"]
+    assert "expected P2P" in bench.transport_check(8, False, shm)
     # a multi-node job legitimately crosses nodes over the network
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
     assert bench.transport_check(2, False, net) is None
@@ -126,4 +130,7 @@ def test_native_transport_error_matches_bench(native):
         cc = native.transport_error(text, world, local, share)
         assert (py is None) == (cc == ""), (text[:40], world, local, share, py, cc)
     assert "transport unknown" in native.transport_error("", 8, 8, False)
+    shm_log = P2P_LOG.replace("via P2P/IPC", "via SHM/direct/direct")
+    assert "expected P2P" in native.transport_error(shm_log, 8, 8, False)
+    assert native.transport_error(P2P_LOG, 8, 8, False) == ""
     assert "expected P2P" in native.transport_error(NET_LOG, 2, 2, False)

@@ -32,9 +32,9 @@ count instead). The results of the last batch of timed steps (every rank holds t
 sums) are checked on the host against the rule's closed-form truncation error. After the timed
 region (outside it) the same ranks also measure, each with its own graphs, timing and
 pass/fail ("verified"): the weak-scaling form, 1e9 samples PER GPU (N = 1e9 x G,
-"weak_1e9_per_gpu"); the same config with IEEE division per sample ("ieee_div"); the series
-path's per-point error against IEEE division on a 64 K-sample window ("per_point"); and the
-other BASELINE configs: #1, the serial CPU sum at N = 1e6 on one host thread
+"weak_1e9_per_gpu"); the same config with IEEE division per sample ("ieee_div"); the headline
+division's per-point error against IEEE division and against the true value on two 64 K-sample
+windows ("per_point"); and the other BASELINE configs: #1, the serial CPU sum at N = 1e6 on one host thread
 ("baseline1_serial_cpu_1e6"); #3, N = 1e10 in total strong-scaled over the same GPUs
 ("baseline3_strong_1e10"); #4, the same integral through the packed-fp32 path
 ("baseline4_fp32", tile values folded in fp64, and "baseline4_fp32_accum32", fp32 accumulation
@@ -42,7 +42,7 @@ to the workgroup partial); #5, the 4096^2 2-D velocity field with its rows split
 GPUs ("baseline5_table2d_4096") — and the same integral on the node's host cores (the native
 host engine, the reference's own CPU/MPI side: "host_engine"). Also: one integration per call,
 launch to pinned result, the reference's own timing unit ("single_shot_1e9"); the headline
-config with the series' residuals at their own precision ("series_exact_div"); and the
+config with the faster g = 1/2 + e series fold (up to 5 ulp per point: "series_div"); and the
 reference's own integrands through the same batches ("integrand_sin", "integrand_train",
 "integrand_table", "integrand_poly"). The record's "verified" is the AND of the headline's,
 every extra's and the RCCL transport check ("transport_verified": ranks of one node on distinct
@@ -713,7 +713,8 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
         import torch
 
         u_all, t_all, per = [], [], []
-        h = np.longdouble(integ.spec.b - integ.spec.a) / np.longdouble(n_total)
+        # the kernels' own step (fp64 (b - a) / N) and the true coordinate a + (i + off) h
+        h = np.longdouble(float((integ.spec.b - integ.spec.a) / n_total))
         off = {"left": 0.0, "mid": 0.5, "right": 1.0}[args.rule]
         for i0 in windows:
             v = kernels.point_values(integ.spec, n_total, rule=args.rule, div=div, i_begin=i0,

@@ -485,6 +485,17 @@ PYBIND11_MODULE(_miint, m) {
                       c.algo = scan_algo_of(s);
                     });
   m.def("trainscan_workspace_bytes", &trainscan_workspace_bytes);
+  // the --replicate fingerprint (host code): FNV-1a over the fp64 bits, compensated sum,
+  // elements at 0, n/4, n/2, 3n/4, n-1
+  m.def("replica_digest", [](const std::vector<double>& v) {
+    const ReplicaDigest d = digest_table(v.data(), v.size());
+    py::dict r;
+    r["hash"] = d.hash;
+    r["n"] = d.n;
+    r["sum"] = d.sum;
+    r["at"] = std::vector<double>(d.at, d.at + 5);
+    return r;
+  });
 
   // ------------------------------------------------------------------ 2-D field plan
   py::class_<Table2DPlan>(m, "Table2DPlan")

@@ -8,6 +8,7 @@ same (a rank made slow with MIINT_FAULT_RANK / MIINT_FAULT_DELAY_MS, miint/fault
 from __future__ import annotations
 
 import json
+import math
 import os
 import subprocess
 import sys
@@ -134,3 +135,24 @@ def test_native_transport_error_matches_bench(native):
     assert "expected P2P" in native.transport_error(shm_log, 8, 8, False)
     assert native.transport_error(P2P_LOG, 8, 8, False) == ""
     assert "expected P2P" in native.transport_error(NET_LOG, 2, 2, False)
+
+
+def test_replica_digest(native):
+    """trainscan --replicate's per-rank fingerprint (runtime/trainscan.cpp digest_table): FNV-1a
+    64 over the little-endian bytes of every double, a compensated sum, and the elements at
+    0, n/4, n/2, 3n/4, n-1 — equal hashes iff bitwise-equal copies."""
+    import struct
+
+    v = [math.sin(0.001 * i) * 1e5 for i in range(10_001)]
+    h = 1469598103934665603
+    for x in v:
+        for byte in struct.pack("<d", x):
+            h = ((h ^ byte) * 1099511628211) & (2**64 - 1)
+    d = native.replica_digest(v)
+    assert d["hash"] == h and d["n"] == len(v)
+    assert d["sum"] == math.fsum(v)
+    n = len(v)
+    assert d["at"] == [v[0], v[n // 4], v[n // 2], v[3 * (n // 4)], v[n - 1]]
+    w = list(v)
+    w[5000] = math.nextafter(w[5000], math.inf)  # one ulp anywhere changes the hash
+    assert native.replica_digest(w)["hash"] != h

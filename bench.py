@@ -803,8 +803,10 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
         del st
     # (5) BASELINE config #5: the 2-D field v(x) v(y) from the velocity profile, 4096^2
     #     bilinear midpoint samples, sample rows split over the same GPUs; one integration =
-    #     one fused kernel per rank, the partials of a 32-integration graph replay meeting in
-    #     one RCCL all-reduce (Table2DPlan) on the shared communicator
+    #     one multi-step launch per graph replay of p2.graph_steps integrations (128 for the
+    #     whole field, up to 1024 for a small row share: a replay holds >= 2^31 samples), the
+    #     replay's per-integration partials meeting in one RCCL all-reduce (Table2DPlan) on the
+    #     shared communicator
     if pi4:
         import torch
 
@@ -828,7 +830,7 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
             "rel_err_vs_oracle": rel, "rows_this_rank": [p2.row0, p2.row1],
             "bucketed_allreduce": bool(p2.bucketed), "n_gpus": ctx.world,
             "step_streams": p2.step_streams, "multistep": bool(p2.multistep),
-            "phases": p2.phases, "workgroups": p2.workgroups,
+            "phases": p2.phases, "workgroups": p2.workgroups, "graph_steps": p2.graph_steps,
             "verified": bool(rel <= 1e-12)}
         del p2
     # (6) BASELINE config #4: the same integral through the packed-fp32 path. Samples are

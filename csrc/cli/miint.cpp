@@ -236,7 +236,7 @@ constexpr const char* kUsage =
     "       miint sweep [--gpus G]\n"
     "       miint table2d [--grid 4096] [--gpus G] [--slice R/W] [--no-graph]\n"
     "                     [--step-streams S] [--min-wg W] [--settle-ms MS] [--no-multistep]\n"
-    "                     [--phases P]\n"
+    "                     [--phases P] [--graph-steps K]\n"
     "       miint selfcheck\n"
     "       miint comm [--gpus G] [--max-bytes 144e6] [--iters 20]\n"
     "Every record is one JSON line on stdout; --jsonl FILE also appends it to FILE.\n";
@@ -287,13 +287,14 @@ int main(int argc, char** argv) {
     if (cmd == "table2d") {  // BASELINE config #5: 2-D field, g x g samples, rows split
       Table2DConfig c;
       c.grid = static_cast<int>(a.integer("grid", 4096));
-      c.bucket = !a.flag("no-bucket");  // one all-reduce per graph replay of kGraphSteps
+      c.bucket = !a.flag("no-bucket");  // one all-reduce per graph replay
       c.chain = !a.flag("no-chain");    // graph replays: chained launches, no per-launch tail
       c.step_streams = static_cast<int>(a.integer("step-streams", 0));  // chains per replay
       c.min_wg = static_cast<int>(a.integer("min-wg", 0));
       c.settle_ms = a.num("settle-ms", c.settle_ms);
       c.multistep = !a.flag("no-multistep");  // A-B: chained launches per integration
       c.phases = static_cast<int>(a.integer("phases", 0));  // multi-step step phases (0 auto)
+      c.graph_steps = static_cast<int>(a.integer("graph-steps", 0));  // per replay (0 auto)
       // --slice R/W: time only rank R's rows of a W-GPU split, on this GPU (no collective)
       const std::string sl = a.str("slice", "");
       if (!sl.empty()) {
@@ -304,7 +305,7 @@ int main(int argc, char** argv) {
       }
       double value = 0.0, timed = 0.0, ms = 0.0;
       bool bucketed = false, chained = false, multistep = false;
-      int streams = 1, phases = 0, resident = 0, min_wg = 0, wgs = 0;
+      int streams = 1, phases = 0, resident = 0, min_wg = 0, wgs = 0, gsteps = 0;
       cli::RankFacts facts;
       std::mutex mu;
       cli::run_ranks(topo, [&](int rank, int dev, const Comm* comm) {
@@ -325,6 +326,7 @@ int main(int argc, char** argv) {
           resident = plan.resident_per_cu();
           min_wg = plan.min_wg();
           wgs = plan.workgroups();
+          gsteps = graphs ? plan.graph_steps() : 0;
         }
         if (t > ms) ms = t;
       });
@@ -333,6 +335,7 @@ int main(int argc, char** argv) {
         r.add("program", "table2d").add("grid", c.grid);
         r.add("step_streams", streams).add("multistep", multistep).add("phases", phases);
         r.add("resident_per_cu", resident).add("min_wg", min_wg).add("workgroups", wgs);
+        r.add("graph_steps", gsteps);
         facts.add(r, topo);
         if (c.world > 1) {
           r.add("slice", std::to_string(c.rank) + "/" + std::to_string(c.world))

@@ -238,9 +238,13 @@ Table2DShapeInfo table2d_shape_info(const Table2DParams& p);
 // Every partial is still one workgroup's, computed as in the one-phase launch: bitwise the
 // same values. 0 = auto: kT2AutoPhases (<= steps) — past residency the later phases'
 // workgroups start as earlier ones finish, and 16 phases measured fastest or level on every
-// shape (profiles/r4/t2d_phases_explicit.jsonl, t2d_variant_ab.jsonl, t2d_shape_sweep.jsonl).
-constexpr int kT2AutoPhases = 16;  // auto
+// shape (profiles/r4/t2d_phases_explicit.jsonl, t2d_variant_ab.jsonl, t2d_shape_sweep.jsonl) —
+// doubled while the launch would hold fewer than kT2AutoWorkgroups workgroups (small row
+// slices at the long replays of round 5, profiles/r5/t2d/n_t2d_steps.jsonl).
+constexpr int kT2AutoPhases = 16;  // auto (at least)
+constexpr long kT2AutoWorkgroups = 4096;  // auto: phases double while nb x phases is below
 constexpr int kT2MaxPhases = 32;  // an explicit request (32: one step per workgroup)
+constexpr int kT2MaxReplaySteps = 1024;  // launch_table2d_multistep's step limit
 bool table2d_multistep_ok(const Table2DParams& p, int num_cus);
 // Multi-step workgroups resident per CU (hipOccupancy; 0 for a shape without the row stream).
 int table2d_multistep_resident(const Table2DParams& p);

@@ -31,8 +31,8 @@ struct Table2DConfig {
   // Without a communicator: integrate only row slice `rank` of `world` (the share one GPU
   // of a `world`-GPU run computes; the result is that partial). Ignored with a communicator.
   int world = 1, rank = 0;
-  // Graph timing with a communicator: the kGraphSteps integrations of one replay each write
-  // their own partial, and ONE all-reduce of kGraphSteps doubles (plus one copy) ends the
+  // Graph timing with a communicator: the graph_steps integrations of one replay each write
+  // their own partial, and ONE all-reduce of graph_steps doubles (plus one copy) ends the
   // replay — every integration still gets its own global sum (RiemannPlan's bucketing).
   // false: kernel -> 8-byte all-reduce -> copy per integration.
   bool bucket = true;
@@ -58,6 +58,12 @@ struct Table2DConfig {
   // per wave that fit the LDS tile, for every launch of the plan, so all its paths still
   // sum the same partials; 1/8 slice of 4096^2: 1.48 -> 1.23 us, profiles/r4/t2d_slice_shapes)
   int min_wg = 0;
+  // Run the RCCL stage (the bucketed all-reduce + copy per replay) even with a 1-rank
+  // communicator — a row slice (world/rank above) then times the per-GPU share of a
+  // world-GPU run with its collective captured (tools/t2d_strong.py).
+  bool force_collective = false;
+  // Integrations per graph replay: 0 = auto (Table2DPlan::graph_steps), else 1..kT2MaxReplaySteps.
+  int graph_steps = 0;
   double settle_ms = 30.0;  // graph time(): untimed warm-up replays first (steady clocks)
 };
 // 4096^2 on one MI355X, us per integration by chains 1/2/3/4/8 (two runs each, settled
@@ -72,14 +78,27 @@ class Table2DPlan {
   // rank) or kernel -> RCCL all-reduce -> 8-byte copy. Returns the value.
   double run();
   // `iters` back-to-back integrations; returns device ms per integration. With graphs,
-  // kGraphSteps integrations are captured once into a hipGraph and replayed (iters rounded
-  // up to whole replays): one launch per kGraphSteps instead of one per integration.
+  // graph_steps() integrations are captured once into a hipGraph and replayed (iters rounded
+  // up to whole replays): one graph launch per graph_steps() integrations.
   double time(int iters, bool graphs = true);
   // Global value of the last integration time() ran (every rank holds it).
   double last_result() const;
   bool bucketed() const { return bucketed_; }
-  bool chained() const { return cfg_.chain && (!comm_ || world_ == 1 || bucketed_); }
+  bool chained() const { return cfg_.chain && (!collective_ || bucketed_); }
+  // the replay ends in a collective over the plan's communicator (world > 1, or forced)
+  bool collective() const { return collective_; }
+  // Integrations per graph replay. Chained and per-launch replays: kGraphSteps (one kernel
+  // node per integration). A multi-step replay (one launch + one close) under auto: doubled
+  // from kGraphSteps until the replay holds kReplaySamples samples (<= kT2MaxReplaySteps) —
+  // a replay pays ~14 us of launch ramp, tail and closing kernel whatever its size, which at
+  // 32 integrations of a 1/8 row slice of 4096^2 (30 us of work) was a third of the time
+  // (profiles/r5/t2d/n_t2d_steps.jsonl, us per integration at 32 / 128 / 512 / 1024 per
+  // replay: 4096^2 4.61-4.71 / 4.34 / 4.12-4.20 / 4.12-4.16; its 1/8 slice 0.95-1.06 / 0.71-0.84
+  // / 0.62 / 0.61-0.63). Every integration is still a complete one (its own staging and
+  // partials), and every replay size gives the same values, bitwise.
   static constexpr int kGraphSteps = 32;
+  static constexpr double kReplaySamples = 8589934592.0;  // 2^33: 512 integrations of 4096^2
+  int graph_steps() const { return graph_steps_; }
   int step_streams() const;  // chains a chained replay runs (1 when not chained)
   // Collective over the plan's communicator (no-op on one rank): time() calls it right
   // before its clock starts, so every rank's interval begins after every rank is here.
@@ -100,13 +119,15 @@ class Table2DPlan {
   bool multistep_ = false;
   int phases_ = 1;
   int resident_per_cu_ = 0;
-  DeviceBuffer<double> ms_partials_;  // multistep: kGraphSteps x workgroups
+  int graph_steps_ = kGraphSteps;
+  DeviceBuffer<double> ms_partials_;  // multistep: graph_steps_ x workgroups
   int device_;
   const Comm* comm_;
   int rank_ = 0, world_ = 1;
   int row0_ = 0, row1_ = 0;
   bool bucketed_ = false;
-  bool last_batched_ = false;  // the last time() left kGraphSteps results in host_
+  bool collective_ = false;
+  bool last_batched_ = false;  // the last time() left graph_steps_ results in host_
   Stream stream_;
   std::vector<Stream> lanes_;  // streams 1.. of a multi-stream chained replay
   std::vector<std::unique_ptr<Event>> ev_join_;

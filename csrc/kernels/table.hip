@@ -295,6 +295,16 @@ __device__ __forceinline__ double fma_sv(double a, double s, double c) {
   return r;
 }
 
+// fma(a, b, c) as a 3-operand VOP3 v_fma_f64 with every source a VGPR: left to itself hipcc
+// picks the 2-operand v_fmac_f64 (destination tied to c), and a loop-carried result then
+// needs a v_mov_b64 from c's register to the value's home; the untied form can be written
+// straight there.
+__device__ __forceinline__ double fma_vvv(double a, double b, double c) {
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
 // One workgroup's share of a row-stream integration, in three parts: its table footprint
 // (t2d_footprint), the staging loads of that footprint (t2d_stage_load: SH / kStageRows doubles per
 // thread, in registers) and their LDS writes (t2d_stage_store), then the rows
@@ -421,7 +431,10 @@ __device__ __forceinline__ double t2d_stream_rows(const Table2DParams& p, int ro
   __syncthreads();
   auto line = [&](int j, int b) {  // table row j interpolated at column b's x
     const double* t = tile + (j - f.sy0) * kSW + col[b];
-    return fma(t[1] - t[0], fx[b], t[0]);
+    // (the untied form only where it removes copies: the single-launch kernels would pay
+    // its registers in occupancy)
+    if constexpr (READ_AHEAD) return fma_vvv(t[1] - t[0], fx[b], t[0]);
+    else return fma(t[1] - t[0], fx[b], t[0]);
   };
   double acc[kSCols], lc[kSCols], ln[kSCols], d[kSCols];
 #pragma unroll
@@ -440,19 +453,47 @@ __device__ __forceinline__ double t2d_stream_rows(const Table2DParams& p, int ro
       n1[b] = t[1];
     }
   };
+  // Where the table row changes, as two wave-uniform bit masks (one ballot each, once per
+  // integration): row k starts a new table row (iy_k != iy_{k-1}; row 0 always), and does so
+  // by one (iy_k == iy_{k-1} + 1). The row loop then tests a bit (SALU) instead of reading
+  // row k's iy back with a v_readlane every row; iy is read only for the rare jump.
+  uint64_t changed, consec;
+  {
+    const int r = rbase + min(lane, max(nrows - 1, 0));
+    const double yyp = ((r - 1 + 0.5) * f.sy) * f.cy;  // row k - 1's, the same arithmetic
+    const int iyp = clampi(static_cast<int>(yyp), 0, p.ny - 2);
+    changed = __ballot(lane == 0 || iyl != iyp);
+    consec = __ballot(lane != 0 && iyl == iyp + 1);
+  }
   for (int k = 0; k < nrows; ++k) {
-    const int iy = __builtin_amdgcn_readlane(iyl, k);
     const double fy = readlane_f64(fyl, k);
-    if (iy != cur) {  // wave-uniform
-      if (iy == cur + 1) {
+    if ((changed >> k) & 1) {  // wave-uniform
+      const bool by_one = (consec >> k) & 1;
+      const int iy = by_one ? cur + 1 : __builtin_amdgcn_readlane(iyl, k);
+      if constexpr (READ_AHEAD) {
+        // One path for both kinds of change (one join, so the line values need no phi copies
+        // between two predecessors): a jump first sets up what a step by one would hold —
+        // ln = line(iy) and the read-ahead at row iy + 1 — and the common update below then
+        // forms line(iy + 1) from it exactly as line() does (the same fma).
+        if (!by_one) {
+#pragma unroll
+          for (int b = 0; b < kSCols; ++b) ln[b] = line(iy, b);
+          fetch(iy + 1);
+        }
 #pragma unroll
         for (int b = 0; b < kSCols; ++b) {
           lc[b] = ln[b];
-          if constexpr (READ_AHEAD) ln[b] = fma(n1[b] - n0[b], fx[b], n0[b]);  // line(iy + 1)
-          else ln[b] = line(iy + 1, b);
+          ln[b] = fma_vvv(n1[b] - n0[b], fx[b], n0[b]);  // line(iy + 1)
           d[b] = ln[b] - lc[b];
         }
-        if constexpr (READ_AHEAD) fetch(iy + 2);
+        fetch(iy + 2);
+      } else if (by_one) {
+#pragma unroll
+        for (int b = 0; b < kSCols; ++b) {
+          lc[b] = ln[b];
+          ln[b] = line(iy + 1, b);
+          d[b] = ln[b] - lc[b];
+        }
       } else {
 #pragma unroll
         for (int b = 0; b < kSCols; ++b) {
@@ -460,7 +501,6 @@ __device__ __forceinline__ double t2d_stream_rows(const Table2DParams& p, int ro
           ln[b] = line(iy + 1, b);
           d[b] = ln[b] - lc[b];
         }
-        if constexpr (READ_AHEAD) fetch(iy + 2);
       }
       cur = iy;
     }
@@ -783,7 +823,18 @@ int table2d_multistep_phases(const Table2DParams& p, int num_cus, int steps, int
   // (profiles/r4/t2d_phases_explicit.jsonl, t2d_variant_ab.jsonl, t2d_shape_sweep.jsonl, us
   // per integration; 4096^2: 5.87 / 5.56 / 5.39 / 5.36 at 1-4 phases on 32-row tiles, 5.13 /
   // 5.07 at 8 / 16 on 30-row tiles; the 1/8 slice 1.92 / 1.48 / 1.49 / 1.45, then 1.01 / 0.97)
-  return std::min(want > 0 ? std::min(want, kT2MaxPhases) : kT2AutoPhases, std::max(1, steps));
+  // Auto also doubles the phases (up to kT2MaxPhases) while a replay would run fewer than
+  // kT2AutoWorkgroups workgroups: the 1/8 slice's 128 blocks at 1024 integrations per replay,
+  // 0.61 -> 0.58 us at 32 phases; the whole field (1024 blocks) ran slower at 32 (4.14-4.30 ->
+  // 4.31-4.49 us; profiles/r5/t2d/n_t2d_steps.jsonl).
+  int phases = kT2AutoPhases;
+  if (want > 0) {
+    phases = std::min(want, kT2MaxPhases);
+  } else {
+    const long nb = static_cast<long>(table2d_grid(p));
+    while (phases < kT2MaxPhases && nb * phases < kT2AutoWorkgroups) phases *= 2;
+  }
+  return std::min(phases, std::max(1, steps));
 }
 
 void launch_table2d_multistep(const Table2DParams& p, double* partials, int steps, double* outs,

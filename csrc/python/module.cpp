@@ -501,8 +501,11 @@ PYBIND11_MODULE(_miint, m) {
   py::class_<Table2DPlan>(m, "Table2DPlan")
       .def(py::init([](int grid, double extent, int device, const Comm* comm, bool bucket,
                        bool chain, int step_streams, int slice_rank, int slice_world,
-                       bool multistep, int phases, int min_wg) {
+                       bool multistep, int phases, int min_wg, int graph_steps,
+                       bool force_collective) {
              Table2DConfig c;
+             c.force_collective = force_collective;
+             c.graph_steps = graph_steps;
              c.phases = phases;
              c.min_wg = min_wg;
              c.grid = grid;
@@ -519,6 +522,7 @@ PYBIND11_MODULE(_miint, m) {
            py::arg("comm") = nullptr, py::arg("bucket") = true, py::arg("chain") = true,
            py::arg("step_streams") = 0, py::arg("slice_rank") = 0, py::arg("slice_world") = 1,
            py::arg("multistep") = true, py::arg("phases") = 0, py::arg("min_wg") = 0,
+           py::arg("graph_steps") = 0, py::arg("force_collective") = false,
            py::keep_alive<1, 5>())
       .def_property_readonly("phases", &Table2DPlan::phases)
       .def_property_readonly("min_wg", &Table2DPlan::min_wg)
@@ -533,7 +537,8 @@ PYBIND11_MODULE(_miint, m) {
       .def("last_result", &Table2DPlan::last_result)
       .def_property_readonly("bucketed", &Table2DPlan::bucketed)
       .def_property_readonly("chained", &Table2DPlan::chained)
-      .def_property_readonly("graph_steps", [](const Table2DPlan&) { return Table2DPlan::kGraphSteps; })
+      .def_property_readonly("collective", &Table2DPlan::collective)
+      .def_property_readonly("graph_steps", &Table2DPlan::graph_steps)
       .def_property_readonly("row0", &Table2DPlan::row0)
       .def_property_readonly("row1", &Table2DPlan::row1);
   m.def("table2d_oracle", &table2d_oracle, py::arg("grid"), py::arg("extent") = 1800.0);

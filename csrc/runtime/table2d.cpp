@@ -13,14 +13,15 @@ namespace miint {
 Table2DPlan::Table2DPlan(const Table2DConfig& cfg, int device, const Comm* comm)
     : cfg_(cfg), device_(device), comm_(comm), stream_((set_device(device), Stream())) {
   MIINT_CHECK(cfg.grid >= 1 && cfg.grid <= (1 << 20), "grid out of range");
-  if (comm) {
+  if (comm && comm->world() > 1) {
     rank_ = comm->rank();
     world_ = comm->world();
-  } else {
+  } else {  // no communicator, or a 1-rank one (force_collective): the configured row slice
     MIINT_CHECK(cfg.world >= 1 && cfg.rank >= 0 && cfg.rank < cfg.world, "bad slice rank/world");
     rank_ = cfg.rank;
     world_ = cfg.world;
   }
+  collective_ = comm && (comm->world() > 1 || cfg.force_collective);
   uint64_t b = 0, c = 0;
   rank_slice(static_cast<uint64_t>(cfg.grid), rank_, world_, &b, &c);
   row0_ = static_cast<int>(b);
@@ -32,7 +33,7 @@ Table2DPlan::Table2DPlan(const Table2DConfig& cfg, int device, const Comm* comm)
   MIINT_HIP(hipMemcpy(v_.get(), prof.data(), v_.bytes(), hipMemcpyHostToDevice));
   launch_outer_product(v_.get(), n, table_.get(), stream_.get());
   // bucketed_ first: chained() (and so the multi-step choice and chain count) depends on it
-  bucketed_ = cfg.bucket && comm_ && world_ > 1;
+  bucketed_ = cfg.bucket && collective_;
   const int cus = device_info(device).num_cus;
   const auto params = [&](int min_wg) {
     return Table2DParams{table_.get(), n, n, cfg.extent, cfg.extent, cfg.grid, cfg.grid,
@@ -48,13 +49,22 @@ Table2DPlan::Table2DPlan(const Table2DConfig& cfg, int device, const Comm* comm)
   partials_ = DeviceBuffer<double>(static_cast<size_t>(table2d_grid(p)));
   multistep_ = cfg.multistep && row1_ > row0_ && table2d_multistep_ok(p, cus);
   resident_per_cu_ = table2d_multistep_resident(p);
+  MIINT_CHECK(cfg.graph_steps >= 0 && cfg.graph_steps <= kT2MaxReplaySteps,
+              "table2d: graph_steps 0 (auto) or 1..kT2MaxReplaySteps");
+  if (cfg.graph_steps > 0) {
+    graph_steps_ = cfg.graph_steps;
+  } else if (multistep_) {
+    const double samples = static_cast<double>(cfg.grid) * std::max(1, row1_ - row0_);
+    while (graph_steps_ < kT2MaxReplaySteps && graph_steps_ * samples < kReplaySamples)
+      graph_steps_ *= 2;
+  }
   if (multistep_) {
-    ms_partials_ = DeviceBuffer<double>(kGraphSteps * partials_.size());
-    phases_ = std::max(1, table2d_multistep_phases(p, cus, kGraphSteps, cfg.phases));
+    ms_partials_ = DeviceBuffer<double>(static_cast<size_t>(graph_steps_) * partials_.size());
+    phases_ = std::max(1, table2d_multistep_phases(p, cus, graph_steps_, cfg.phases));
   }
   const int L = (!chained() || multistep_)
                     ? 1
-                    : std::max(1, std::min(kGraphSteps, cfg_.step_streams > 0 ? cfg_.step_streams
+                    : std::max(1, std::min(graph_steps_, cfg_.step_streams > 0 ? cfg_.step_streams
                                                                               : kAutoT2Streams));
   // chained launches: a double buffer per chain
   chain_ = DeviceBuffer<double>(2 * static_cast<size_t>(L) * partials_.size());
@@ -63,12 +73,12 @@ Table2DPlan::Table2DPlan(const Table2DConfig& cfg, int device, const Comm* comm)
     ev_join_.emplace_back(new Event(false));
   }
   fill_unset_slots(partials_.get(), partials_.size(), stream_.get());  // fused kernel's slots
-  result_ = DeviceBuffer<double>(kGraphSteps);
+  result_ = DeviceBuffer<double>(static_cast<size_t>(graph_steps_));
   sync_ = DeviceBuffer<double>(1);
   MIINT_HIP(hipMemset(sync_.get(), 0, sync_.bytes()));
   ticket_ = DeviceBuffer<unsigned int>(kTicketWords);
   MIINT_HIP(hipMemset(ticket_.get(), 0, ticket_.bytes()));
-  host_ = PinnedBuffer<double>(kGraphSteps);
+  host_ = PinnedBuffer<double>(static_cast<size_t>(graph_steps_));
   stream_.sync();
 }
 
@@ -76,7 +86,7 @@ Table2DPlan::Table2DPlan(const Table2DConfig& cfg, int device, const Comm* comm)
 int Table2DPlan::step_streams() const { return 1 + static_cast<int>(lanes_.size()); }
 
 void Table2DPlan::barrier() {
-  if (!comm_ || world_ <= 1) return;
+  if (!collective_) return;
   comm_->allreduce_sum(sync_.get(), sync_.get(), 1, stream_.get());
   wait_with_timeout(stream_.get(), 300.0, comm_);
 }
@@ -93,7 +103,7 @@ void Table2DPlan::launch_local(double* out, hipStream_t s) {
 }
 
 void Table2DPlan::enqueue(hipStream_t s) {
-  const bool multi = comm_ && world_ > 1;
+  const bool multi = collective_;
   // one rank: the kernel's last workgroup stores straight into mapped pinned memory
   launch_local(multi ? result_.get() : host_.device_ptr(), s);
   if (!multi) return;
@@ -123,25 +133,25 @@ double Table2DPlan::time(int iters, bool graphs) {
     stream_.sync();
     return Event::elapsed_ms(e0_, e1_) / iters;
   }
-  const Comm* gc = comm_ && world_ > 1 ? comm_ : nullptr;  // group-wide graphs (loopback)
+  const Comm* gc = collective_ ? comm_ : nullptr;  // group-wide graphs (loopback)
   const bool multi = gc != nullptr;
-  const bool batched = !multi || bucketed_;  // kGraphSteps results land in one replay
+  const bool batched = !multi || bucketed_;  // graph_steps_ results land in one replay
   if (!graph_.ready())
     capture_with(gc, graph_, s, [&](hipStream_t cs) {
       if (!batched) {  // one 8-byte all-reduce per integration
-        for (int i = 0; i < kGraphSteps; ++i) enqueue(cs);
+        for (int i = 0; i < graph_steps_; ++i) enqueue(cs);
         return;
       }
       // integration i's value -> outs[i]: mapped pinned memory on one rank, else the
       // device slots one all-reduce (+ one copy) closes
       double* outs = multi ? result_.get() : host_.device_ptr();
       if (row1_ <= row0_) {  // more ranks than rows
-        MIINT_HIP(hipMemsetAsync(outs, 0, kGraphSteps * sizeof(double), cs));
+        MIINT_HIP(hipMemsetAsync(outs, 0, graph_steps_ * sizeof(double), cs));
       } else if (multistep()) {  // one launch for the replay's integrations + one close
         const int n = static_cast<int>(oracle::profile_table().size());
         const Table2DParams p{table_.get(), n, n, cfg_.extent, cfg_.extent, cfg_.grid,
                               cfg_.grid, row0_, row1_, cfg_.min_wg};
-        launch_table2d_multistep(p, ms_partials_.get(), kGraphSteps, outs, cs, phases_);
+        launch_table2d_multistep(p, ms_partials_.get(), graph_steps_, outs, cs, phases_);
       } else if (chained()) {
         // integration i runs on chain i % L as that chain's step i / L: launch j of a chain
         // closes the chain's launch j - 1 (its workgroup 0), a finalize closes each chain,
@@ -159,13 +169,13 @@ double Table2DPlan::time(int iters, bool graphs) {
           ev_fork_.record(cs);
           for (int l = 1; l < L; ++l) MIINT_HIP(hipStreamWaitEvent(lane(l), ev_fork_.get(), 0));
         }
-        for (int i = 0; i < kGraphSteps; ++i) {
+        for (int i = 0; i < graph_steps_; ++i) {
           const int l = i % L, j = i / L;
           launch_table2d_chained(p, half(l, j), j ? half(l, j - 1) : nullptr,
                                  j ? outs + i - L : nullptr, lane(l));
         }
         for (int l = 0; l < L; ++l) {
-          const int last = l + ((kGraphSteps - 1 - l) / L) * L;
+          const int last = l + ((graph_steps_ - 1 - l) / L) * L;
           launch_table2d_finalize(half(l, last / L), static_cast<int>(nb), outs + last, lane(l));
           if (l > 0) {
             ev_join_[static_cast<size_t>(l - 1)]->record(lane(l));
@@ -173,22 +183,22 @@ double Table2DPlan::time(int iters, bool graphs) {
           }
         }
       } else {
-        for (int i = 0; i < kGraphSteps; ++i) launch_local(outs + i, cs);
+        for (int i = 0; i < graph_steps_; ++i) launch_local(outs + i, cs);
       }
       if (multi) {
-        comm_->allreduce_sum(result_.get(), result_.get(), kGraphSteps, cs);
-        MIINT_HIP(hipMemcpyAsync(host_.get(), result_.get(), kGraphSteps * sizeof(double),
+        comm_->allreduce_sum(result_.get(), result_.get(), graph_steps_, cs);
+        MIINT_HIP(hipMemcpyAsync(host_.get(), result_.get(), graph_steps_ * sizeof(double),
                                  hipMemcpyDeviceToHost, cs));
       }
     });
-  const int launches = std::max(1, (iters + kGraphSteps - 1) / kGraphSteps);
+  const int launches = std::max(1, (iters + graph_steps_ - 1) / graph_steps_);
   // Warm-up: from idle the GPU needs ~25 ms of continuous work to reach steady clocks
   // (profiles/r1/clock_ramp.jsonl) and one replay here is 0.1-0.3 ms, so replay for about
   // cfg_.settle_ms first. Every replay of a collective plan holds collectives, so the count must
   // be the same on every rank: it comes from the plan's size (an estimate of the replay
   // time: ~0.5 ps per sample, >= 3 us per integration), not from a measurement.
   const double samples = static_cast<double>(cfg_.grid) * cfg_.grid / world_;
-  const double est_replay_ms = kGraphSteps * std::max(3e-3, samples * 5e-10);
+  const double est_replay_ms = graph_steps_ * std::max(3e-3, samples * 5e-10);
   const int warm = std::max(1, static_cast<int>(cfg_.settle_ms / est_replay_ms));
   for (int i = 0; i < warm; ++i) launch_with(gc, graph_, s);
   stream_.sync();
@@ -199,11 +209,11 @@ double Table2DPlan::time(int iters, bool graphs) {
   e1_.record(s);
   stream_.sync();
   last_batched_ = batched;
-  return Event::elapsed_ms(e0_, e1_) / (launches * kGraphSteps);
+  return Event::elapsed_ms(e0_, e1_) / (launches * graph_steps_);
 }
 
 double Table2DPlan::last_result() const {
-  return last_batched_ ? host_[kGraphSteps - 1] : host_[0];
+  return last_batched_ ? host_[graph_steps_ - 1] : host_[0];
 }
 
 double table2d_oracle(int grid, double extent) {

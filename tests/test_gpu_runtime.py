@@ -612,11 +612,12 @@ def test_table2d_multistep_phases_bitwise(native, cuda, g, sl, phases):
 
 def test_table2d_multistep_auto_phases(native, cuda):
     """Auto: kT2AutoPhases (16) step phases on the most rows per wave that fit (16 rows on
-    4096^2: 16 x 8 = 128 blocks for the 1/8 row slice, 16 x 64 for the whole field) — the
-    fastest measured (profiles/r4/t2d_slice_shapes.jsonl, t2d_phases_explicit.jsonl) — and
-    the same values as one phase."""
+    4096^2: 16 x 8 = 128 blocks for the 1/8 row slice, 16 x 64 for the whole field), doubled
+    while the launch holds fewer than 4096 workgroups (the 1/8 slice: 32) — the fastest
+    measured (profiles/r4/t2d_slice_shapes.jsonl, t2d_phases_explicit.jsonl,
+    profiles/r5/t2d/n_t2d_steps.jsonl) — and the same values as one phase."""
     p = native.Table2DPlan(4096, 1800.0, 0, None, True, True, 1, 0, 8)
-    assert p.multistep and p.phases == 16 and p.min_wg == 1 and p.workgroups == 128
+    assert p.multistep and p.phases == 32 and p.min_wg == 1 and p.workgroups == 128
     full = native.Table2DPlan(4096)
     assert full.multistep and full.phases == 16 and full.workgroups == 1024
     one = native.Table2DPlan(4096, phases=1)
@@ -626,6 +627,43 @@ def test_table2d_multistep_auto_phases(native, cuda):
     # an explicit shape target is kept
     assert native.Table2DPlan(4096, 1800.0, 0, None, True, True, 1, 0, 8,
                               min_wg=512).workgroups == 512
+
+
+def test_table2d_replay_steps_adapt_to_the_share(native, cuda):
+    """A multi-step replay holds at least kReplaySamples = 2^33 samples (doubling from 32 up to
+    1024 integrations): 512 for the whole 4096^2 field, 1024 for its 1/8 row slice. Chained
+    replays keep 32 (one kernel node per integration); an explicit count is kept. Every
+    replay size gives the same values, bitwise."""
+    full = native.Table2DPlan(4096)
+    s8 = native.Table2DPlan(4096, 1800.0, 0, None, True, True, 1, 0, 8)
+    s8_32 = native.Table2DPlan(4096, 1800.0, 0, None, True, True, 1, 0, 8, graph_steps=32)
+    chained = native.Table2DPlan(4096, multistep=False)
+    assert (full.graph_steps, s8.graph_steps, s8_32.graph_steps) == (512, 1024, 32)
+    assert chained.graph_steps == 32 and not chained.multistep
+    for p in (full, s8, s8_32):
+        p.time(p.graph_steps, True)
+    assert full.last_result() == native.table2d_oracle(4096)
+    assert s8.last_result() == s8_32.last_result() == s8.run()
+    with pytest.raises(Exception):
+        native.Table2DPlan(4096, graph_steps=1025)
+
+
+def test_table2d_slice_with_forced_rccl_stage(native, cuda):
+    """A row slice with a 1-rank RCCL communicator and force_collective (tools/t2d_strong.py's
+    rehearsal of one rank of a G-GPU run): every replay ends in the bucketed all-reduce +
+    copy, and the partial is bitwise the plain slice's."""
+    from cuda_v_mpi_amd.parallel.dist import DistContext, native_comm
+
+    comm = native_comm(DistContext())
+    forced = native.Table2DPlan(4096, 1800.0, 0, comm, True, True, 0, 0, 8, force_collective=True)
+    plain = native.Table2DPlan(4096, 1800.0, 0, None, True, True, 0, 0, 8)
+    quiet = native.Table2DPlan(4096, 1800.0, 0, comm, True, True, 0, 0, 8)
+    assert forced.collective and forced.bucketed and forced.multistep
+    assert not plain.collective and not quiet.collective and not quiet.bucketed
+    assert (forced.row0, forced.row1) == (plain.row0, plain.row1) == (0, 512)
+    for p in (forced, plain):
+        p.time(p.graph_steps, True)
+    assert forced.last_result() == plain.last_result() == forced.run() == plain.run()
 
 
 def test_table2d_multistep_past_residency(native, cuda):

@@ -28,7 +28,7 @@ for g in G1 G2; do
   run pi4_fp32acc $g "${!g}" "$REPO/build/bin/miint" bench --iters 200 --settle 300 --dtype fp32acc
   run sin_fast $g "${!g}" "$REPO/build/bin/miint" bench --iters 40 --settle 40 --integrand sin --div ieee
   run train_fast $g "${!g}" "$REPO/build/bin/miint" bench --iters 40 --settle 40 --integrand train --div ieee
-  run table2d_slice8 $g "${!g}" "$REPO/build/bin/miint" table2d --slice 0/8 --iters 320 --settle-ms 20
+  run table2d_slice8 $g "${!g}" "$REPO/build/bin/miint" table2d --slice 0/8 --iters 2048 --settle-ms 20
   run pi4_ieee $g "${!g}" "$REPO/build/bin/miint" bench --iters 20 --settle 60 --div ieee
   run pi4_fp32 $g "${!g}" "$REPO/build/bin/miint" bench --iters 200 --settle 300 --dtype fp32
   run pi4_series_exact $g "${!g}" "$REPO/build/bin/miint" bench --iters 200 --settle 300 --div series_exact
@@ -38,13 +38,13 @@ for g in G1 G2; do
   run train $g "${!g}" "$REPO/build/bin/miint" bench --iters 200 --settle 300 --integrand train
   run poly $g "${!g}" "$REPO/build/bin/miint" bench --iters 100 --settle 200 --integrand poly
   run table $g "${!g}" "$REPO/build/bin/miint" bench --iters 200 --settle 300 --integrand table
-  run table2d $g "${!g}" "$REPO/build/bin/miint" table2d --iters 320 --settle-ms 20
+  run table2d $g "${!g}" "$REPO/build/bin/miint" table2d --iters 1024 --settle-ms 20
   run dpp_selftest $g "${!g}" python3 "$REPO/tools/dpp_probe.py"
 done
 # the 2-D field re-stages its table footprint every integration: bytes fetched past L2
 for g in G3; do
-  run table2d_slice8 $g "${!g}" "$REPO/build/bin/miint" table2d --slice 0/8 --iters 320 --settle-ms 20
-  run table2d $g "${!g}" "$REPO/build/bin/miint" table2d --iters 320 --settle-ms 20
+  run table2d_slice8 $g "${!g}" "$REPO/build/bin/miint" table2d --slice 0/8 --iters 2048 --settle-ms 20
+  run table2d $g "${!g}" "$REPO/build/bin/miint" table2d --iters 1024 --settle-ms 20
 done
 for g in G1 G2 G3 G4; do
   run trainscan $g "${!g}" "$REPO/build/bin/trainscan"

@@ -15,7 +15,7 @@ For every (workload, kernel) whose median dispatch is at least --min-us long:
   sol            max(bounds) / measured median dispatch time: the fraction of the tighter
                  roofline the kernel reaches
   valu_per_sample, when the workload's sample count is known (Riemann workloads: 1e9; the
-                 2-D multi-step dispatch runs 32 integrations of its field)
+                 2-D multi-step dispatch runs T2D_REPLAY integrations of its field)
   clock_ghz      GRBM_GUI_ACTIVE / 8 XCDs / measured median: the shader clock the dispatch
                  actually ran at (the counter sums the 8 XCDs' busy cycles; its window runs a
                  few us past the dispatch, so only dispatches >= 500 us get a clock)
@@ -48,6 +48,10 @@ SAMPLES = {  # samples per dispatch of the Riemann workloads (miint bench defaul
     "pi4_series_exact_share8": 1.25e8, "pi4_series_g": 1e9,
     "materialize": 18e6,
 }
+
+# integrations per 2-D multi-step dispatch (Table2DPlan::graph_steps, auto since round 5: a
+# replay holds 2^33 samples; round 4's profiles ran 32)
+T2D_REPLAY = {"table2d": 512, "table2d_slice8": 1024}
 
 
 def short(name: str) -> str:
@@ -114,7 +118,8 @@ def main() -> None:
             nbytes = (med.get("FETCH_SIZE", 0.0) + med.get("WRITE_SIZE", 0.0)) * 1024
         hb = nbytes / HBM_BPS * 1e6 if nbytes else None
         bound = max(b for b in (vb, hb, 0.0) if b is not None)
-        samples = SAMPLES.get(w, 0) * (32 if w.startswith("table2d") and "multistep" in kname else 1)
+        samples = SAMPLES.get(w, 0) * (T2D_REPLAY.get(w, 32)
+                                       if w.startswith("table2d") and "multistep" in kname else 1)
         per = f"{valu * 64 / samples:.2f}" if valu and samples else "—"
         grbm = med.get("GRBM_GUI_ACTIVE")
         # the counter window spans a few us past the dispatch: only long dispatches give a clock

@@ -53,8 +53,15 @@ Table2DPlan::Table2DPlan(const Table2DConfig& cfg, int device, const Comm* comm)
               "table2d: graph_steps 0 (auto) or 1..kT2MaxReplaySteps");
   if (cfg.graph_steps > 0) {
     graph_steps_ = cfg.graph_steps;
-  } else if (multistep_) {
-    const double samples = static_cast<double>(cfg.grid) * std::max(1, row1_ - row0_);
+  } else if (const int rows = (cfg.grid + world_ - 1) / world_;
+             cfg.multistep && chained() &&
+             table2d_multistep_ok(Table2DParams{table_.get(), n, n, cfg.extent, cfg.extent,
+                                                cfg.grid, cfg.grid, 0, rows, 1},
+                                  cus)) {
+    // From the configuration only (the largest rank's row count, not this rank's rows):
+    // every rank of a collective plan must replay the same count, its all-reduce covering
+    // graph_steps_ values.
+    const double samples = static_cast<double>(cfg.grid) * rows;
     while (graph_steps_ < kT2MaxReplaySteps && graph_steps_ * samples < kReplaySamples)
       graph_steps_ *= 2;
   }

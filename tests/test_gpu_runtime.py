@@ -646,6 +646,10 @@ def test_table2d_replay_steps_adapt_to_the_share(native, cuda):
     assert s8.last_result() == s8_32.last_result() == s8.run()
     with pytest.raises(Exception):
         native.Table2DPlan(4096, graph_steps=1025)
+    # every rank of an uneven split replays the same count (its all-reduce covers them all)
+    assert {native.Table2DPlan(4095, 1800.0, 0, None, True, True, 1, r, 8).graph_steps
+            for r in range(8)} == {1024}
+    assert native.Table2DPlan(1000).graph_steps == 32  # the tile kernel: chained replays
 
 
 def test_table2d_slice_with_forced_rccl_stage(native, cuda):

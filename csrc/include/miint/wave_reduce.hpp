@@ -44,17 +44,67 @@ __device__ __forceinline__ float dpp(float v, float old = 0.0f) {
   return __builtin_amdgcn_update_dpp(old, v, CTRL, ROW_MASK, BANK_MASK, false);
 }
 
+// A lane permutation inside each row (quad_perm, row mirrors: every lane has a source lane,
+// every row is written): no `old` value is read, so none is materialised — dpp<>()'s old = 0
+// costs a v_mov_b32 per 32-bit half at every step (2 per fp64 step).
+template <int CTRL>
+__device__ __forceinline__ double dpp_perm(double v) {
+  const long long bits = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_mov_dpp(static_cast<int>(bits), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(static_cast<int>(bits >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, (static_cast<long long>(hi) << 32) |
+                                        static_cast<unsigned int>(lo));
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_perm(float v) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, false));
+}
+
+// Sum over each row of 16 lanes (every lane of the row holds it) in 4 steps.
+template <typename T>
+__device__ __forceinline__ T row_sum(T v) {
+  v += dpp_perm<kDppQuadXor1>(v);
+  v += dpp_perm<kDppQuadXor2>(v);
+  v += dpp_perm<kDppRowHalfMirror>(v);
+  v += dpp_perm<kDppRowMirror>(v);          // every lane: its row's sum
+  return v;
+}
+
 // Full-wave sum. Returns the total in lane 63 (other lanes hold partial sums); use
 // wave_broadcast_last() when every lane needs it.
 template <typename T>
 __device__ __forceinline__ T wave_sum_to_last(T v) {
-  v += dpp<kDppQuadXor1>(v);
-  v += dpp<kDppQuadXor2>(v);
-  v += dpp<kDppRowHalfMirror>(v);
-  v += dpp<kDppRowMirror>(v);               // every lane: its row's sum
+  v = row_sum(v);
   v += dpp<kDppRowBcast15, 0xA>(v);         // rows 1,3 += rows 0,2
   v += dpp<kDppRowBcast31, 0xC>(v);         // rows 2,3 += (row0+row1)
   return v;                                 // lane 63 = total
+}
+
+// Sum of lanes 0 .. N-1 (N <= 16; every other lane holds 0) in lane 0: the steps of
+// wave_sum_to_last that combine non-zero values — the rest only add zeros — so the value is
+// bitwise wave_sum_to_last's lane 63 (up to the sign of an exact zero). The cross-wave step
+// of a block sum (4 wave totals at 256 threads, 16 at 1024): 2 or 4 DPP steps on the
+// critical path after the barrier instead of 6.
+template <typename T>
+__device__ __forceinline__ T lanes_sum_small(T v, int n) {
+  v += dpp_perm<kDppQuadXor1>(v);
+  v += dpp_perm<kDppQuadXor2>(v);
+  if (n > 4) {
+    v += dpp_perm<kDppRowHalfMirror>(v);
+    v += dpp_perm<kDppRowMirror>(v);
+  }
+  return v;  // lanes 0..3 (n <= 4) or 0..15: the sum
+}
+__device__ __forceinline__ double wave_broadcast_first(double v) {
+  const long long bits = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_readfirstlane(static_cast<int>(bits));
+  const int hi = __builtin_amdgcn_readfirstlane(static_cast<int>(bits >> 32));
+  return __builtin_bit_cast(double, (static_cast<long long>(hi) << 32) |
+                                        static_cast<unsigned int>(lo));
+}
+__device__ __forceinline__ float wave_broadcast_first(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v)));
 }
 
 __device__ __forceinline__ double wave_broadcast_last(double v) {
@@ -104,7 +154,7 @@ __device__ __forceinline__ T block_sum(T v, T* lds) {
     T r = T(0);
     if (wid == 0) {
       r = lane < kNW ? lds[lane] : T(0);
-      r = wave_sum(r);
+      r = kNW <= 16 ? wave_broadcast_first(lanes_sum_small(r, kNW)) : wave_sum(r);
     }
     return r;  // meaningful in wave 0
   }
@@ -125,7 +175,7 @@ __device__ __forceinline__ T block_sum_dyn(T v, T* lds) {
   T r = T(0);
   if (wid == 0) {
     r = lane < nw ? lds[lane] : T(0);
-    r = wave_sum(r);
+    r = wave_broadcast_first(lanes_sum_small(r, nw));  // nw <= 16
   }
   return r;  // meaningful in wave 0
 }

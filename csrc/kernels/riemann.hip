@@ -688,8 +688,12 @@ __device__ __forceinline__ void multistep_body(const RiemannParams& p, const dou
                                                int table_n, double* partials, int steps,
                                                unsigned rot) {
   using Acc = typename AccOf<F>::type;
-  __shared__ double red[kMaxBlock / kWave];
-  __shared__ Acc red_acc[__is_same(Acc, double) ? 1 : kMaxBlock / kWave];
+  // The block sum's LDS slots alternate between steps: step s + 2 writes red[s & 1] only
+  // after every wave passed step s + 1's block-sum barrier, which wave 0 reaches after its
+  // step-s reads — so no second barrier per step, and waves 1-3 start the next step while
+  // wave 0 finishes the cross-wave sum.
+  __shared__ double red[2][kMaxBlock / kWave];
+  __shared__ Acc red_acc[2][__is_same(Acc, double) ? 1 : kMaxBlock / kWave];
   __shared__ double lds[lds_words<M, F>()];
   const F f = make_functor<M, F>(p, table, table_n, lds);
   const unsigned nb = gridDim.x;
@@ -699,10 +703,9 @@ __device__ __forceinline__ void multistep_body(const RiemannParams& p, const dou
     RiemannParams q = p;
     asm volatile("" : "+s"(q.a));  // a fresh value every step (no instructions)
     double v;
-    if constexpr (__is_same(Acc, double)) v = block_sum_dyn(lane_sum<M>(q, f, vb, sp), red);
-    else v = static_cast<double>(block_sum_dyn(lane_sum<M>(q, f, vb, sp), red_acc));
+    if constexpr (__is_same(Acc, double)) v = block_sum_dyn(lane_sum<M>(q, f, vb, sp), red[s & 1]);
+    else v = static_cast<double>(block_sum_dyn(lane_sum<M>(q, f, vb, sp), red_acc[s & 1]));
     if (threadIdx.x == 0) partials[static_cast<size_t>(s) * nb + vb] = v;
-    __syncthreads();  // wave 0 has read red before the next step writes it
     vb += rot;
     if (vb >= nb) vb -= nb;
   }

@@ -6,9 +6,10 @@ vs analytic pi"). One step = one complete integration of N = 1e9 samples IN TOTA
 the G GPUs as the reference splits its fixed STEPS over its workers (riemann.cpp:10,71-73:
 strong scaling, so the record at every G is the metric's own config): gfx950 kernel (every
 sample evaluated, fp64) -> in-kernel DPP/LDS reduction -> RCCL all-reduce of the per-GPU
-partial over xGMI -> D2H into pinned memory. Steps are hipGraph replays of batches of --slots
-(48) steps plus one replay of a remainder-sized batch (every graph is captured before the
-warmup, so the timed region only replays); with >1 GPU each batch ends in ONE all-reduce of its
+partial over xGMI -> D2H into pinned memory. Steps run in batches of --slots (48) steps plus
+one remainder-sized batch; a batch is ONE persistent multi-step launch of all its steps and a
+closing kernel, enqueued directly (--graph-batches: as a hipGraph replay, captured before the
+warmup; measured slower, profiles/r5/graph_vs_direct.md); with >1 GPU each batch ends in ONE all-reduce of its
 step results (bucketed: every step still gets its own global sum; --no-bucket = one 8-byte
 all-reduce per step, overlapped on a side stream).
 
@@ -107,6 +108,9 @@ def parse(argv=None) -> argparse.Namespace:
                    help="cpu: torch fp64 evaluation + gloo (launcher / decomposition tests "
                         "on a GPU-less box; not a performance configuration)")
     p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--graph-batches", action="store_true",
+                   help="replay multi-step batches as hipGraphs (default: launch their two "
+                        "kernels directly, measured faster; profiles/r5/graph_vs_direct.md)")
     p.add_argument("--no-pipeline", action="store_true")
     p.add_argument("--unfused", action="store_true", help="partials + finalize (2 launches)")
     p.add_argument("--grid", type=int, default=0, help="workgroups (0 = auto; the reference's SM)")
@@ -305,6 +309,15 @@ def main(argv=None) -> int:
     use_torch = args.comm == "torch" and world > 1 and not cpu
     plan = integ.plan
     graphs = not args.no_graph and not use_torch and not cpu
+    # A multi-step plan's batch is two launches (the persistent launch of all its steps and
+    # the closing kernel; then the all-reduce and the copy on several GPUs). Enqueued
+    # directly they ran ~1 % (one GPU) and 2-4 % (the 1/8 share of an 8-GPU step) faster than
+    # the same nodes as a graph replay (profiles/r5/graph_vs_direct.md): a hipGraphLaunch
+    # costs more than two kernel launches. --graph-batches replays them anyway.
+    direct_batches = bool(graphs and plan is not None and plan.multistep
+                          and not args.graph_batches)
+    if direct_batches:
+        graphs = False
     pipeline = not args.no_pipeline and (world > 1 or args.force_collective)
 
     if cpu:  # torch fp64 evaluation of the rank slice + gloo all_reduce per step
@@ -498,9 +511,13 @@ def main(argv=None) -> int:
                 "pipeline": pipeline,
                 "bucketed_allreduce": bool(plan.bucketed) if plan is not None else False,
                 "fused_reduction": not args.unfused,
-                "chained_batches": bool(plan.chained) and graphs if plan is not None else False,
-                # a graph batch is ONE persistent launch of all its steps + a closing kernel
-                "multistep": bool(plan.multistep) and graphs if plan is not None else False,
+                "chained_batches": bool(plan.chained) and (graphs or direct_batches)
+                if plan is not None else False,
+                # a batch is ONE persistent launch of all its steps + a closing kernel
+                "multistep": bool(plan.multistep) and (graphs or direct_batches)
+                if plan is not None else False,
+                # multi-step batches: their two kernels enqueued directly, or a graph replay
+                "batch_launch": ("direct" if direct_batches else "graph" if graphs else "none"),
                 "step_streams": plan.step_streams(min(args.steps, plan.slots))
                 if plan is not None else 1,
                 "grid": plan.grid if plan is not None else 0,
@@ -584,27 +601,31 @@ def result_ok(integrand: str, rule: str, dtype: str, n: int, abs_err: float, spe
     return abs_err <= (4.0 * span / n + 1e-12 if rule == "left" else 1e-9)
 
 
-def _timed_steps(ctx, plan, steps, pipeline, dev) -> float:
-    """ms per step of `steps` graph-replayed steps (slowest rank), warmed and bracketed."""
+def _timed_steps(ctx, plan, steps, pipeline, dev, graph_batches: bool = False) -> float:
+    """ms per step of `steps` steps in batches (slowest rank), warmed and bracketed: graph
+    replays, except a multi-step plan's batches, whose two kernels are launched directly
+    (see main) unless graph_batches."""
     import torch
 
-    plan.prepare_steps(steps)
-    # warm + clock settle: >= 30 ms of the same replays. The replay count is agreed across
-    # ranks (MAX) — every replay holds a collective, so every rank must run the same number.
+    graphs = graph_batches or not plan.multistep
+    if graphs:
+        plan.prepare_steps(steps)
+    # warm + clock settle: >= 30 ms of the same batches. The count is agreed across ranks
+    # (MAX) — every batch holds a collective, so every rank must run the same number.
     t_w = time.perf_counter()
-    plan.launch_steps(steps, pipeline, True)
+    plan.launch_steps(steps, pipeline, graphs)
     plan.sync()
     per = max(time.perf_counter() - t_w, 1e-6)
     reps = torch.tensor([math.ceil(0.03 / per)], dtype=torch.float64, device=dev)
     ctx.all_reduce_max(reps)
     for _ in range(int(reps.item())):
-        plan.launch_steps(steps, pipeline, True)
+        plan.launch_steps(steps, pipeline, graphs)
     plan.sync()
     ctx.barrier()
     plan.barrier()  # device barrier (see main's timed region)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    plan.launch_steps(steps, pipeline, True)
+    plan.launch_steps(steps, pipeline, graphs)
     plan.sync()
     torch.cuda.synchronize()
     t = torch.tensor([(time.perf_counter() - t0) / steps * 1e3], dtype=torch.float64, device=dev)
@@ -691,7 +712,7 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
     if pi4 and args.div != "ieee":
         ie = Integrator(args.integrand, n=n_total, div="ieee", **kw)
         steps = 40
-        ms = _timed_steps(ctx, ie.plan, steps, pipeline, dev)
+        ms = _timed_steps(ctx, ie.plan, steps, pipeline, dev, args.graph_batches)
         v = ie.plan.host_result(ie.plan.host_index_of(steps - 1, True))
         e = abs(v - math.pi)
         out["ieee_div"] = {"value": n_total / (ms * 1e-3), "ms_per_step": ms, "steps": steps,
@@ -758,7 +779,7 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
         alt = "series" if args.div == "series_exact" else "series_exact"
         ex = Integrator(args.integrand, n=n_total, div=alt, **kw)
         steps = 48
-        ms = _timed_steps(ctx, ex.plan, steps, pipeline, dev)
+        ms = _timed_steps(ctx, ex.plan, steps, pipeline, dev, args.graph_batches)
         v = ex.plan.host_result(ex.plan.host_index_of(steps - 1, True))
         e = abs(v - math.pi)
         ab = {"series_exact": 2.0}.get(alt, 5.0)
@@ -779,7 +800,7 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
         key, n1 = ("weak_1e9_per_gpu", 10**9 * ctx.world) if weak_extra else ("strong_1e9", 10**9)
         st = Integrator("pi4", n=n1, div=args.div, **dict(kw, dtype="fp64"))
         steps = 48
-        ms = _timed_steps(ctx, st.plan, steps, pipeline, dev)
+        ms = _timed_steps(ctx, st.plan, steps, pipeline, dev, args.graph_batches)
         v = st.plan.host_result(st.plan.host_index_of(steps - 1, True))
         e = abs(v - math.pi)
         out[key] = {"N": n1, "value": n1 / (ms * 1e-3), "ms_per_step": ms,
@@ -793,7 +814,7 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
         n3 = 10**10
         st = Integrator("pi4", n=n3, div=args.div, **dict(kw, dtype="fp64"))
         steps = 20
-        ms = _timed_steps(ctx, st.plan, steps, pipeline, dev)
+        ms = _timed_steps(ctx, st.plan, steps, pipeline, dev, args.graph_batches)
         v = st.plan.host_result(st.plan.host_index_of(steps - 1, True))
         e = abs(v - math.pi)
         out["baseline3_strong_1e10"] = {"N": n3, "value": n3 / (ms * 1e-3), "ms_per_step": ms,
@@ -843,7 +864,7 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
         # two full 48-step batches: a batch's fixed cost (~28 us: launch, ramp, tail, close,
         # syncs; profiles/r4/replay_overhead.jsonl) is 1.8 % of a 40-step fp32 batch
         steps = 96
-        ms = _timed_steps(ctx, f32.plan, steps, pipeline, dev)
+        ms = _timed_steps(ctx, f32.plan, steps, pipeline, dev, args.graph_batches)
         v = f32.plan.host_result(f32.plan.host_index_of(steps - 1, True))
         ref = integ.plan.host_result(integ.plan.host_index_of(0, True))
         e, rd = abs(v - math.pi), abs(v - ref) / abs(ref)
@@ -857,7 +878,7 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
         # v_add_f32_dpp wave reduction, fp32 LDS step): the all-fp32 reduction the config
         # names, kept as the measured alternative (bound: fp32-level agreement, 1e-6)
         fa = Integrator("pi4", n=n_total, div=args.div, **dict(kw, dtype="fp32acc"))
-        ms = _timed_steps(ctx, fa.plan, steps, pipeline, dev)
+        ms = _timed_steps(ctx, fa.plan, steps, pipeline, dev, args.graph_batches)
         v = fa.plan.host_result(fa.plan.host_index_of(steps - 1, True))
         e, rd = abs(v - math.pi), abs(v - ref) / abs(ref)
         out["baseline4_fp32_accum32"] = {"value": n_total / (ms * 1e-3), "ms_per_step": ms,
@@ -878,7 +899,7 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
         for name in ("sin", "train", "table", "poly"):
             it = Integrator(name, n=n_total, **dict(kw, dtype="fp64"))
             steps = 48
-            ms = _timed_steps(ctx, it.plan, steps, pipeline, dev)
+            ms = _timed_steps(ctx, it.plan, steps, pipeline, dev, args.graph_batches)
             v = it.plan.host_result(it.plan.host_index_of(steps - 1, True))
             e = abs(v - it.spec.analytic())
             out[f"integrand_{name}"] = {

@@ -117,6 +117,9 @@ def sweep(counts: list[int], steps: int = 200, warmup: int = 10, comm: bool = Tr
             "rccl_nnodes": b.get("rccl_nnodes"),
             "transport_error": b.get("transport_error"),
             "graphs": b["config"]["graphs"],
+            # how a batch was launched: one persistent multi-step launch + close enqueued
+            # directly (the default), or a graph replay
+            "batch_launch": b["config"].get("batch_launch"),
             "verified": b["verified"],
         }
         if n > have:

@@ -452,14 +452,17 @@ def test_bench_native_comm_failure_falls_back_to_torch(native, cuda):
 
 @pytest.mark.parametrize("bucket", [True, False])
 def test_bench_force_collective_graph(native, cuda, bucket):
+    """The 1-rank RCCL stage with the multi-step batches replayed as hipGraphs
+    (--graph-batches; the default launches them directly, test_bench_contract)."""
     p = _run(["python", os.path.join(REPO, "bench.py"), "--steps", "40", "--warmup", "8",
-              "--force-collective"] + ([] if bucket else ["--no-bucket"]))
+              "--force-collective", "--graph-batches"] + ([] if bucket else ["--no-bucket"]))
     assert p.returncode == 0, p.stderr[-2000:]
     js = json.loads(p.stdout.strip().splitlines()[-1])
     bad = [k for k, v in js.items() if isinstance(v, dict) and v.get("verified") is False]
     assert "extras_error" not in js, js["extras_error"]
     assert js["verified"] and not bad, bad
     assert js["config"]["graphs"] and js["config"]["pipeline"]
+    assert js["config"]["batch_launch"] == "graph"
     assert js["config"]["bucketed_allreduce"] == bucket
 
 
@@ -472,9 +475,12 @@ def test_bench_contract(native, cuda):
         assert k in js
     assert js["n_gpus"] == 1 and js["steps"] == 20 and js["verified"]
     assert js["value"] > 1e11
-    # the 20 timed steps are ONE replay of a captured 20-step graph (slots = 48)
-    assert js["graph_replays_timed"] == 1 and js["direct_steps_timed"] == 0
-    assert js["config"]["graphs"] is True
+    # the 20 timed steps are ONE multi-step batch (slots = 48): one persistent launch of the
+    # 20 steps and its closing kernel, enqueued directly (measured faster than the same two
+    # kernels as a graph replay, profiles/r5/graph_vs_direct.md)
+    assert js["direct_steps_timed"] == 20 and js["graph_replays_timed"] == 0
+    assert js["config"]["batch_launch"] == "direct" and js["config"]["multistep"]
+    assert js["config"]["graphs"] is False
     # the record carries what the headline rests on: IEEE-division speed and per-point ulp
     assert js["ieee_div_value"] > 1e11 and js["ieee_div"]["abs_err"] < 2e-9
     # the headline division (series_exact): per point within 2 ulp of the IEEE path's own

@@ -138,7 +138,8 @@ def test_bench_two_ranks_native_rccl_one_gpu(cuda):
     assert r["rccl_world"] == 2 and r["native_rccl_comms"] == 1 and r["torch_nccl_groups"] == 0
     assert r["rccl_transport"] == "NET/Socket" and r["rccl_nnodes"] == 2
     assert r["transport_verified"] and r["transport_error"] is None
-    assert r["comm_fallback"] is None and r["graph_replays_timed"] == 1
+    assert r["comm_fallback"] is None and r["config"]["batch_launch"] == "direct"
+    assert r["direct_steps_timed"] == 10 and r["config"]["multistep"]
     assert r["config"]["bucketed_allreduce"] and r["config"]["N"] == 10**9
     assert r["config"]["n_per_gpu"] == 5 * 10**8 and r["scaling"] == "strong"
 

@@ -92,7 +92,8 @@ def test_bench_torchrun_rccl(native, cuda, g):
     assert js["verified"] and js["n_gpus"] == g and js["config"]["N"] == 10**9
     assert js["scaling"] == "strong" and js["config"]["n_per_gpu"] == 10**9 // g
     assert abs(js["abs_err"] - 1e-9) < 1e-13  # the N = 1e9 left-rule truncation
-    assert js["config"]["bucketed_allreduce"] and js["config"]["graphs"]
+    assert js["config"]["bucketed_allreduce"] and js["config"]["multistep"]
+    assert js["config"]["batch_launch"] == "direct"
     assert js["rccl_transport"].startswith("P2P") and js["rccl_nnodes"] == 1
     assert js["transport_verified"] and js["transport_error"] is None
     assert js["weak_1e9_per_gpu"]["N"] == g * 10**9 and js["weak_1e9_per_gpu"]["verified"]

@@ -9,6 +9,7 @@ Forms (each: launch_steps(K) on the plan's compute stream, then ...):
   plan_sync    plan.sync() (hipStreamSynchronize) + torch.cuda.synchronize()   (bench.py today)
   poll         native.wait_with_timeout(compute stream) (hipStreamQuery spin) + torch sync
   torch_only   torch.cuda.synchronize() alone
+  direct_plan_sync   the batch's two kernels launched directly (no graph), plan.sync + torch
 The device span comes from hipEvents recorded around the same launch (separate reps).
 """
 from __future__ import annotations
@@ -53,26 +54,31 @@ def main(argv=None) -> int:
         torch.cuda.synchronize()
 
     forms = {
-        "plan_sync": lambda: (plan.sync(), torch.cuda.synchronize()),
-        "poll": lambda: (m.wait_with_timeout(cs, 60.0), torch.cuda.synchronize()),
-        "torch_only": lambda: torch.cuda.synchronize(),
+        "plan_sync": (True, lambda: (plan.sync(), torch.cuda.synchronize())),
+        "poll": (True, lambda: (m.wait_with_timeout(cs, 60.0), torch.cuda.synchronize())),
+        "torch_only": (True, lambda: torch.cuda.synchronize()),
+        # the batch's two kernels launched directly instead of as a graph replay
+        "direct_plan_sync": (False, lambda: (plan.sync(), torch.cuda.synchronize())),
     }
     rows = []
     settle()
     for rep in range(a.reps):
-        for name, wait in forms.items():
+        for name, (graphs, wait) in forms.items():
             idle_sync()
             t0 = time.perf_counter()
-            plan.launch_steps(K, True, True)
+            plan.launch_steps(K, True, graphs)
             wait()
             rows.append((name, (time.perf_counter() - t0) * 1e6))
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        idle_sync()
-        e0.record(stream)
-        plan.launch_steps(K, True, True)
-        e1.record(stream)
-        torch.cuda.synchronize()
-        rows.append(("device_events", e0.elapsed_time(e1) * 1e3))
+        for graphs in (True, False):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            idle_sync()
+            e0.record(stream)
+            plan.launch_steps(K, True, graphs)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            rows.append(("device_events" if graphs else "direct_device_events",
+                         e0.elapsed_time(e1) * 1e3))
         t0 = time.perf_counter()
         torch.cuda.synchronize()
         rows.append(("idle_torch_sync", (time.perf_counter() - t0) * 1e6))

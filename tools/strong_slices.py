@@ -22,20 +22,21 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def timed(plan, steps: int, pipeline: bool) -> float:
-    """ms per step of graph-replayed batches, after >= 30 ms of the same replays."""
+def timed(plan, steps: int, pipeline: bool, graphs: bool = True) -> float:
+    """ms per step of graph-replayed (or directly launched) batches, after >= 30 ms of the
+    same batches."""
     plan.prepare_steps(steps)
     t = time.perf_counter()
-    plan.launch_steps(steps, pipeline, True)
+    plan.launch_steps(steps, pipeline, graphs)
     plan.sync()
     reps = max(1, math.ceil(0.03 / max(time.perf_counter() - t, 1e-6)))
     for _ in range(reps):
-        plan.launch_steps(steps, pipeline, True)
+        plan.launch_steps(steps, pipeline, graphs)
     plan.sync()
     best = math.inf
     for _ in range(5):
         t = time.perf_counter()
-        plan.launch_steps(steps, pipeline, True)
+        plan.launch_steps(steps, pipeline, graphs)
         plan.sync()
         best = min(best, (time.perf_counter() - t) / steps * 1e3)
     return best
@@ -50,6 +51,8 @@ def main(argv=None) -> int:
     ap.add_argument("--steps", type=int, default=48)
     ap.add_argument("--collective", choices=["on", "off", "both"], default="both")
     ap.add_argument("--step-streams", default="0", help="comma list (0 = the plan's auto)")
+    ap.add_argument("--graphs", choices=["on", "off", "both"], default="on",
+                    help="batches as graph replays, direct launches, or both")
     ap.add_argument("--jsonl", default="")
     a = ap.parse_args(argv)
 
@@ -58,20 +61,22 @@ def main(argv=None) -> int:
     n = int(a.n)
     rows = []
     modes = {"on": [True], "off": [False], "both": [True, False]}[a.collective]
-    configs = [(gr, c, q) for gr in (int(x) for x in a.grids.split(","))
-               for c in modes for q in (int(y) for y in a.step_streams.split(","))]
+    gmodes = {"on": [True], "off": [False], "both": [True, False]}[a.graphs]
+    configs = [(gr, c, q, gm) for gr in (int(x) for x in a.grids.split(","))
+               for c in modes for q in (int(y) for y in a.step_streams.split(","))
+               for gm in gmodes]
     for g in (int(x) for x in a.gpus.split(",")):
-        for grid, coll, ss in configs:
+        for grid, coll, ss, gm in configs:
             it = Integrator("pi4", n=n, slots=48, grid=grid, force_collective=coll,
                             slice_of=(0, g), step_streams=ss)
-            ms = timed(it.plan, a.steps, coll)
+            ms = timed(it.plan, a.steps, coll, gm)
             v = it.plan.host_result(it.plan.host_index_of(a.steps - 1, True))
             # rank 0's slice of [0, 1): its exact integral is 4 atan(x1)
             x1 = it.plan.count / n
             err = abs(v - 4.0 * math.atan(x1))
             row = {"G": g, "n_total": n, "n_per_gpu": it.plan.count,
                    "grid": it.plan.grid, "grid_arg": grid, "rccl_stage": coll,
-                   "step_streams": it.plan.step_streams(a.steps),
+                   "step_streams": it.plan.step_streams(a.steps), "graphs": gm,
                    "ms_per_step": ms, "us_per_step": ms * 1e3,
                    "per_gpu_subint_per_s": it.plan.count / (ms * 1e-3),
                    "projected_strong_value": n / (ms * 1e-3),
@@ -79,7 +84,7 @@ def main(argv=None) -> int:
             rows.append(row)
             print(json.dumps(row), flush=True)
             del it
-    key = lambda r: (r["grid_arg"], r["rccl_stage"], r["step_streams"])  # noqa: E731
+    key = lambda r: (r["grid_arg"], r["rccl_stage"], r["step_streams"], r["graphs"])  # noqa: E731
     base = {key(r): r["ms_per_step"] for r in rows if r["G"] == 1}
     for r in rows:
         b = base.get(key(r))

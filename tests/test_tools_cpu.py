@@ -128,3 +128,25 @@ def test_shared_rccl_report_flags_records_above_one_rank(tmp_path):
     assert "NET/Socket" in rows["riemann_np2"]
     assert p.stdout.count("miint_comm_np2") == 1  # one row per step
     assert "one-rank rate: 1" in p.stdout
+
+
+def test_roofline_t2d_multistep_counts_the_replay(tmp_path):
+    """A 2-D multi-step dispatch runs one replay of integrations (512 of 4096^2 since round 5,
+    Table2DPlan::graph_steps): VALU per sample divides by all of them; a Riemann multi-step
+    dispatch is not multiplied."""
+    d = tmp_path / "table2d_G1"
+    os.makedirs(d)
+    with open(d / "run_counter_collection.csv", "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=["Dispatch_Id", "Correlation_Id", "Kernel_Name",
+                                          "Counter_Name", "Counter_Value", "Start_Timestamp",
+                                          "End_Timestamp"])
+        w.writeheader()
+        w.writerow({"Dispatch_Id": 1, "Correlation_Id": 1,
+                    "Kernel_Name": "void miint::(anonymous namespace)::table2d_multistep_kernel<30>(x)",
+                    "Counter_Name": "SQ_INSTS_VALU", "Counter_Value": 9.23e8,
+                    "Start_Timestamp": 0, "End_Timestamp": 2_231_100})
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "roofline.py"),
+                          str(tmp_path)], capture_output=True, text=True, check=True).stdout
+    row = [ln for ln in out.splitlines() if ln.startswith("| table2d")][0]
+    cells = [c.strip() for c in row.strip("|").split("|")]
+    assert cells[4] == f"{9.23e8 * 64 / (4096 * 4096 * 512):.2f}" == "6.88"

@@ -318,6 +318,7 @@ def main(argv=None) -> int:
                           and not args.graph_batches)
     if direct_batches:
         graphs = False
+    ran_plan = plan is not None and not use_torch and not cpu  # the native plan ran the steps
     pipeline = not args.no_pipeline and (world > 1 or args.force_collective)
 
     if cpu:  # torch fp64 evaluation of the rank slice + gloo all_reduce per step
@@ -511,13 +512,14 @@ def main(argv=None) -> int:
                 "pipeline": pipeline,
                 "bucketed_allreduce": bool(plan.bucketed) if plan is not None else False,
                 "fused_reduction": not args.unfused,
-                "chained_batches": bool(plan.chained) and (graphs or direct_batches)
-                if plan is not None else False,
+                "chained_batches": bool(ran_plan and plan.chained and (graphs or plan.multistep)),
                 # a batch is ONE persistent launch of all its steps + a closing kernel
-                "multistep": bool(plan.multistep) and (graphs or direct_batches)
-                if plan is not None else False,
-                # multi-step batches: their two kernels enqueued directly, or a graph replay
-                "batch_launch": ("direct" if direct_batches else "graph" if graphs else "none"),
+                "multistep": bool(ran_plan and plan.multistep),
+                # how the timed batches were launched: a graph replay, a multi-step batch's
+                # two kernels enqueued directly, or one launch per step
+                "batch_launch": ("graph" if graphs else
+                                 "direct" if ran_plan and plan.multistep else
+                                 "per-step" if ran_plan else "none"),
                 "step_streams": plan.step_streams(min(args.steps, plan.slots))
                 if plan is not None else 1,
                 "grid": plan.grid if plan is not None else 0,

@@ -69,35 +69,37 @@ struct TileDefaults {
 // g_{+-k} = c_k +- k A. c_k is formed directly with one fma from an SGPR k^2 (no running
 // recurrence: increments of ~1e-17 would be lost against ulp(1/2)). Per PAIR of samples:
 // 1 fma for c_k, 2 for g, 2 accumulations = 2.5 VALU per sample.
-// A 192-sample tile is 6 sub-tiles of 32 whose centres sit at c0 = -80, -48, ..., 48, 80
-// steps from x_m; re-expanding the exact quadratic there gives e_c = e_m + c0 A + c0^2 B and
-// slope A' = A + 2 c0 B (3 fma per sub-tile, against ~10 for a fresh seed). The 16 pair
-// constants k_j and k_j^2 - kMeanK2 and the centre tables fill 96 SGPRs, 11 of the
-// k_j^2 - kMeanK2 sit in VGPRs: 64 VGPRs, 8 resident workgroups per CU.
-// Measured (gfx950 .s, tools/isa_count.py): 508 VALU per 192-sample tile = 2.65 per sample
-// (128-sample tiles of 4: 342 = 2.67; 8 sub-tiles of 16: 354 per 128 = 2.77; 64-sample
-// tiles with a Newton step: 183 per 64 = 2.86; the first form, t += e; t = fma(e, e, t) with
-// one seed per 32 samples: 127 per 32 = 3.97).
+// A 384-sample tile is 12 sub-tiles of 32 whose centres sit at c0 = -176, -144, ..., 144,
+// 176 steps from x_m; re-expanding the exact quadratic there gives e_c = e_m + c0 A + c0^2 B
+// and slope A' = A + 2 c0 B (3 fma per sub-tile, against ~10 for a fresh seed). The 16 pair
+// constants k_j and k_j^2 - kMeanK2 sit in SGPRs and VGPRs, the centre tables in SGPRs.
+// Measured (gfx950 .s, tools/isa_guard.py): 1007 VALU per 384-sample tile = 2.62 per sample
+// (round 5; 192-sample tiles of 6: 508 = 2.65 — the per-seed work over twice the samples,
+// 1.2 % less time for kSeries, 1.8 % for kSeriesExact, profiles/r5/tile384_ab.md; 128-sample
+// tiles of 4: 342 = 2.67; 8 sub-tiles of 16: 354 per 128 = 2.77; 64-sample tiles with a
+// Newton step: 183 per 64 = 2.86; the first form, t += e; t = fma(e, e, t) with one seed per
+// 32 samples: 127 per 32 = 3.97).
 //
 // Accuracy: every sample still gets its own residual and its own contribution. Per point,
 // g is rounded at ulp(1/2) scale: <= 5 ulp vs IEEE division anywhere. On the bench record's
-// window (64 K samples from x = 0.125, N = 1e9; BENCH_r02 / test_pi4_series_record_window):
-// max 4 ulp, 83.2 % of points within 1 ulp (|d| <= 1), 98.1 % within 2. (Round 1 quoted
+// window (64 K samples from x = 0.125, N = 1e9; test_pi4_series_record_window): max 4 ulp,
+// 82.5 % of points within 1 ulp (|d| <= 1), 98.0 % within 2 with 384-sample tiles (83.2 /
+// 98.1 % with 192). (Round 1 quoted
 // "92 % within 1": tools/ulp_probe.py then binned round(|d|), i.e. |d| < 1.5.) The sum agrees
 // with the IEEE path to 1e-15 relative and |error| at N = 1e9 is unchanged (4.4e-16, mid).
 struct Pi4 : TileDefaults<Pi4> {
   static constexpr double kScale = 4.0;
   static constexpr int kPairs = 16;                 // sample pairs per sub-tile
   static constexpr int kSub = 2 * kPairs;           // 32 samples per sub-tile
-  // Sub-tiles per series tile: 6 (192 samples per seed; 128-sample tiles of 4 ran 342 VALU
-  // per 128 samples, these 508 per 192: 1.35e13 -> 1.36e13 subint/s at N = 1e9, and 1e9 /
-  // 192 deals 9.93 tiles per lane of the 2048 x 256 grid, as even as 128's 14.9).
-  static constexpr int kSubs = 6;
-  static constexpr int kSeriesTile = kSub * kSubs;  // 192 samples per seed
+  // Sub-tiles per series tile: 12 (384 samples per seed; 6 sub-tiles ran 508 VALU per 192
+  // samples, these 1007 per 384: 73.1 -> 71.8 us at N = 1e9 with series_exact). The longer
+  // tile needs 192 h <= 2e-6 (kSeriesHalfSpan): N >= 9.6e7 on [0, 1].
+  static constexpr int kSubs = 12;
+  static constexpr int kSeriesTile = kSub * kSubs;  // 384 samples per seed
   // sum over a series tile's samples of k_u^2, k_u = u - (U-1)/2: 2 sum_{j<U/2} (j + 1/2)^2
   static constexpr double kSumK2 = (kSeriesTile / 2) * (kSeriesTile / 2 - 1) * (kSeriesTile - 1) / 3.0 +
                                    (kSeriesTile / 2) * (kSeriesTile / 2 - 1) + kSeriesTile / 4.0;
-  static_assert(kSumK2 == 589808.0, "sum of squared midpoint offsets of a 192-sample tile");
+  static_assert(kSumK2 == 4718560.0, "sum of squared midpoint offsets of a 384-sample tile");
 
   template <DivMode M>
   __host__ __device__ static constexpr int tile_len() {

@@ -24,15 +24,17 @@ inline bool is_fp32(DType t) { return t == DType::kF32 || t == DType::kF32Acc32;
 // Tile (unroll) size of the Riemann kernels: U consecutive samples per lane per step.
 constexpr int kRiemannTile = 32;     // default samples per lane tile (Pi4 series: 64)
 constexpr int kRiemannBlock = 256;
-constexpr int kSeriesHalfSpan = 96;  // max |sample offset| from a Pi4 series seed, in steps
+constexpr int kSeriesHalfSpan = 192;    // max |sample offset| from an fp64 Pi4 series seed, in steps
+constexpr int kSeriesHalfSpanF32 = 96;  // the same for the fp32 Pi4 series tiles
 
 constexpr int kDirectHalfSpan = 16;  // the same for kSeriesDirect's 32-sample tiles
 
 // True when the fp64 Pi4 series reciprocal is exact to fp64 for this h (see integrands.hpp).
 inline bool series_ok(double h) { return kSeriesHalfSpan * (h < 0 ? -h : h) <= 2e-6; }
+inline bool series_ok_f32(double h) { return kSeriesHalfSpanF32 * (h < 0 ? -h : h) <= 2e-6; }
 inline bool direct_ok(double h) { return kDirectHalfSpan * (h < 0 ? -h : h) <= 2e-6; }
 
-// Division mode actually used for step h: the 192-sample series tiles need N > 4.8e7 on
+// Division mode actually used for step h: the 384-sample series tiles need N >= 9.6e7 on
 // [0, 1]; a coarser step still fits the 32-sample kSeriesDirect tiles down to N = 8e6
 // (5 VALU per sample against ~10 for IEEE division); coarser steps use IEEE division.
 inline DivMode effective_div(DivMode d, double h) {
@@ -54,14 +56,14 @@ inline DivMode effective_div(DivMode d, double h, Integrand f) {
 
 constexpr int kPolySeriesMaxCoeffs = 8;  // polynomials up to degree 7 have a series path
 
-// With the dtype (the fp32 paths: pi4's 192-sample first-order tiles where series_ok, and
+// With the dtype (the fp32 paths: pi4's 192-sample first-order tiles where series_ok_f32, and
 // the packed-fp32 forms of the other integrands' series tiles) and the polynomial's
 // coefficient count (Taylor-pair tiles for up
 // to kPolySeriesMaxCoeffs coefficients, exact for any h; Horner per sample otherwise).
 inline DivMode effective_div(DivMode d, double h, Integrand f, DType t, int ncoef = 0) {
   if (is_fp32(t)) {  // fp32: one series form per integrand (integrands_f32.hpp)
     if (d == DivMode::kIeee) return DivMode::kIeee;
-    if (f == Integrand::kPi4) return series_ok(h) ? DivMode::kSeries : DivMode::kIeee;
+    if (f == Integrand::kPi4) return series_ok_f32(h) ? DivMode::kSeries : DivMode::kIeee;
     if (f == Integrand::kPoly)
       return (ncoef >= 1 && ncoef <= kPolySeriesMaxCoeffs) ? DivMode::kSeries : DivMode::kIeee;
     return DivMode::kSeries;  // sin, train velocity, table: exact for any h

@@ -358,12 +358,12 @@ struct Pi4F32Acc32 : Pi4F32 {
 };
 template <> struct AccOf<Pi4F32Acc32> { using type = float; };
 
-// The host's series validity check (series_ok: kSeriesHalfSpan * h <= 2e-6) must bound the
-// farthest sample offset of both Pi4 series tiles.
+// The host's series validity checks (series_ok: kSeriesHalfSpan * h <= 2e-6; series_ok_f32
+// with kSeriesHalfSpanF32) must bound the farthest sample offset of each Pi4 series tile.
 static_assert(2 * AngleSeries<12>::kPairs + 12 == kSinTrig, "trig table sized for Sin");
 static_assert(Pi4::kSeriesTile / 2 == kSeriesHalfSpan &&
-                  Pi4F32::kSubs * Pi4F32::kSubLen / 2 == kSeriesHalfSpan,
-              "kSeriesHalfSpan must be half the Pi4 series tile length");
+                  Pi4F32::kSubs * Pi4F32::kSubLen / 2 == kSeriesHalfSpanF32,
+              "kSeriesHalfSpan(F32) must be half the Pi4 series tile lengths");
 
 // ---------------------------------------------------------------------------- functor makers
 // Each integrand gets its own kernel instantiation (own register allocation); only the

@@ -91,6 +91,7 @@ PYBIND11_MODULE(_miint, m) {
   m.attr("RIEMANN_TILE") = kRiemannTile;
   m.attr("RIEMANN_BLOCK") = kRiemannBlock;
   m.def("series_ok", &series_ok);
+  m.def("series_ok_f32", &series_ok_f32);
   m.def("integrand_scale", &integrand_scale);
 
   // ------------------------------------------------------------------ devices

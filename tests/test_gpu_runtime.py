@@ -42,8 +42,8 @@ def test_chained_batches_equal_fused_bitwise(cuda, name, collective):
     the bucketed 1-rank RCCL stage."""
     dtype = "fp32" if name.endswith("_fp32") else "fp64"
     name = name.split("_")[0]
-    kw = dict(n=50_000_017, rule="mid", slots=8, force_collective=collective, dtype=dtype)
-    want = Integrator(name, n=50_000_017, rule="mid", dtype=dtype).run().value
+    kw = dict(n=100_000_017, rule="mid", slots=8, force_collective=collective, dtype=dtype)
+    want = Integrator(name, n=100_000_017, rule="mid", dtype=dtype).run().value
     for chain in (True, False):
         it = Integrator(name, chain=chain, **kw)
         assert it.plan.chained == chain
@@ -63,7 +63,7 @@ def test_multistep_batches_equal_chained_bitwise(cuda, name):
     parts = name.split("_")
     dtype = parts[1] if len(parts) > 1 and parts[1].startswith("fp") else "fp64"
     div = {"ieee": "ieee", "exact": "series_exact"}.get(parts[-1], "series")
-    kw = dict(n=60_000_011, rule="mid", dtype=dtype, div=div)
+    kw = dict(n=120_000_011, rule="mid", dtype=dtype, div=div)
     ms = Integrator(parts[0], slots=20, **kw)
     ch = Integrator(parts[0], slots=20, multistep=False, grid=ms.plan.grid, **kw)
     assert ms.plan.multistep and not ch.plan.multistep and ms.plan.grid == ch.plan.grid
@@ -698,7 +698,7 @@ def test_host_direct_off_copies_batch_results(native, cuda, graphs):
     slots; a multi-step (or chained) batch must still copy them into pinned memory."""
     m = native
     cfg = m.RiemannConfig()
-    cfg.integrand, cfg.n, cfg.rule = m.Integrand.pi4, 50_000_017, m.Rule.mid
+    cfg.integrand, cfg.n, cfg.rule = m.Integrand.pi4, 100_000_017, m.Rule.mid
     cfg.host_direct = False
     cfg.slots = 8
     p = m.RiemannPlan(cfg, 0)

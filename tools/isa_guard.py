@@ -39,9 +39,9 @@ VALU_SLACK = 1.03
 CH = r"riemann_chained_kernel(?:_o8)?ILNS_7DivModeE"
 MS = r"riemann_multistep_kernel(?:_o8)?ILNS_7DivModeE"
 GUARDED = {
-    "pi4_series": ("riemann", CH + r"0ENS_3Pi4EE", 192),
+    "pi4_series": ("riemann", CH + r"0ENS_3Pi4EE", 384),
     "pi4_ieee": ("riemann", CH + r"1ENS_3Pi4EE", 32),
-    "pi4_series_exact": ("riemann", CH + r"3ENS_3Pi4EE", 192),
+    "pi4_series_exact": ("riemann", CH + r"3ENS_3Pi4EE", 384),
     "sin_series": ("riemann", CH + r"0ENS_3SinEE", 192),
     "sin_ieee": ("riemann", CH + r"1ENS_3SinEE", 32),
     "train_series": ("riemann", CH + r"0ENS_8TrainVelEE", 128),

@@ -264,3 +264,5 @@ def test_bench_multi_rank_record_is_the_metric_config():
     assert js["config"]["global_batch"] == 10**9
     assert js["verified"] and abs(js["abs_err"] - (1e-9 - 1e-18 / 6)) <= 1e-13
     assert js["value"] == pytest.approx(10**9 / (js["ms_per_step"] * 1e-3))
+    # the CPU path runs no native plan: no batches to launch, none claimed
+    assert js["config"]["batch_launch"] == "none" and not js["config"]["multistep"]

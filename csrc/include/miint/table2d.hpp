@@ -139,6 +139,12 @@ class Table2DPlan {
   Graph graph_;
 };
 
+// Auto integrations per multi-step replay (Table2DPlan::graph_steps) for a g x g grid whose
+// rows are split over `world` ranks: from the configuration only — the largest rank's row
+// count and whether that shape runs the row stream — so every rank of a collective plan
+// replays the same count. kGraphSteps when the shape has no multi-step launch.
+int table2d_auto_graph_steps(int grid, double extent, int world);
+
 // Host oracle for the midpoint sum on a g x g grid: (sum_j v(x_j) dx)^2.
 double table2d_oracle(int grid, double extent = 1800.0);
 

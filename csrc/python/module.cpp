@@ -543,6 +543,8 @@ PYBIND11_MODULE(_miint, m) {
       .def_property_readonly("row0", &Table2DPlan::row0)
       .def_property_readonly("row1", &Table2DPlan::row1);
   m.def("table2d_oracle", &table2d_oracle, py::arg("grid"), py::arg("extent") = 1800.0);
+  m.def("table2d_auto_graph_steps", &table2d_auto_graph_steps, py::arg("grid"),
+        py::arg("extent") = 1800.0, py::arg("world") = 1);
   m.def("launch_trainscan", [](uintptr_t table, int tn, double dt, uint64_t i0, uint64_t n,
                                uint64_t win_lo, uint64_t win_hi, uintptr_t ws, uintptr_t totals,
                                uintptr_t carries, uintptr_t vel, uintptr_t pos, uintptr_t s) {

@@ -53,17 +53,10 @@ Table2DPlan::Table2DPlan(const Table2DConfig& cfg, int device, const Comm* comm)
               "table2d: graph_steps 0 (auto) or 1..kT2MaxReplaySteps");
   if (cfg.graph_steps > 0) {
     graph_steps_ = cfg.graph_steps;
-  } else if (const int rows = (cfg.grid + world_ - 1) / world_;
-             cfg.multistep && chained() &&
-             table2d_multistep_ok(Table2DParams{table_.get(), n, n, cfg.extent, cfg.extent,
-                                                cfg.grid, cfg.grid, 0, rows, 1},
-                                  cus)) {
-    // From the configuration only (the largest rank's row count, not this rank's rows):
-    // every rank of a collective plan must replay the same count, its all-reduce covering
-    // graph_steps_ values.
-    const double samples = static_cast<double>(cfg.grid) * rows;
-    while (graph_steps_ < kT2MaxReplaySteps && graph_steps_ * samples < kReplaySamples)
-      graph_steps_ *= 2;
+  } else if (cfg.multistep && chained()) {
+    // from the configuration only: every rank of a collective plan must replay the same
+    // count, its all-reduce covering graph_steps_ values
+    graph_steps_ = table2d_auto_graph_steps(cfg.grid, cfg.extent, world_);
   }
   if (multistep_) {
     ms_partials_ = DeviceBuffer<double>(static_cast<size_t>(graph_steps_) * partials_.size());
@@ -221,6 +214,20 @@ double Table2DPlan::time(int iters, bool graphs) {
 
 double Table2DPlan::last_result() const {
   return last_batched_ ? host_[graph_steps_ - 1] : host_[0];
+}
+
+int table2d_auto_graph_steps(int grid, double extent, int world) {
+  MIINT_CHECK(grid >= 1 && world >= 1, "table2d: grid and world >= 1");
+  const int n = static_cast<int>(oracle::profile_table().size());
+  const int rows = (grid + world - 1) / world;  // the largest rank's rows
+  // (num_cus is not consulted: the row-stream shape needs no residency)
+  if (!table2d_multistep_ok(Table2DParams{nullptr, n, n, extent, extent, grid, grid, 0, rows, 1},
+                            0))
+    return Table2DPlan::kGraphSteps;
+  const double samples = static_cast<double>(grid) * rows;
+  int steps = Table2DPlan::kGraphSteps;
+  while (steps < kT2MaxReplaySteps && steps * samples < Table2DPlan::kReplaySamples) steps *= 2;
+  return steps;
 }
 
 double table2d_oracle(int grid, double extent) {

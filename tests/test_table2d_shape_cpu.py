@@ -79,3 +79,26 @@ def test_4096_shapes():
     assert full["rows_per_wave"] == 16 and full["tile_rows"] == 30 and full["grid"] == (16, 64)
     s8 = m.table2d_shape_info(1801, 1801, 1800.0, 1800.0, 4096, 4096, 0, 512, 1)
     assert s8["rows_per_wave"] == 16 and s8["grid"] == (16, 8)
+
+
+def test_auto_replay_steps_rule():
+    """Table2DPlan's auto replay size (table2d_auto_graph_steps, host code): doubled from 32
+    until a replay holds 2^33 samples of the LARGEST rank's rows, capped at 1024; 32 for a
+    shape without the row stream (chained replays of one kernel node per integration). The
+    same answer for every rank of an uneven split (it depends on grid and world only)."""
+    m = native()
+    assert m.table2d_auto_graph_steps(4096) == 512
+    assert m.table2d_auto_graph_steps(4096, world=2) == 1024
+    assert m.table2d_auto_graph_steps(4096, world=8) == 1024
+    assert m.table2d_auto_graph_steps(4095, world=8) == 1024
+    assert m.table2d_auto_graph_steps(8192) == 128
+    assert m.table2d_auto_graph_steps(16384) == 32  # 2^28 samples x 32 = 2^33 already
+    assert m.table2d_auto_graph_steps(1000) == 32   # the tile kernel
+    assert m.table2d_auto_graph_steps(2048) == 32   # 0.88 table cells per sample: the tile kernel
+    for g in (4096, 6144, 8192):  # row-stream shapes
+        for w in (1, 2, 3, 4, 8):
+            s = m.table2d_auto_graph_steps(g, world=w)
+            rows = -(-g // w)
+            assert s in (32, 64, 128, 256, 512, 1024)
+            assert s == 1024 or s * g * rows >= 2**33
+            assert s == 32 or (s // 2) * g * rows < 2**33

@@ -110,11 +110,14 @@ def test_cintegrate_and_miint_ranks_share_gpu(cuda):
     c = _records(_np(2, os.path.join(BIN, "cintegrate"), "--json"))[0]
     _shared_rccl(c, 2)
     assert abs(c["result"] - 122000.004) < 1e-6
-    b = _records(_np(2, os.path.join(BIN, "miint"), "bench", "--integrand", "pi4", "--iters", "20",
-                     "--settle", "20"))[0]
+    # both runs settled (~60 ms of steps, the default): a 20-step settle left the one-rank
+    # run inside the clock ramp (1.04e13) while the two ranks' longer run was past it
+    # (1.12e13 aggregate), which flipped this sanity check once
+    b = _records(_np(2, os.path.join(BIN, "miint"), "bench", "--integrand", "pi4", "--iters",
+                     "200"))[0]
     _shared_rccl(b, 2)
-    one = _records([os.path.join(BIN, "miint"), "bench", "--integrand", "pi4", "--iters", "20",
-                    "--settle", "20"])[0]
+    one = _records([os.path.join(BIN, "miint"), "bench", "--integrand", "pi4", "--iters",
+                    "200"])[0]
     assert b["subintervals_per_s"] <= 1.05 * one["subintervals_per_s"], (b, one)
 
 

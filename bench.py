@@ -134,6 +134,12 @@ def parse(argv=None) -> argparse.Namespace:
     p.add_argument("--sweep-gpus", default="",
                    help="e.g. 1,2,4,8: run the scaling sweep (cuda_v_mpi_amd/parallel/scaling.py) "
                         "over these GPU counts instead of one benchmark")
+    p.add_argument("--no-diag", action="store_true",
+                   help="skip the untimed diagnostic batch and communicator probes that a "
+                        "multi-rank run records after its timed region (diagnostic_batch)")
+    p.add_argument("--diag-allgather-mb", type=float, default=144.0,
+                   help="total size of the diagnostic allgather (the reference's 144 MB "
+                        "table, 4main.c:157)")
     p.add_argument("--verbose", action="store_true")
     p.add_argument("--jsonl", default="", help="also append the JSON line to this file")
     return p.parse_args(argv)
@@ -429,8 +435,17 @@ def main(argv=None) -> int:
     # the transport check applies only where RCCL carried the ranks' collectives
     transport_error = transport_check(world, share, transport,
                                       rccl=not cpu and bool(native_rccl or ctx.nccl_groups))
+    native_comm_ok = comm_fallback is None
     if transport_error:
         print(f"bench.py: {transport_error}", file=sys.stderr)
+    diag = None
+    if world > 1 and not args.no_diag:
+        # untimed, after the timed region: where a multi-GPU step's time went
+        try:
+            diag = batch_diagnostics(args, ctx, integ, plan, dev, cpu, use_torch, transport)
+        except Exception as e:  # noqa: BLE001  (every rank runs the same probes)
+            diag = {"error": f"{type(e).__name__}: {e}"}
+            print(f"bench.py: diagnostics failed: {diag['error']}", file=sys.stderr)
     extras = {}
     extras_ok = True
     if not cpu and not use_torch and not args.no_extras:
@@ -465,8 +480,9 @@ def main(argv=None) -> int:
             "data": "synthetic (analytic integrand 4/(1+x^2); no dataset)",
             "abs_err": abs_err,
             "result": vals[-1],
-            "verified": bool(ok and extras_ok and not transport_error),
+            "verified": record_verified(ok, extras_ok, transport_error, comm_fallback),
             "headline_verified": ok,
+            "native_comm_verified": native_comm_ok,
             "extras_verified": extras_ok,
             "transport_verified": not transport_error,
             "transport_error": transport_error,
@@ -493,6 +509,7 @@ def main(argv=None) -> int:
             "graph_replays_timed": graph_replays,
             "comm_fallback": comm_fallback,
             "direct_steps_timed": direct_timed,
+            **({"diagnostic_batch": diag} if diag is not None else {}),
             **extras,
             "config": {
                 "model": f"riemann_{args.integrand}_{args.dtype}",
@@ -511,6 +528,11 @@ def main(argv=None) -> int:
                 "graph_nodes": plan.graph_nodes if (graphs and plan is not None) else 0,
                 "pipeline": pipeline,
                 "bucketed_allreduce": bool(plan.bucketed) if plan is not None else False,
+                # the bucketed all-reduce writes every rank's step values straight into
+                # pinned host memory (no copy after it); multi-step batches closed inside the
+                # persistent launch instead of by a closing kernel
+                "allreduce_to_host": bool(plan.allreduce_to_host) if plan is not None else False,
+                "close_in_launch": bool(plan.close_in_launch) if plan is not None else False,
                 "fused_reduction": not args.unfused,
                 "chained_batches": bool(ran_plan and plan.chained and (graphs or plan.multistep)),
                 # a batch is ONE persistent launch of all its steps + a closing kernel
@@ -533,6 +555,168 @@ def main(argv=None) -> int:
                 f.write(json.dumps(out) + "\n")
     ctx.destroy()
     return 0 if ok else 1
+
+
+def _spread(vals: list[float]) -> dict:
+    return {"max": max(vals), "min": min(vals), "per_rank": vals}
+
+
+def rccl_init_lines(path: str | None, limit: int = 16) -> dict:
+    """Channel and protocol facts from this rank's captured RCCL INIT log (NCCL_DEBUG_SUBSYS
+    INIT,P2P,GRAPH: printed once per communicator): the distinct channel ids of the peer
+    connections, and the lines naming channels, rings or protocols."""
+    import re
+
+    if not path or not os.path.exists(path):
+        return {"log": path, "channels": None, "lines": []}
+    chans, lines = set(), []
+    keep = re.compile(r"channels|nChannels|Pattern|Ring \d+|[Pp]roto|LL128|Tree \d+")
+    with open(path, errors="replace") as f:
+        for ln in f:
+            m = re.search(r"Channel (\d+)/\d+ :", ln)
+            if m:
+                chans.add(int(m.group(1)))
+            elif keep.search(ln) and len(lines) < limit:
+                lines.append(ln.split("NCCL INFO", 1)[-1].strip())
+    return {"log": path, "channels": len(chans) or None, "lines": lines}
+
+
+def comm_probes(ctx, comm, allgather_mb: float, cpu: bool) -> dict:
+    """Latency of an 8-byte all-reduce and the bus bandwidth of an allgather of
+    `allgather_mb` MB in total (each rank's 1/world share), on the run's own communicator:
+    the native RCCL one (hipEvents on the torch stream), or, on the CPU path, the gloo group.
+    busbw = total bytes x (world - 1) / world / time (the ring's per-link traffic)."""
+    import statistics
+
+    import torch
+    import torch.distributed as tdist
+
+    world = ctx.world
+    per = max(1, int(allgather_mb * 1e6 / 8) // world)
+    out: dict = {"allgather_bytes": per * world * 8, "world": world}
+    if cpu or comm is None:
+        x = torch.zeros(1, dtype=torch.float64)
+        for _ in range(5):
+            tdist.all_reduce(x)
+        lat = []
+        for _ in range(20):
+            t = time.perf_counter()
+            tdist.all_reduce(x)
+            lat.append((time.perf_counter() - t) * 1e6)
+        send = torch.zeros(per, dtype=torch.float64)
+        recv = [torch.empty(per, dtype=torch.float64) for _ in range(world)]
+        tdist.all_gather(recv, send)
+        ts = []
+        for _ in range(3):
+            t = time.perf_counter()
+            tdist.all_gather(recv, send)
+            ts.append(time.perf_counter() - t)
+        out.update(transport="gloo", allreduce_8b_us=statistics.median(lat))
+        t_ag = min(ts)
+    else:
+        s = torch.cuda.current_stream()
+        x = torch.zeros(1, dtype=torch.float64, device="cuda")
+        for _ in range(20):
+            comm.allreduce_sum(x.data_ptr(), x.data_ptr(), 1, s.cuda_stream)
+        lat = []
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            for _ in range(50):
+                comm.allreduce_sum(x.data_ptr(), x.data_ptr(), 1, s.cuda_stream)
+            e1.record(s)
+            e1.synchronize()
+            lat.append(e0.elapsed_time(e1) * 1e3 / 50)
+        send = torch.zeros(per, dtype=torch.float64, device="cuda")
+        recv = torch.empty(per * world, dtype=torch.float64, device="cuda")
+        for _ in range(2):
+            comm.allgather(send.data_ptr(), recv.data_ptr(), per, s.cuda_stream)
+        ts = []
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(s)
+            comm.allgather(send.data_ptr(), recv.data_ptr(), per, s.cuda_stream)
+            e1.record(s)
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1) * 1e-3)
+        out.update(transport=getattr(comm, "kind", "native"),
+                   allreduce_8b_us=statistics.median(lat))
+        t_ag = min(ts)
+        del send, recv
+    # the slowest rank's numbers
+    m = torch.tensor([out["allreduce_8b_us"], t_ag], dtype=torch.float64,
+                     device="cpu" if (cpu or ctx.host_collectives) else "cuda")
+    ctx.all_reduce_max(m)
+    total = per * world * 8
+    out.update(allreduce_8b_us=float(m[0]), allgather_s=float(m[1]),
+               allgather_algbw_gbs=total / float(m[1]) / 1e9,
+               allgather_busbw_gbs=total * (world - 1) / world / float(m[1]) / 1e9)
+    return out
+
+
+def batch_diagnostics(args, ctx, integ, plan, dev, cpu: bool, use_torch: bool,
+                      transport: dict) -> dict:
+    """VERDICT r5 Next #2: one untimed batch after the timed region, taken apart on every
+    rank — compute (the batch's kernels), tail (closing kernel + all-reduce + copy to pinned
+    memory) and the host's part (wall - device) — with the max and min over ranks; then the
+    communicator's 8-byte all-reduce latency and allgather bus bandwidth, and RCCL's channel
+    and protocol lines from rank 0's INIT log. These say where a multi-GPU step's time went
+    (the reference's reduce / barrier / broadcast costs, 4main.c:134-157)."""
+    import torch
+
+    steps = min(args.steps, plan.slots if plan is not None else args.slots)
+    keys = ("compute_us", "close_us", "allreduce_us", "copy_us", "tail_us", "device_us",
+            "wall_us", "marker_us")
+    if cpu:  # as the timed CPU steps run: per step the torch fp64 evaluation of the rank's
+        # slice, then its gloo all-reduce (which also waits for the slowest rank)
+        comp = red = 0.0
+        t_start = time.perf_counter()
+        for _ in range(steps):
+            t0 = time.perf_counter()
+            v = torch.tensor([integ._cpu_local()], dtype=torch.float64)
+            t1 = time.perf_counter()
+            ctx.all_reduce_sum(v)
+            t2 = time.perf_counter()
+            comp, red = comp + (t1 - t0), red + (t2 - t1)
+        wall = time.perf_counter() - t_start
+        d = {"steps": steps, "compute_us": comp * 1e6, "close_us": 0.0,
+             "allreduce_us": red * 1e6, "copy_us": 0.0, "tail_us": red * 1e6,
+             "device_us": (comp + red) * 1e6, "wall_us": wall * 1e6, "marker_us": 0.0,
+             "path": "cpu"}
+    elif use_torch or plan is None:
+        d = {"steps": steps, "path": "torch", **{k: None for k in keys}}
+    else:
+        d = dict(plan.diagnose_batch(steps), path="native",
+                 close_in_launch=bool(plan.close_in_launch),
+                 allreduce_to_host=bool(plan.allreduce_to_host))
+    out: dict = {"steps": d["steps"], "path": d["path"]}
+    for k in keys:
+        if d.get(k) is None:
+            out[k] = None
+            continue
+        out[k] = _spread(ctx.all_gather_scalars(float(d[k]), device=dev))
+    out["host_us"] = (None if d.get("wall_us") is None else
+                      _spread(ctx.all_gather_scalars(float(d["wall_us"] - d["device_us"]),
+                                                     device=dev)))
+    for k in ("close_in_launch", "allreduce_to_host"):
+        if k in d:
+            out[k] = d[k]
+    if not use_torch:
+        out["comm"] = comm_probes(ctx, getattr(integ, "_comm", None), args.diag_allgather_mb,
+                                  cpu)
+    if not cpu:
+        out["rccl_init"] = rccl_init_lines((transport or {}).get("log"))
+    return out
+
+
+def record_verified(headline_ok: bool, extras_ok: bool, transport_error: str | None,
+                    comm_fallback: str | None) -> bool:
+    """The record's `verified`: the headline's check AND every extra's AND the transport check
+    AND the native communicator having carried the run. A native-communicator failure that the
+    run survived on the torch.distributed data plane (comm_fallback) still fails it: the
+    record stands for the native RCCL path, and a fallback there would otherwise turn a
+    native-comm bug into a passing record on another code path (native_comm_verified)."""
+    return bool(headline_ok and extras_ok and not transport_error and comm_fallback is None)
 
 
 def transport_check(world: int, share: bool, transport: dict, rccl: bool = True) -> str | None:
@@ -762,13 +946,20 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
                 "vs_true_frac_within_1ulp": float((t <= 1.0).mean()),
                 "window": [int(windows[-1]), int(w)], "windows": per}
 
-    # per-point bounds against the IEEE path's values: series_exact is exact-grade (within 2,
-    # both sides round), the g-fold of series within 5
-    bound = {"series_exact": 2.0}.get(eff, 5.0)
+    # per-point bounds. series_exact is checked against the TRUE value
+    # (<= 1.5 ulp, as test_pi4_series_exact_per_point_accuracy; measured max 1.42): against
+    # the IEEE path's own values both sides round independently (series_exact up to ~1.42
+    # ulp from the true value, IEEE division up to ~1.57), so the two may sit 3 ulp apart
+    # where neither is wrong — that comparison is reported, bounded by 3. The g-fold of
+    # series rounds every sample at ulp(1/2): within 5 of IEEE.
+    bound = {"series_exact": 3.0}.get(eff, 5.0)
+    true_bound = {"series_exact": 1.5}.get(eff)
     if pi4 and args.dtype == "fp64" and eff != "ieee":
         pp = ulps(eff)
+        good = pp["max_ulp"] <= bound and (true_bound is None or
+                                           pp["vs_true_max_ulp"] <= true_bound)
         out["per_point"] = dict(pp, division=eff, bound_max_ulp=bound,
-                                verified=bool(pp["max_ulp"] <= bound))
+                                bound_vs_true_max_ulp=true_bound, verified=bool(good))
         out["per_point_max_ulp"] = out["per_point"]["max_ulp"]
         out["per_point_frac_within_1ulp"] = out["per_point"]["frac_within_1ulp"]
         out["per_point_vs_true_max_ulp"] = out["per_point"]["vs_true_max_ulp"]
@@ -784,14 +975,15 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
         ms = _timed_steps(ctx, ex.plan, steps, pipeline, dev, args.graph_batches)
         v = ex.plan.host_result(ex.plan.host_index_of(steps - 1, True))
         e = abs(v - math.pi)
-        ab = {"series_exact": 2.0}.get(alt, 5.0)
+        ab = {"series_exact": 3.0}.get(alt, 5.0)
         pp = ulps(alt)
         out[f"{alt}_div"] = {
             "value": n_total / (ms * 1e-3), "ms_per_step": ms, "steps": steps, "result": v,
             "abs_err": e, "division": str(ex.plan.effective_div).split(".")[-1],
             "per_point": dict(pp, bound_max_ulp=ab),
             "verified": bool(result_ok("pi4", args.rule, args.dtype, n_total, e) and
-                             pp["max_ulp"] <= ab)}
+                             pp["max_ulp"] <= ab and
+                             (alt != "series_exact" or pp["vs_true_max_ulp"] <= 1.5))}
         del ex
     # (3) the headline config in its other scaling form. Strong headline (the default: N = 1e9
     #     IN TOTAL, riemann.cpp:10,71-73): the weak form, 1e9 samples PER GPU (N = 1e9 x G,
@@ -826,10 +1018,11 @@ def run_extras(args, ctx, integ, n_total, pipeline, dev) -> dict:
         del st
     # (5) BASELINE config #5: the 2-D field v(x) v(y) from the velocity profile, 4096^2
     #     bilinear midpoint samples, sample rows split over the same GPUs; one integration =
-    #     one multi-step launch per graph replay of p2.graph_steps integrations (128 for the
-    #     whole field, up to 1024 for a small row share: a replay holds >= 2^31 samples), the
-    #     replay's per-integration partials meeting in one RCCL all-reduce (Table2DPlan) on the
-    #     shared communicator
+    #     one multi-step launch per graph replay of p2.graph_steps integrations (the replay
+    #     size rule is table2d_auto_graph_steps: about Table2DPlan::kReplaySamples = 2^33
+    #     samples per replay, 512 integrations for the whole field, up to 1024 for a small
+    #     row share), the replay's per-integration partials meeting in one RCCL all-reduce
+    #     (Table2DPlan) on the shared communicator
     if pi4:
         import torch
 

@@ -66,8 +66,11 @@ enum class Rule : int { kLeft = 0, kMid = 1, kRight = 2 };
 //   kSeriesDirect  the same series with x, d formed explicitly per sample (5 ops; A/B)
 //   kSeriesExact   kSeries's residuals without the g = 1/2 + e fold: each sample's value is
 //                  s (1 + e + e^2) at e's own precision, the seed residual from the exact
-//                  d_m (2.68 VALU per sample; per point max 1.34 ulp / mean 0.27 ulp from the
-//                  true value, where IEEE division per sample is 1.57 / 0.45): the headline
+//                  d_m (2.68 VALU per sample; per point from the true value max 1.34 ulp /
+//                  mean 0.27 ulp on profiles/r5/accuracy_ab.md's windows, max 1.42 on the
+//                  bench record's 1/8-in window, <= 1.5 enforced by
+//                  test_pi4_series_exact_per_point_accuracy and the record's per_point check;
+//                  IEEE division per sample is 1.57 / 0.45): the headline
 //                  division since round 5 (profiles/r5/accuracy_ab.md). For the other
 //                  integrands (and fp32) it selects their series path.
 enum class DivMode : int { kSeries = 0, kIeee = 1, kSeriesDirect = 2, kSeriesExact = 3 };

@@ -74,9 +74,11 @@ __device__ __forceinline__ double slot_wait(const double* p, double first,
 // Thread t sums partials t, t + BLOCK, t + 2 BLOCK, ... in increasing order. The loads of a
 // batch are all issued before the first add (a plain loop waited for every load).
 // SLOTS = true: the partials are write-once slots of this launch (waited for, see above);
-// false: plain loads of partials a previous launch wrote (the kernel boundary orders them).
+// false: plain loads of partials a previous launch wrote (the kernel boundary orders them),
+// or, with SC1, sc1 loads of partials this launch stored write-through before a counted
+// arrival the caller has already seen complete (close_batch_in_launch).
 // BLOCK = 0: the launch's own block size (blockDim.x), for kernels launched at several sizes.
-template <int BLOCK, bool SLOTS>
+template <int BLOCK, bool SLOTS, bool SC1 = false>
 __device__ __forceinline__ double ordered_partials(const double* partials, int n) {
   const int bs = BLOCK > 0 ? BLOCK : static_cast<int>(blockDim.x);
   double v = 0.0;
@@ -85,7 +87,7 @@ __device__ __forceinline__ double ordered_partials(const double* partials, int n
 #pragma unroll
     for (int k = 0; k < kFinalBatch; ++k) {
       const int i = base + k * bs + static_cast<int>(threadIdx.x);
-      if constexpr (SLOTS)
+      if constexpr (SLOTS || SC1)
         r[k] = i < n ? slot_load(&partials[i]) : 0.0;
       else
         r[k] = i < n ? partials[i] : 0.0;
@@ -135,6 +137,85 @@ __device__ __forceinline__ bool publish_and_ticket(double s, double* partials, u
   }
   __syncthreads();
   return *flag != 0;  // the slots are read as atomics: no acquire fence needed
+}
+
+// In-launch close of a multi-step batch (RiemannConfig::close, "launch"): the persistent
+// launch's own workgroups turn its `steps` rows of `nb` step partials into the step values
+// out[s] = scale * (row s summed exactly as multistep_close_kernel sums it) — no closing
+// kernel, no kernel boundary after the launch.
+//  * Every workgroup's thread 0 stored ALL of its step partials write-through (slot_store,
+//    sc1), then waits for them (s_waitcnt vmcnt(0)) and counts the workgroup in shard
+//    b % S (S = min(kTicketGroups, nb) counters, each on its own 256-byte line: one counter
+//    serialised ~12 ns per arrival, MI355X_MICROARCH.md "fanin").
+//  * The last arrival of shard c becomes closer c: its wave 0 polls every shard (lane l
+//    loads shard l, sc1, s_sleep between polls, bounded) until all nb workgroups have
+//    arrived, then the workgroup barrier releases the closer's other waves, and all of them
+//    read the rows with sc1 loads: the first row of the sc1 hand-off table in
+//    MI355X_MICROARCH.md "Valid forms" (one lane per storing workgroup for all its stores,
+//    agent-scope adds, an sc1 poll of every shard, a barrier before the other waves load).
+//  * Closer c closes steps c, c + S, ...: ordered_partials + block_sum_dyn at the launch's
+//    block size, the closing kernel's arithmetic, so the values are bitwise the same.
+//  * The closer whose count on the done line (after the shards) is last re-arms every
+//    counter to zero for the next launch; no other workgroup reads them after its poll.
+// Spinning is safe where the close kernel was not needed: only the last arrival of each
+// shard waits, for workgroups already past their last step (at most S closers hold slots
+// while every other workgroup has exited). A poll that hits kSlotSpinLimit writes NaN
+// results instead of hanging the GPU.
+// `ticket` holds kTicketWords words, zero before the first launch.
+__device__ __forceinline__ void close_batch_in_launch(const double* partials, unsigned nb,
+                                                      int steps, unsigned* ticket, double scale,
+                                                      double* out, double* red, int* role) {
+  const unsigned S = nb < static_cast<unsigned>(kTicketGroups) ? nb : kTicketGroups;
+  if (threadIdx.x == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this workgroup's sc1 partials landed
+    const unsigned g = blockIdx.x % S;
+    const unsigned members = (nb - g + S - 1) / S;
+    const unsigned prev = __hip_atomic_fetch_add(ticket + g * kTicketStride, 1u,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *role = prev == members - 1 ? static_cast<int>(g) : -1;
+  }
+  __syncthreads();
+  const int c = *role;
+  if (c < 0) return;
+  __shared__ int timed_out;
+  if (threadIdx.x < kWave) {
+    const unsigned lane = threadIdx.x;
+    const unsigned want = lane < S ? (nb - lane + S - 1) / S : 0u;
+    int late = 0;
+    for (unsigned spins = 0;; ++spins) {
+      const unsigned got =
+          lane < S ? __hip_atomic_load(ticket + lane * kTicketStride, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT)
+                   : 0u;
+      if (__all(got >= want)) break;
+      if (spins > kSlotSpinLimit) {
+        late = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (lane == 0) timed_out = late;
+  }
+  __syncthreads();
+  const bool bad = timed_out != 0;
+  for (int s = c; s < steps; s += static_cast<int>(S)) {
+    const double t = ordered_partials<0, false, true>(partials + static_cast<size_t>(s) * nb,
+                                                      static_cast<int>(nb));
+    const double tot = block_sum_dyn(t, red);
+    if (threadIdx.x == 0) out[s] = bad ? __builtin_nan("") : tot * scale;
+    __syncthreads();  // red is reused by the next step
+  }
+  if (threadIdx.x == 0) {
+    const unsigned d = __hip_atomic_fetch_add(ticket + kTicketGroups * kTicketStride, 1u,
+                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == S - 1) {  // every closer is past its poll: re-arm for the next launch
+      for (unsigned g = 0; g < S; ++g)
+        __hip_atomic_store(ticket + g * kTicketStride, 0u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ticket + kTicketGroups * kTicketStride, 0u, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 // Re-arm the ticket (last workgroup only: every group has arrived, nobody else touches it).

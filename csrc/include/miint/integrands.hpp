@@ -313,7 +313,10 @@ struct Pi4 : TileDefaults<Pi4> {
           const double en = fma(-pk[j], a, c);  // sample kSub/2 - 1 - j's
           t = fma(ep, ep, t);
           t = fma(en, en, t);
-          asm volatile("" : "+v"(t));  // program order, as kSeries
+          // program order, as kSeries. (One chain even at 1 wave per SIMD: two running sums,
+          // e+ and e- apart, ran 4-5 % slower at G = 1 and at the 1/4 and 1/8 shares,
+          // profiles/r6/batch_tail.md.)
+          asm volatile("" : "+v"(t));
         }
       }
       // U samples of s (1 + e + e^2): s U + s (sum e + sum e^2)
@@ -324,7 +327,11 @@ struct Pi4 : TileDefaults<Pi4> {
   }
 
   // kSeriesExact value of sample u of a full tile (validation kernel): s + s (e + e^2), one
-  // rounding — what the tile adds for the sample (s U + s sum f: no 1 + f is ever formed).
+  // rounding, from the same seed, centre and residual e as the tile. The tile itself does
+  // not form this per-sample value: it adds the residuals' linear terms once per tile
+  // (s U + s (U e_m + B sum k^2 + sum e^2)), so the two differ by roundings only; over one
+  // full tile they agree to a few ulp of the tile sum
+  // (test_pi4_series_exact_point_kernel_sums_to_the_tile).
   __device__ __forceinline__ double series_exact_point(double xm, double h, int u) const {
     const Seed sd = seed_exact(xm, h);
     const double b2 = 2.0 * sd.b;

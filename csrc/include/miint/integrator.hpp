@@ -46,6 +46,14 @@ namespace miint {
 constexpr int kAutoStepStreams = 4;
 constexpr uint64_t kStepStreamsMaxCount = 600000000ull;
 
+// RiemannConfig::close = "auto": multi-step batches of at most this many workgroups (at the
+// default 256-thread block) are closed inside the persistent launch, larger ones by the
+// closing kernel. (See auto_close_in_launch.)
+constexpr int kAutoCloseLaunchMaxGrid = 0;
+inline bool auto_close_in_launch(int grid, int block) {
+  return block == kRiemannBlock && grid <= kAutoCloseLaunchMaxGrid;
+}
+
 struct RiemannConfig {
   Integrand integrand = Integrand::kPi4;
   double a = 0.0, b = 1.0;
@@ -80,6 +88,17 @@ struct RiemannConfig {
                                 // the multi-step kernel's residency (auto grid), so every path
                                 // of the plan sums the same partials: values bit for bit equal.
                                 // An explicit grid above residency turns it off.
+  // How a multi-step batch is closed (its step partials summed into step values):
+  //   "kernel": a closing kernel of one workgroup per step after the persistent launch;
+  //   "launch": inside the persistent launch (handoff.hpp close_batch_in_launch): the last
+  //             arrivals close it, no second kernel and no kernel boundary;
+  //   "auto":   kAutoCloseLaunch below.
+  // Both give the same values bit for bit.
+  std::string close = "auto";
+  // Bucketed batches all-reduce their step values straight into the pinned host slots
+  // (RCCL's receive buffer is the mapped host memory) instead of in place on the device
+  // followed by a copy to pinned memory: one stream operation and one kernel boundary fewer.
+  bool allreduce_to_host = true;
   int step_streams = 0;         // chained graph batches: steps dealt round-robin to this many
                                 // streams (each its own chain, ramp and tail of one step
                                 // overlapping the next one's work); 0 = auto (kAutoStepStreams
@@ -120,6 +139,28 @@ struct OneShotTiming {
   double median_us = 0.0, min_us = 0.0, max_us = 0.0;  // host: launch call -> result on host
   double device_median_us = 0.0, device_min_us = 0.0;  // hipEvent span of the same calls
   double value = 0.0;
+};
+
+// One batch of a plan taken apart by hipEvents between its stream stages (RiemannPlan::
+// diagnose_batch; bench.py's untimed diagnostic batch on several GPUs). Microseconds.
+// An event between two stages is a queue packet of its own whose release costs the device
+// ~2 us (gfx950, ROCm 7.2: profiles/r6/batch_tail.md), so the batch runs twice: once between
+// two events only (device_us, wall_us: the batch as the timed region runs it), once with an
+// event after every stage (staged_us); marker_us = (staged_us - device_us) / 3 is the price
+// of one event, and every stage below has it subtracted once.
+struct BatchDiag {
+  int steps = 0;
+  double compute_us = 0.0;    // the batch's kernels up to the step values' partials (a multi-
+                              // step launch with its in-launch close, or a chain)
+  double close_us = 0.0;      // the closing kernel (~0: closed in the launch / by the chain)
+  double allreduce_us = 0.0;  // the bucketed all-reduce (~0 without a collective)
+  double copy_us = 0.0;       // the copy to pinned memory (~0: the all-reduce or the kernel
+                              // stored there)
+  double marker_us = 0.0;     // one event's own cost (see above)
+  double device_us = 0.0;     // the batch between two events
+  double staged_us = 0.0;     // the same batch with the stage events
+  double wall_us = 0.0;       // host: launch call to every stage drained (the plan's sync)
+  double tail_us() const { return device_us - compute_us; }  // close + all-reduce + copy
 };
 
 class RiemannPlan {
@@ -179,6 +220,11 @@ class RiemannPlan {
   // bucketed(): batches of `slots` steps, one all-reduce each, host slot k % slots.
   // With a collective, every rank's clock starts after a collective barrier (barrier()).
   StepTiming run_steps(int steps, bool pipeline, bool graphs);
+  // One batch of `nsteps` (<= slots) steps enqueued directly with hipEvents between its
+  // stages (BatchDiag); the same operations and values as a timed batch, which it must not
+  // be part of: the events are queue packets of their own. Collective over ranks (a barrier
+  // first, and the batch's all-reduce). Results land in host slots 0 .. nsteps-1.
+  BatchDiag diagnose_batch(int nsteps);
   // Collective: returns once every rank of the plan's communicator has entered (a 1-double
   // all-reduce, drained under the watchdog). No-op without a collective.
   void barrier();
@@ -206,9 +252,14 @@ class RiemannPlan {
   bool chained() const { return cfg_.fused && cfg_.chain && (!collective() || bucketed()); }
   // Chained batches run as one multi-step launch (RiemannConfig::multistep, in effect).
   bool multistep() const { return chained() && multistep_; }
+  // Multi-step batches are closed inside the persistent launch (RiemannConfig::close).
+  bool close_in_launch() const { return multistep() && close_launch_; }
+  // Bucketed batches all-reduce into pinned host memory (RiemannConfig::allreduce_to_host).
+  bool allreduce_to_host() const { return bucketed() && cfg_.allreduce_to_host; }
 
  private:
   void enqueue_batch(hipStream_t cs, hipStream_t rs, int nsteps, bool overlap);
+  void enqueue_bucket_reduce(hipStream_t s, int nsteps) const;
   void enqueue_chain(hipStream_t s, int nsteps) const;
   void enqueue_chain_streams(hipStream_t cs, int nsteps);
  public:
@@ -231,6 +282,8 @@ class RiemannPlan {
   DeviceBuffer<double> slots_;     // grid write-once slots of the fused (ticket) kernel
   DeviceBuffer<double> ms_partials_;  // multistep: slots x grid partials
   bool multistep_ = false;
+  bool close_launch_ = false;         // multistep batches closed in-launch
+  DeviceBuffer<unsigned int> ms_ticket_;  // its arrival counters (close_batch_in_launch)
   DeviceBuffer<double> result_;
   DeviceBuffer<double> sync_;      // barrier(): the 1-double all-reduce's operand
   DeviceBuffer<unsigned int> ticket_;

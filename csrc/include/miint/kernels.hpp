@@ -131,14 +131,23 @@ void launch_riemann_chained(const RiemannParams& p, DType dtype, DivMode div, La
 // chained / two-kernel value at the same grid. `partials` holds steps x grid doubles. The
 // grid should be resident as a whole: at most riemann_multistep_grid(...) workgroups (0 for
 // the instantiations that keep chained batches).
+// ticket != nullptr (kTicketWords words, zero before the first launch; re-armed by the
+// kernel): no closing kernel — the launch's last arrivals close the batch themselves
+// (handoff.hpp close_batch_in_launch), bitwise the same values; its residency is
+// riemann_multistep_grid(..., close = true).
 // 1 <= steps <= kMaxMultiSteps.
 constexpr int kMaxMultiSteps = 64;
 int riemann_multistep_grid(const RiemannParams& p, DType dtype, DivMode div, int block,
-                           int num_cus);
+                           int num_cus, bool close = false);
 void launch_riemann_multistep(const RiemannParams& p, DType dtype, DivMode div,
                               LaunchShape shape, const double* table, int table_n,
                               double* partials, int steps, double scale, double* out,
-                              hipStream_t stream);
+                              hipStream_t stream, unsigned int* ticket = nullptr,
+                              bool close_kernel = true);
+// The closing kernel of a multi-step launch on its own (launch_riemann_multistep with
+// close_kernel = false, e.g. to time the two apart): out[s] = scale * step s's sum.
+void launch_multistep_close(const double* partials, int grid, int steps, double scale,
+                            double* out, int block, hipStream_t stream);
 
 // Debug/validation: write every sample's f value (as the hot tile path computes it) to
 // `out[0..p.n)`; fp64 only. Used by the per-point accuracy tests of the series division.

@@ -28,8 +28,10 @@ namespace miint {
 struct Table2DConfig {
   int grid = 4096;       // samples per axis
   double extent = 1800;  // [0, extent]^2
-  // Without a communicator: integrate only row slice `rank` of `world` (the share one GPU
-  // of a `world`-GPU run computes; the result is that partial). Ignored with a communicator.
+  // Without a communicator, or with a 1-rank one (force_collective): integrate only row
+  // slice `rank` of `world` (the share one GPU of a `world`-GPU run computes; run() and
+  // last_result() then return that slice's partial — a 1-rank all-reduce adds nothing).
+  // Ignored with a communicator of more than one rank (its rank and world rule).
   int world = 1, rank = 0;
   // Graph timing with a communicator: the graph_steps integrations of one replay each write
   // their own partial, and ONE all-reduce of graph_steps doubles (plus one copy) ends the

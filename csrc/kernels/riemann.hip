@@ -683,10 +683,11 @@ __global__ __launch_bounds__(kMaxBlock) kFullOccupancy void riemann_chained_kern
 // Each step re-derives its sample coordinates from p.a laundered through an empty asm, so
 // nothing of a step is loop-invariant: no step's work can be hoisted out of the loop or shared
 // with another, K steps are K full integrations.
-template <DivMode M, class F>
+template <DivMode M, class F, bool CLOSE>
 __device__ __forceinline__ void multistep_body(const RiemannParams& p, const double* table,
                                                int table_n, double* partials, int steps,
-                                               unsigned rot) {
+                                               unsigned rot, unsigned* ticket, double scale,
+                                               double* out) {
   using Acc = typename AccOf<F>::type;
   // The block sum's LDS slots alternate between steps: step s + 2 writes red[s & 1] only
   // after every wave passed step s + 1's block-sum barrier, which wave 0 reaches after its
@@ -705,22 +706,31 @@ __device__ __forceinline__ void multistep_body(const RiemannParams& p, const dou
     double v;
     if constexpr (__is_same(Acc, double)) v = block_sum_dyn(lane_sum<M>(q, f, vb, sp), red[s & 1]);
     else v = static_cast<double>(block_sum_dyn(lane_sum<M>(q, f, vb, sp), red_acc[s & 1]));
-    if (threadIdx.x == 0) partials[static_cast<size_t>(s) * nb + vb] = v;
+    if (threadIdx.x == 0) {
+      // in-launch close: write-through, read by other workgroups' closers in this launch
+      if constexpr (CLOSE) slot_store(&partials[static_cast<size_t>(s) * nb + vb], v);
+      else partials[static_cast<size_t>(s) * nb + vb] = v;
+    }
     vb += rot;
     if (vb >= nb) vb -= nb;
   }
+  if constexpr (CLOSE) {
+    __shared__ int role;
+    __syncthreads();  // red[] is the close's block-sum scratch: every wave past its last read
+    close_batch_in_launch(partials, nb, steps, ticket, scale, out, red[0], &role);
+  }
 }
-template <DivMode M, class F>
+template <DivMode M, class F, bool CLOSE>
 __global__ __launch_bounds__(kMaxBlock) void riemann_multistep_kernel(
     RiemannParams p, const double* table, int table_n, double* partials, int steps,
-    unsigned rot) {
-  multistep_body<M, F>(p, table, table_n, partials, steps, rot);
+    unsigned rot, unsigned* ticket, double scale, double* out) {
+  multistep_body<M, F, CLOSE>(p, table, table_n, partials, steps, rot, ticket, scale, out);
 }
-template <DivMode M, class F>
+template <DivMode M, class F, bool CLOSE>
 __global__ __launch_bounds__(kMaxBlock) kFullOccupancy void riemann_multistep_kernel_o8(
     RiemannParams p, const double* table, int table_n, double* partials, int steps,
-    unsigned rot) {
-  multistep_body<M, F>(p, table, table_n, partials, steps, rot);
+    unsigned rot, unsigned* ticket, double scale, double* out) {
+  multistep_body<M, F, CLOSE>(p, table, table_n, partials, steps, rot, ticket, scale, out);
 }
 // The step loop's state lifts every multi-step kernel to 106 SGPRs: 7 waves per SIMD. Those
 // with few VGPRs take the 8-wave hint instead (the extra SGPRs go to VGPR lanes, outside the
@@ -844,31 +854,55 @@ void launch_chained_t(const RiemannParams& p, LaunchShape shape, const double* t
                                                                prev, nprev, scale, out_prev);
 }
 
+template <DivMode M, class F, bool CLOSE>
+void launch_multistep_c(const RiemannParams& p, LaunchShape shape, const double* table,
+                        int table_n, double* partials, int steps, unsigned rot,
+                        unsigned* ticket, double scale, double* out, hipStream_t stream) {
+  if constexpr (multistep_o8<M, F>())
+    riemann_multistep_kernel_o8<M, F, CLOSE><<<shape.grid, shape.block, 0, stream>>>(
+        p, table, table_n, partials, steps, rot, ticket, scale, out);
+  else
+    riemann_multistep_kernel<M, F, CLOSE><<<shape.grid, shape.block, 0, stream>>>(
+        p, table, table_n, partials, steps, rot, ticket, scale, out);
+}
+// ticket != nullptr: the in-launch close (close_batch_in_launch) stores the step values;
+// otherwise the caller closes the batch with multistep_close_kernel.
 template <DivMode M, class F>
 void launch_multistep_t(const RiemannParams& p, LaunchShape shape, const double* table,
                         int table_n, double* partials, int steps, unsigned rot,
-                        hipStream_t stream) {
-  if constexpr (multistep_o8<M, F>())
-    riemann_multistep_kernel_o8<M, F><<<shape.grid, shape.block, 0, stream>>>(
-        p, table, table_n, partials, steps, rot);
-  else
-    riemann_multistep_kernel<M, F><<<shape.grid, shape.block, 0, stream>>>(
-        p, table, table_n, partials, steps, rot);
+                        unsigned* ticket, double scale, double* out, hipStream_t stream) {
+  if constexpr (multistep_pays<M, F>()) {
+    if (ticket)
+      launch_multistep_c<M, F, true>(p, shape, table, table_n, partials, steps, rot, ticket,
+                                     scale, out, stream);
+    else
+      launch_multistep_c<M, F, false>(p, shape, table, table_n, partials, steps, rot, ticket,
+                                      scale, out, stream);
+  } else {
+    fail("this integrand/division keeps chained batches (no multi-step kernel)", __FILE__,
+         __LINE__);
+  }
 }
-// Workgroups of the multi-step kernel resident at once on one CU at this block size.
-// (0 for instantiations whose batches run chained: multistep_pays)
-template <DivMode M, class F>
-void multistep_per_cu_t(int block, int* out) {
+// Workgroups of the multi-step kernel (with or without the in-launch close) resident at once
+// on one CU at this block size. (0 for instantiations whose batches run chained:
+// multistep_pays)
+template <DivMode M, class F, bool CLOSE>
+int multistep_occupancy(int block) {
   int n = 0;
-  if constexpr (!multistep_pays<M, F>())
-    n = 0;
-  else if constexpr (multistep_o8<M, F>())
+  if constexpr (multistep_o8<M, F>())
     MIINT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &n, reinterpret_cast<const void*>(&riemann_multistep_kernel_o8<M, F>), block, 0));
+        &n, reinterpret_cast<const void*>(&riemann_multistep_kernel_o8<M, F, CLOSE>), block, 0));
   else
     MIINT_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &n, reinterpret_cast<const void*>(&riemann_multistep_kernel<M, F>), block, 0));
-  *out = n;
+        &n, reinterpret_cast<const void*>(&riemann_multistep_kernel<M, F, CLOSE>), block, 0));
+  return n;
+}
+template <DivMode M, class F>
+void multistep_per_cu_t(int block, bool close, int* out) {
+  if constexpr (!multistep_pays<M, F>())
+    *out = 0;
+  else
+    *out = close ? multistep_occupancy<M, F, true>(block) : multistep_occupancy<M, F, false>(block);
 }
 
 // kIeee Pi4 launches take Pi4::recip_narrow when both end coordinates (the extremes: x is
@@ -978,7 +1012,7 @@ template <DivMode M, class F> struct MultiStepOp {
   template <class... A> static void run(A... a) { launch_multistep_t<M, F>(a...); }
 };
 template <DivMode M, class F> struct MultiStepOccOp {
-  static void run(int block, int* out) { multistep_per_cu_t<M, F>(block, out); }
+  static void run(int block, bool close, int* out) { multistep_per_cu_t<M, F>(block, close, out); }
 };
 template <DivMode M, class F> struct TileLenOp {
   static void run(int* out) { *out = F::template tile_len<M>(); }
@@ -1118,17 +1152,17 @@ void launch_riemann_chained(const RiemannParams& p, DType dtype, DivMode div, La
 }
 
 int riemann_multistep_grid(const RiemannParams& p, DType dtype, DivMode div, int block,
-                          int num_cus) {
+                          int num_cus, bool close) {
   MIINT_CHECK(riemann_block_ok(block), "unsupported Riemann block size");
   int per_cu = 0;
-  dispatch<MultiStepOccOp>(p, dtype, effective_div(p, div, dtype), block, &per_cu);
+  dispatch<MultiStepOccOp>(p, dtype, effective_div(p, div, dtype), block, close, &per_cu);
   return per_cu * num_cus;  // 0: this instantiation runs chained batches
 }
 
 void launch_riemann_multistep(const RiemannParams& p, DType dtype, DivMode div,
                               LaunchShape shape, const double* table, int table_n,
                               double* partials, int steps, double scale, double* out,
-                              hipStream_t stream) {
+                              hipStream_t stream, unsigned int* ticket, bool close_kernel) {
   check_shape(shape);
   check_params(p, table, table_n);
   MIINT_CHECK(steps >= 1 && steps <= kMaxMultiSteps, "multi-step launch: 1..64 steps");
@@ -1143,9 +1177,17 @@ void launch_riemann_multistep(const RiemannParams& p, DType dtype, DivMode div,
   const unsigned heavy = static_cast<unsigned>((extra + shape.block - 1) / shape.block);
   const unsigned rot = heavy % static_cast<unsigned>(shape.grid);
   dispatch<MultiStepOp>(p, dtype, eff, prepared(p, eff), shape, table, table_n, partials, steps,
-                        rot, stream);
+                        rot, ticket, scale, out, stream);
   MIINT_HIP(hipGetLastError());
-  multistep_close_kernel<<<steps, shape.block, 0, stream>>>(partials, shape.grid, scale, out);
+  if (ticket || !close_kernel) return;  // closed inside the launch, or by the caller
+  launch_multistep_close(partials, shape.grid, steps, scale, out, shape.block, stream);
+}
+
+void launch_multistep_close(const double* partials, int grid, int steps, double scale,
+                            double* out, int block, hipStream_t stream) {
+  MIINT_CHECK(steps >= 1 && steps <= kMaxMultiSteps && grid >= 1 && riemann_block_ok(block),
+              "multi-step close: 1..64 steps, a Riemann block size");
+  multistep_close_kernel<<<steps, block, 0, stream>>>(partials, grid, scale, out);
   MIINT_HIP(hipGetLastError());
 }
 

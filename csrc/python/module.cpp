@@ -254,6 +254,8 @@ PYBIND11_MODULE(_miint, m) {
       .def_readwrite("slice_world", &RiemannConfig::slice_world)
       .def_readwrite("timeout_s", &RiemannConfig::timeout_s)
       .def_readwrite("host_direct", &RiemannConfig::host_direct)
+      .def_readwrite("close", &RiemannConfig::close)
+      .def_readwrite("allreduce_to_host", &RiemannConfig::allreduce_to_host)
       .def_readwrite("chain", &RiemannConfig::chain);
 
   py::class_<RiemannPlan>(m, "RiemannPlan")
@@ -311,12 +313,33 @@ PYBIND11_MODULE(_miint, m) {
              r["value"] = t.value;
              return r;
            }, py::arg("reps"), py::arg("mode") = "direct", py::arg("warmup") = 400)
+      .def("diagnose_batch", [](RiemannPlan& p, int steps) {
+             BatchDiag d;
+             {
+               py::gil_scoped_release nogil;
+               d = p.diagnose_batch(steps);
+             }
+             py::dict r;
+             r["steps"] = d.steps;
+             r["compute_us"] = d.compute_us;
+             r["close_us"] = d.close_us;
+             r["allreduce_us"] = d.allreduce_us;
+             r["copy_us"] = d.copy_us;
+             r["tail_us"] = d.tail_us();
+             r["marker_us"] = d.marker_us;
+             r["device_us"] = d.device_us;
+             r["staged_us"] = d.staged_us;
+             r["wall_us"] = d.wall_us;
+             return r;
+           }, py::arg("steps"))
       .def("host_result", &RiemannPlan::host_result)
       .def_property_readonly("host_capacity", &RiemannPlan::host_capacity)
       .def_property_readonly("slots", &RiemannPlan::slots)
       .def_property_readonly("bucketed", &RiemannPlan::bucketed)
       .def_property_readonly("chained", &RiemannPlan::chained)
       .def_property_readonly("multistep", &RiemannPlan::multistep)
+      .def_property_readonly("close_in_launch", &RiemannPlan::close_in_launch)
+      .def_property_readonly("allreduce_to_host", &RiemannPlan::allreduce_to_host)
       .def_property_readonly("direct", &RiemannPlan::direct)
       .def_property_readonly("graph_nodes", &RiemannPlan::graph_nodes)
       .def_property_readonly("graphs_ready", &RiemannPlan::graphs_ready)

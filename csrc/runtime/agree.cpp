@@ -208,8 +208,10 @@ void capture_rccl_log() {
   }
   const char* sub = std::getenv("NCCL_DEBUG_SUBSYS");
   if (!sub || !*sub) {
-    // the peer-connection lines ("... via P2P/IPC") are INIT|P2P / INIT|NET messages
-    ::setenv("NCCL_DEBUG_SUBSYS", "INIT,P2P", 1);
+    // the peer-connection lines ("... via P2P/IPC") are INIT|P2P / INIT|NET messages; GRAPH
+    // adds the topology search's channel lines ("Pattern .., nChannels ..", "Ring 00 : ..",
+    // bench.py's diagnostic record) — all printed once per communicator, never per call
+    ::setenv("NCCL_DEBUG_SUBSYS", "INIT,P2P,GRAPH", 1);
   } else if (sub[0] != '^' && !std::strstr(sub, "INIT") && !std::strstr(sub, "ALL")) {
     ::setenv("NCCL_DEBUG_SUBSYS", (std::string(sub) + ",INIT").c_str(), 1);
   }

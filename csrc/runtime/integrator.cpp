@@ -86,11 +86,24 @@ RiemannPlan::RiemannPlan(const RiemannConfig& cfg, int device, const Comm* comm)
   // every path of such a plan (run(), direct steps, graphs), so all of them sum the same
   // partials, bit for bit. A plan whose batches can never run chained (unfused, or a
   // collective without bucketing) keeps the full grid and allocates no multi-step partials.
+  MIINT_CHECK(cfg.close == "auto" || cfg.close == "kernel" || cfg.close == "launch",
+              "close must be auto, kernel or launch (got " + cfg.close + ")");
   if (cfg.multistep && chained()) {
+    // the in-launch close (kAutoCloseLaunch decides "auto" from the grid the plan would
+    // run): its own instantiation, so its own residency
+    const int res_kernel =
+        riemann_multistep_grid(params_, cfg.dtype, cfg.div, cfg.block, info.num_cus, false);
+    int g = shape_.grid;
+    if (res_kernel > 0 && cfg.grid <= 0 && g > res_kernel) g = res_kernel;
+    close_launch_ = cfg.close == "launch" ||
+                    (cfg.close == "auto" && auto_close_in_launch(g, cfg.block));
     const int resident =
-        riemann_multistep_grid(params_, cfg.dtype, cfg.div, cfg.block, info.num_cus);
+        close_launch_
+            ? riemann_multistep_grid(params_, cfg.dtype, cfg.div, cfg.block, info.num_cus, true)
+            : res_kernel;
     if (resident > 0 && cfg.grid <= 0 && shape_.grid > resident) shape_.grid = resident;
     multistep_ = resident > 0 && shape_.grid <= resident;
+    if (!multistep_) close_launch_ = false;
   }
 
   // chained batches: two partial halves per step stream
@@ -105,6 +118,10 @@ RiemannPlan::RiemannPlan(const RiemannConfig& cfg, int device, const Comm* comm)
   fill_unset_slots(slots_.get(), slots_.size(), nullptr);
   if (multistep_)
     ms_partials_ = DeviceBuffer<double>(static_cast<size_t>(cfg.slots) * shape_.grid);
+  if (close_launch_) {
+    ms_ticket_ = DeviceBuffer<unsigned int>(kTicketWords);
+    MIINT_HIP(hipMemset(ms_ticket_.get(), 0, ms_ticket_.bytes()));
+  }
   result_ = DeviceBuffer<double>(static_cast<size_t>(cfg.slots));
   sync_ = DeviceBuffer<double>(1);
   MIINT_HIP(hipMemset(sync_.get(), 0, sync_.bytes()));
@@ -241,6 +258,21 @@ void RiemannPlan::enqueue_chain_streams(hipStream_t cs, int nsteps) {
   }
 }
 
+// A bucketed batch's step values (device slots 0 .. nsteps-1) -> every rank's global sums in
+// pinned host slots 0 .. nsteps-1: the all-reduce writes them there itself
+// (allreduce_to_host: RCCL's receive buffer is the mapped pinned memory), or it reduces in
+// place and one copy follows.
+void RiemannPlan::enqueue_bucket_reduce(hipStream_t s, int nsteps) const {
+  const size_t n = static_cast<size_t>(nsteps);
+  if (allreduce_to_host()) {
+    comm_->allreduce_sum(result_.get(), host_.device_ptr(), n, s);
+    return;
+  }
+  comm_->allreduce_sum(result_.get(), result_.get(), n, s);
+  MIINT_HIP(hipMemcpyAsync(host_.get(), result_.get(), sizeof(double) * n,
+                           hipMemcpyDeviceToHost, s));
+}
+
 void RiemannPlan::enqueue_batch(hipStream_t cs, hipStream_t rs, int nsteps, bool overlap) {
   if (chained()) {
     if (nsteps == 1)
@@ -253,23 +285,24 @@ void RiemannPlan::enqueue_batch(hipStream_t cs, hipStream_t rs, int nsteps, bool
     else if (multistep_)
       launch_riemann_multistep(params_, cfg_.dtype, cfg_.div, shape_, table_.get(),
                                static_cast<int>(cfg_.table.size()), ms_partials_.get(), nsteps,
-                               scale_, result_ptr(0), cs);
+                               scale_, result_ptr(0), cs,
+                               close_launch_ ? ms_ticket_.get() : nullptr);
     else
       enqueue_chain_streams(cs, nsteps);
-    if (bucketed())  // one all-reduce + one copy of all the batch's results
-      comm_->allreduce_sum(result_.get(), result_.get(), static_cast<size_t>(nsteps), cs);
-    // results in device slots (a bucketed batch, or a single-GPU plan built with
-    // host_direct = false): one copy of the batch's results into pinned memory
+    if (bucketed()) {  // one all-reduce of all the batch's results
+      enqueue_bucket_reduce(cs, nsteps);
+      return;
+    }
+    // results in device slots (a single-GPU plan built with host_direct = false): one copy
+    // of the batch's results into pinned memory
     if (!direct_)
       MIINT_HIP(hipMemcpyAsync(host_.get(), result_.get(), sizeof(double) * nsteps,
                                hipMemcpyDeviceToHost, cs));
     return;
   }
-  if (bucketed()) {  // nsteps kernels, then one all-reduce + one copy of all their results
+  if (bucketed()) {  // nsteps kernels, then one all-reduce of all their results
     for (int j = 0; j < nsteps; ++j) enqueue_compute(cs, j, j);
-    comm_->allreduce_sum(result_.get(), result_.get(), static_cast<size_t>(nsteps), cs);
-    MIINT_HIP(hipMemcpyAsync(host_.get(), result_.get(), sizeof(double) * nsteps,
-                             hipMemcpyDeviceToHost, cs));
+    enqueue_bucket_reduce(cs, nsteps);
     return;
   }
   if (!overlap || direct_ || !collective()) {
@@ -430,6 +463,77 @@ StepTiming RiemannPlan::run_steps(int steps, bool pipeline, bool graphs) {
   t.device_ms = Event::elapsed_ms(ev_t0_, ev_t1_);
   t.steps = steps;
   return t;
+}
+
+BatchDiag RiemannPlan::diagnose_batch(int nsteps) {
+  MIINT_CHECK(nsteps >= 1 && nsteps <= cfg_.slots, "diagnose_batch: 1 <= steps <= slots");
+  DeviceGuard g(device_);
+  TraceRange tr("miint.plan.diagnose_batch");
+  hipStream_t cs = compute_.get();
+  const int tn = static_cast<int>(cfg_.table.size());
+  BatchDiag d;
+  d.steps = nsteps;
+  // pass 1: the batch exactly as launch_steps enqueues it, between two events
+  {
+    Event a0, a1;
+    sync();
+    barrier();
+    const double w0 = wall_seconds();
+    a0.record(cs);
+    enqueue_batch(cs, comm_stream_.get(), nsteps, false);
+    a1.record(cs);
+    sync();
+    d.wall_us = (wall_seconds() - w0) * 1e6;
+    d.device_us = Event::elapsed_ms(a0, a1) * 1e3;
+  }
+  // pass 2: the same operations with an event after every stage
+  Event e0, e1, e2, e3, e4;
+  sync();
+  barrier();
+  e0.record(cs);
+  if (chained() && nsteps > 1 && multistep_) {
+    launch_riemann_multistep(params_, cfg_.dtype, cfg_.div, shape_, table_.get(), tn,
+                             ms_partials_.get(), nsteps, scale_, result_ptr(0), cs,
+                             close_launch_ ? ms_ticket_.get() : nullptr, false);
+    e1.record(cs);
+    if (!close_launch_)
+      launch_multistep_close(ms_partials_.get(), shape_.grid, nsteps, scale_, result_ptr(0),
+                             shape_.block, cs);
+  } else if (chained() && nsteps > 1) {
+    enqueue_chain_streams(cs, nsteps);
+    e1.record(cs);
+  } else {  // fused launches, one per step (a 1-step batch, or an unchained plan)
+    for (int j = 0; j < nsteps; ++j) enqueue_compute(cs, j, j);
+    e1.record(cs);
+  }
+  e2.record(cs);
+  if (bucketed()) {
+    const size_t n = static_cast<size_t>(nsteps);
+    if (allreduce_to_host()) {
+      comm_->allreduce_sum(result_.get(), host_.device_ptr(), n, cs);
+      e3.record(cs);
+    } else {
+      comm_->allreduce_sum(result_.get(), result_.get(), n, cs);
+      e3.record(cs);
+      MIINT_HIP(hipMemcpyAsync(host_.get(), result_.get(), sizeof(double) * n,
+                               hipMemcpyDeviceToHost, cs));
+    }
+  } else {
+    for (int j = 0; j < nsteps; ++j) enqueue_reduce(cs, j);
+    e3.record(cs);
+    for (int j = 0; j < nsteps; ++j) enqueue_copyout(cs, j, j);
+  }
+  e4.record(cs);
+  sync();
+  last_mode_ = 1;
+  d.staged_us = Event::elapsed_ms(e0, e4) * 1e3;
+  const double m = std::max(0.0, (d.staged_us - d.device_us) / 3.0);
+  d.marker_us = m;
+  d.compute_us = Event::elapsed_ms(e0, e1) * 1e3 - m;
+  d.close_us = std::max(0.0, Event::elapsed_ms(e1, e2) * 1e3 - m);
+  d.allreduce_us = std::max(0.0, Event::elapsed_ms(e2, e3) * 1e3 - m);
+  d.copy_us = std::max(0.0, Event::elapsed_ms(e3, e4) * 1e3 - m);
+  return d;
 }
 
 OneShotTiming RiemannPlan::time_one_shot(int reps, const std::string& mode, int warmup) {

@@ -155,7 +155,8 @@ void LoopbackComm::allreduce_sum(const double* send, double* recv, size_t count,
   for (int q = 0; q < W; ++q)
     if (ev && q != r) wait_on(s, *G.done_[q]);  // every rank has read every send buffer
   if (count)
-    MIINT_HIP(hipMemcpyAsync(recv, st, count * sizeof(double), hipMemcpyDeviceToDevice, s));
+    // (hipMemcpyDefault: recv may be mapped pinned host memory, RiemannConfig::allreduce_to_host)
+    MIINT_HIP(hipMemcpyAsync(recv, st, count * sizeof(double), hipMemcpyDefault, s));
 }
 
 void LoopbackComm::reduce_sum(const double* send, double* recv, size_t count, int root,

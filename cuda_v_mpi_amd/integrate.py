@@ -71,7 +71,8 @@ class Integrator:
                  b: float | None = None, force_collective: bool = False, bucket: bool = True,
                  chain: bool = True, comm_obj=None, threads: int = 0,
                  slice_of: tuple[int, int] | None = None, step_streams: int = 0,
-                 block: int = 256, multistep: bool = True, **spec_kw):
+                 block: int = 256, multistep: bool = True, close: str = "auto",
+                 allreduce_to_host: bool = True, **spec_kw):
         spec = integrands.get(integrand, **spec_kw) if isinstance(integrand, str) else integrand
         if a is not None or b is not None:
             spec = dataclasses.replace(spec, a=spec.a if a is None else a,
@@ -115,6 +116,8 @@ class Integrator:
             cfg.chain = chain
             cfg.step_streams = step_streams
             cfg.multistep = multistep  # graph batches as one persistent launch
+            cfg.close = close  # multi-step batches closed by a kernel or inside the launch
+            cfg.allreduce_to_host = allreduce_to_host  # bucketed all-reduce into pinned memory
             if slice_of is not None:  # (rank, world): that rank's share, on this device
                 cfg.slice_rank, cfg.slice_world = int(slice_of[0]), int(slice_of[1])
             self._m = m

@@ -62,3 +62,21 @@ def cuda(native):
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     return torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="session")
+def slice_tol():
+    """Relative tolerance of a G-rank value (rank slices, all-reduced) against the 1-rank one,
+    derived on one GPU from the same G slices summed in every order an all-reduce may use
+    (tools/slice_sum_spread.py -> profiles/r6/slice_sum_spread.json: 4x the largest spread,
+    at least 4 ulp). Bitwise equality is not the contract — the slices move the series tiles'
+    seeds and the partial sums — but a value further out is a real error (a slice lost or
+    counted twice moves it by ~1/G)."""
+    import json
+    import os
+
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        "profiles", "r6", "slice_sum_spread.json")
+    with open(path) as f:
+        table = json.load(f)["tolerance_rel_by_g"]
+    return lambda g: float(table[str(g)])

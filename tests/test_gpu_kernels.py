@@ -778,6 +778,24 @@ def test_fp32_accumulation_policy(cuda, rule):
     assert abs(fold - ref) < abs(acc32 - ref)
 
 
+@pytest.mark.parametrize("i0", [0, 384 * 325_521, 10**9 - 384])
+def test_pi4_series_exact_point_kernel_sums_to_the_tile(native, cuda, i0):
+    """the validation kernel forms each sample's value s (1 + e + e^2) on its own,
+    while the production tile (Pi4::tile_acc) adds the residuals' linear terms once per tile
+    (s U + s (U e_m + B sum k^2 + sum e^2)). Over exactly one full 384-sample tile the two
+    must agree to a few ulp of the tile sum: the per-point figures then describe what the
+    headline kernel sums."""
+    n = 10**9
+    spec = integrands.pi4()
+    pts = kernels.point_values(spec, n, rule="left", div="series_exact", i_begin=i0,
+                               n_local=384)
+    h = 1.0 / n
+    want = math.fsum(pts.cpu().tolist()) * h
+    got = float(kernels.riemann(spec, n, rule="left", div="series_exact", grid=1, i_begin=i0,
+                                n_local=384).item())
+    assert got == pytest.approx(want, rel=4 * 2.0**-52, abs=0), (got, want)
+
+
 @pytest.mark.parametrize("n", [10**9, 96_000_001])
 def test_pi4_series_exact_per_point_accuracy(native, cuda, n):
     """div series_exact (the headline division since round 5: every sample's value

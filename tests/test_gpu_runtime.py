@@ -64,7 +64,7 @@ def test_multistep_batches_equal_chained_bitwise(cuda, name):
     dtype = parts[1] if len(parts) > 1 and parts[1].startswith("fp") else "fp64"
     div = {"ieee": "ieee", "exact": "series_exact"}.get(parts[-1], "series")
     kw = dict(n=120_000_011, rule="mid", dtype=dtype, div=div)
-    ms = Integrator(parts[0], slots=20, **kw)
+    ms = Integrator(parts[0], slots=20, close="kernel", **kw)
     ch = Integrator(parts[0], slots=20, multistep=False, grid=ms.plan.grid, **kw)
     assert ms.plan.multistep and not ch.plan.multistep and ms.plan.grid == ch.plan.grid
     assert ms.plan.step_streams(20) == 1
@@ -78,6 +78,79 @@ def test_multistep_batches_equal_chained_bitwise(cuda, name):
     one = Integrator(parts[0], slots=1, **kw)
     one.run_steps(3, pipeline=True, graphs=True)
     assert one.plan.host_result(one.plan.host_index_of(2, True)) == want[0]
+
+
+@pytest.mark.parametrize("shape", ["g1", "s2", "s4", "s8", "grid5", "grid17_b64",
+                                   "grid100_b1024", "s8_slots64"])
+@pytest.mark.parametrize("graphs", [False, True])
+def test_multistep_close_in_launch_bitwise(cuda, shape, graphs):
+    """close="launch" (the persistent launch's last arrivals close its batch: sc1 partials,
+    sharded arrival counters, closers polling every shard) gives every step the closing
+    kernel's value bit for bit: N = 1e9 and rank 0's 1/2, 1/4 and 1/8 slices, odd grids and
+    64- / 1024-thread workgroups, batches of 20 (and of 64: more steps than shards, so one
+    closer closes several), remainders, repeated launches (the counters re-arm)."""
+    kw = dict(n=10**9, rule="left")
+    name = "pi4"
+    slots, steps = (64, 131) if shape.endswith("slots64") else (20, 47)
+    if shape.startswith("s"):
+        kw["slice_of"] = (0, int(shape[1]))
+    elif shape.startswith("grid"):  # sin's 192-sample tiles: a few tiles per lane
+        g = shape[4:].split("_")[0]
+        name = "sin"
+        kw.update(n=192 * 1000 + 77, grid=int(g), rule="mid",
+                  block=int(shape.split("_b")[1]) if "_b" in shape else 256)
+    a = Integrator(name, slots=slots, close="launch", **kw)
+    b = Integrator(name, slots=slots, close="kernel", grid=a.plan.grid,
+                   **{k: v for k, v in kw.items() if k != "grid"})
+    assert a.plan.multistep and a.plan.close_in_launch and not b.plan.close_in_launch
+    assert a.plan.grid == b.plan.grid
+    for it in (a, b):
+        it.run_steps(steps, pipeline=False, graphs=graphs)
+        it.run_steps(steps, pipeline=False, graphs=graphs)
+    if graphs:
+        assert a.plan.graph_nodes == 1 and b.plan.graph_nodes == 2
+    got = [a.plan.host_result(a.plan.host_index_of(k, graphs)) for k in range(steps)]
+    want = [b.plan.host_result(b.plan.host_index_of(k, graphs)) for k in range(steps)]
+    assert got == want and len(set(got)) == 1 and math.isfinite(got[0])
+
+
+@pytest.mark.parametrize("to_host", [False, True])
+@pytest.mark.parametrize("close", ["kernel", "launch"])
+def test_bucketed_allreduce_to_host_bitwise(cuda, to_host, close):
+    """The 1-rank RCCL stage of bucketed multi-step batches: all-reduced straight into the
+    pinned host slots (allreduce_to_host) or in place + a copy, closed by a kernel or in the
+    launch — the same values as the single-GPU plan, bit for bit."""
+    kw = dict(n=10**9 // 8, rule="left", slots=20)
+    ref = Integrator("pi4", close="kernel", **kw)
+    ref.run_steps(20, pipeline=False, graphs=False)
+    want = ref.plan.host_result(ref.plan.host_index_of(19, False))
+    it = Integrator("pi4", force_collective=True, close=close, allreduce_to_host=to_host, **kw)
+    assert it.plan.bucketed and it.plan.allreduce_to_host == to_host
+    assert it.plan.grid == ref.plan.grid
+    for graphs in (False, True):
+        it.run_steps(43, pipeline=True, graphs=graphs)
+        vals = {it.plan.host_result(it.plan.host_index_of(k, graphs)) for k in range(43 - 3, 43)}
+        assert vals == {want}, (graphs, vals, want)
+
+
+def test_diagnose_batch_accounts_for_the_timed_batch(cuda):
+    """VERDICT r5 Next #2: the diagnostic batch (events between the persistent launch, the
+    close, the all-reduce and the copy) accounts for a timed batch of the same shape —
+    compute + tail within 5 % of the host-timed batch — and gives its values bit for bit."""
+    import statistics
+
+    it = Integrator("pi4", n=10**9, slots=20, force_collective=True, slice_of=(0, 2))
+    for _ in range(40):
+        it.plan.run_steps(20, True, False)
+    walls = [it.plan.run_steps(20, True, False)["wall_s"] * 1e6 for _ in range(9)]
+    want = it.plan.host_result(it.plan.host_index_of(19, False))
+    d = it.plan.diagnose_batch(20)
+    assert d["steps"] == 20 and d["compute_us"] > 0 and d["marker_us"] >= 0
+    assert d["compute_us"] + d["tail_us"] == pytest.approx(d["device_us"], rel=1e-9)
+    assert d["device_us"] == pytest.approx(statistics.median(walls), rel=0.05), (d, walls)
+    assert d["close_us"] > 0 and d["staged_us"] >= d["device_us"]
+    got = {it.plan.host_result(it.plan.host_index_of(k, False)) for k in range(20)}
+    assert got == {want}
 
 
 @pytest.mark.parametrize("block", [64, 256, 1024])
@@ -440,14 +513,16 @@ def test_bench_two_ranks_shared_gpu_torch_comm(native, cuda):
 def test_bench_native_comm_failure_falls_back_to_torch(native, cuda):
     """Two ranks on one GPU with the native communicator: RCCL rejects ranks that share a
     device ("invalid usage") on both ranks, the ranks agree on the failure over the gloo
-    group and run the torch.distributed step path instead; the record names the fallback."""
+    group and run the torch.distributed step path instead; the record names the fallback and
+    is NOT verified (native_comm_verified false), though its headline numbers check out."""
     p = _torchrun(2, [os.path.join(REPO, "bench.py"), "--gpus", "2", "--backend", "gloo",
                       "--comm", "native", "--steps", "12", "--warmup", "2", "--samples", "2e8",
                       "--settle-ms", "0"])
     assert p.returncode == 0, p.stderr[-3000:]
     js = json.loads(p.stdout.strip().splitlines()[-1])
-    assert js["verified"] and js["n_gpus"] == 2 and js["config"]["comm"] == "torch"
+    assert js["headline_verified"] and js["n_gpus"] == 2 and js["config"]["comm"] == "torch"
     assert js["comm_fallback"] and "falling back to --comm torch" in p.stderr
+    assert not js["verified"] and not js["native_comm_verified"]
 
 
 @pytest.mark.parametrize("bucket", [True, False])
@@ -483,10 +558,10 @@ def test_bench_contract(native, cuda):
     assert js["config"]["graphs"] is False
     # the record carries what the headline rests on: IEEE-division speed and per-point ulp
     assert js["ieee_div_value"] > 1e11 and js["ieee_div"]["abs_err"] < 2e-9
-    # the headline division (series_exact): per point within 2 ulp of the IEEE path's own
+    # the headline division (series_exact): per point within 3 ulp of the IEEE path's own
     # values, within 1.5 of the true value; the faster g-fold (series) rides along as an extra
     assert js["config"]["division"] == "series_exact" and js["per_point"]["division"] == "series_exact"
-    assert js["per_point_max_ulp"] <= 2.0 and js["per_point_vs_true_max_ulp"] <= 1.5
+    assert js["per_point_max_ulp"] <= 3.0 and js["per_point_vs_true_max_ulp"] <= 1.5
     assert js["series_div"]["verified"] and js["series_div"]["per_point"]["max_ulp"] <= 5.0
     b3 = js["baseline3_strong_1e10"]
     assert b3["N"] == 10**10 and abs(b3["abs_err"] - 1e-10) < 1e-13 and b3["value"] > 1e11

@@ -133,8 +133,12 @@ def test_table2d_two_ranks_reports_the_chains_it_ran(cuda):
 
 
 def test_bench_two_ranks_native_rccl_one_gpu(cuda):
+    """Two ranks on the one GPU over RCCL's socket transport: the record, the all-reduce into
+    pinned host memory, and the untimed diagnostic batch (compute, tail, per-rank max / min,
+    the communicator's 8-byte all-reduce latency and allgather bandwidth, RCCL's channel
+    lines)."""
     rec = _records([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "10",
-                    "--warmup", "3", "--no-extras"], timeout=240)
+                    "--warmup", "3", "--no-extras", "--diag-allgather-mb", "16"], timeout=240)
     assert len(rec) == 1
     r = rec[0]
     assert r["verified"] and r["n_gpus"] == 2 and r["ranks_share_gpus"]
@@ -145,6 +149,15 @@ def test_bench_two_ranks_native_rccl_one_gpu(cuda):
     assert r["direct_steps_timed"] == 10 and r["config"]["multistep"]
     assert r["config"]["bucketed_allreduce"] and r["config"]["N"] == 10**9
     assert r["config"]["n_per_gpu"] == 5 * 10**8 and r["scaling"] == "strong"
+    assert r["native_comm_verified"] and r["config"]["allreduce_to_host"]
+    d = r["diagnostic_batch"]
+    assert d["path"] == "native" and d["steps"] == 10 and d["allreduce_to_host"]
+    for k in ("compute_us", "tail_us", "allreduce_us", "device_us", "wall_us", "host_us"):
+        assert len(d[k]["per_rank"]) == 2 and d[k]["max"] >= d[k]["min"], k
+    assert d["compute_us"]["min"] > 0 and d["allreduce_us"]["max"] > 0
+    assert d["comm"]["transport"] == "rccl" and d["comm"]["allreduce_8b_us"] > 0
+    assert d["comm"]["allgather_busbw_gbs"] > 0 and d["comm"]["allgather_bytes"] == 16_000_000
+    assert d["rccl_init"]["channels"] and d["rccl_init"]["lines"]
 
 
 def test_bench_driver_launch_form_two_ranks(cuda):

@@ -54,9 +54,10 @@ def _riemann_ranks(world, steps, *, graphs, bucket, pipeline=True, fused=True, s
 @pytest.mark.parametrize("mode", ["bucketed_graph", "bucketed_direct", "perstep_graph",
                                   "perstep_direct_pipelined", "perstep_direct_serial",
                                   "unfused_bucketed_graph"])
-def test_riemann_loopback_matches_single(single_pi4, world, mode):
+def test_riemann_loopback_matches_single(single_pi4, slice_tol, world, mode):
     """37 steps (two full batches of 16 + a remainder batch of 5): every rank of every step
-    holds the global sum, equal to the one-rank integration of the same N to 1e-15."""
+    holds the global sum, equal to the one-rank integration of the same N within the
+    all-reduce-order spread of the W slices (slice_tol, profiles/r6/slice_sum_spread.json)."""
     graphs = "graph" in mode
     out, grp = _riemann_ranks(world, 37, graphs=graphs, bucket="bucketed" in mode,
                               pipeline="serial" not in mode, fused="unfused" not in mode)
@@ -66,7 +67,7 @@ def test_riemann_loopback_matches_single(single_pi4, world, mode):
     for r, o in enumerate(out):
         assert o["graph_error"] == ""
         for v in o["vals"]:
-            assert v == pytest.approx(single_pi4, rel=1e-15, abs=0), (r, mode)
+            assert v == pytest.approx(single_pi4, rel=slice_tol(world), abs=0), (r, mode)
         # every rank holds bitwise the same global values
         assert o["vals"] == out[0]["vals"]
         if graphs:
@@ -277,13 +278,13 @@ def test_cli_trainscan_loopback_parity(native, cuda, world, want):
     assert lines[2] == f"Total distance traveled = {want}"
 
 
-def test_cli_riemann_and_table2d_loopback(native, cuda):
+def test_cli_riemann_and_table2d_loopback(native, cuda, slice_tol):
     one = json.loads(_cli([os.path.join(BIN, "riemann"), "--integrand", "pi4", "--rule", "mid",
                            "--json"])[-1])
     many = json.loads(_cli([os.path.join(BIN, "riemann"), "--integrand", "pi4", "--rule",
                             "mid", "--json", "--loopback", "8", "--iters", "20"])[-1])
     assert many["gpus"] == 8
-    assert many["result"] == pytest.approx(one["result"], rel=1e-15, abs=0)
+    assert many["result"] == pytest.approx(one["result"], rel=slice_tol(8), abs=0)
     t2 = json.loads(_cli([os.path.join(BIN, "miint"), "table2d", "--loopback", "3"])[-1])
     assert t2["rel_err_vs_oracle"] < 1e-14
 

@@ -52,13 +52,16 @@ GUARDED = {
     "poly7_series": ("riemann", CH + r"0ENS_4PolyILi7EEE", 64),
     # the multi-step kernels (graph batches by default): the hot loop found is the step loop
     # around a tile, so no per-sample figure; max_block_valu is one tile's straight line
-    "ms_pi4_series": ("riemann", MS + r"0ENS_3Pi4EE", 0),
-    "ms_pi4_series_exact": ("riemann", MS + r"3ENS_3Pi4EE", 0),
-    "ms_pi4f32_series": ("riemann", MS + r"0ENS0_6Pi4F32EE", 0),
-    "ms_sin_series": ("riemann", MS + r"0ENS_3SinEE", 0),
-    "ms_sin_ieee": ("riemann", MS + r"1ENS_3SinEE", 0),
-    "ms_train_series": ("riemann", MS + r"0ENS_8TrainVelEE", 0),
-    "ms_poly7_series": ("riemann", MS + r"0ENS_4PolyILi7EEE", 0),
+    "ms_pi4_series": ("riemann", MS + r"0ENS_3Pi4ELb0EE", 0),
+    "ms_pi4_series_exact": ("riemann", MS + r"3ENS_3Pi4ELb0EE", 0),
+    "ms_pi4f32_series": ("riemann", MS + r"0ENS0_6Pi4F32ELb0EE", 0),
+    "ms_sin_series": ("riemann", MS + r"0ENS_3SinELb0EE", 0),
+    "ms_sin_ieee": ("riemann", MS + r"1ENS_3SinELb0EE", 0),
+    "ms_train_series": ("riemann", MS + r"0ENS_8TrainVelELb0EE", 0),
+    "ms_poly7_series": ("riemann", MS + r"0ENS_4PolyILi7EEELb0EE", 0),
+    # the same step loops with the in-launch close after them (RiemannConfig::close "launch")
+    "msc_pi4_series_exact": ("riemann", MS + r"3ENS_3Pi4ELb1EE", 0),
+    "msc_pi4_series": ("riemann", MS + r"0ENS_3Pi4ELb1EE", 0),
     "table2d_stream_0_16": ("table", r"table2d_stream_kernelILi0ELi16ELb0EE", 0),
     "table2d_stream_0_30": ("table", r"table2d_stream_kernelILi0ELi30ELb0EE", 0),
     "table2d_stream_1_16": ("table", r"table2d_stream_kernelILi1ELi16ELb0EE", 0),

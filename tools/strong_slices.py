@@ -53,6 +53,11 @@ def main(argv=None) -> int:
     ap.add_argument("--step-streams", default="0", help="comma list (0 = the plan's auto)")
     ap.add_argument("--graphs", choices=["on", "off", "both"], default="on",
                     help="batches as graph replays, direct launches, or both")
+    ap.add_argument("--close", default="auto",
+                    help="comma list of multi-step batch closes: auto, kernel, launch")
+    ap.add_argument("--ar-host", default="on", choices=["on", "off", "both"],
+                    help="bucketed all-reduce straight into pinned memory (on), or in place "
+                         "on the device + a copy (off)")
     ap.add_argument("--jsonl", default="")
     a = ap.parse_args(argv)
 
@@ -62,13 +67,14 @@ def main(argv=None) -> int:
     rows = []
     modes = {"on": [True], "off": [False], "both": [True, False]}[a.collective]
     gmodes = {"on": [True], "off": [False], "both": [True, False]}[a.graphs]
-    configs = [(gr, c, q, gm) for gr in (int(x) for x in a.grids.split(","))
+    armodes = {"on": [True], "off": [False], "both": [True, False]}[a.ar_host]
+    configs = [(gr, c, q, gm, cl, ar) for gr in (int(x) for x in a.grids.split(","))
                for c in modes for q in (int(y) for y in a.step_streams.split(","))
-               for gm in gmodes]
+               for gm in gmodes for cl in a.close.split(",") for ar in armodes]
     for g in (int(x) for x in a.gpus.split(",")):
-        for grid, coll, ss, gm in configs:
+        for grid, coll, ss, gm, cl, ar in configs:
             it = Integrator("pi4", n=n, slots=48, grid=grid, force_collective=coll,
-                            slice_of=(0, g), step_streams=ss)
+                            slice_of=(0, g), step_streams=ss, close=cl, allreduce_to_host=ar)
             ms = timed(it.plan, a.steps, coll, gm)
             v = it.plan.host_result(it.plan.host_index_of(a.steps - 1, True))
             # rank 0's slice of [0, 1): its exact integral is 4 atan(x1)
@@ -77,6 +83,9 @@ def main(argv=None) -> int:
             row = {"G": g, "n_total": n, "n_per_gpu": it.plan.count,
                    "grid": it.plan.grid, "grid_arg": grid, "rccl_stage": coll,
                    "step_streams": it.plan.step_streams(a.steps), "graphs": gm,
+                   "close": cl, "close_in_launch": it.plan.close_in_launch,
+                   "allreduce_to_host": it.plan.allreduce_to_host,
+                   "result": v,
                    "ms_per_step": ms, "us_per_step": ms * 1e3,
                    "per_gpu_subint_per_s": it.plan.count / (ms * 1e-3),
                    "projected_strong_value": n / (ms * 1e-3),
@@ -84,7 +93,8 @@ def main(argv=None) -> int:
             rows.append(row)
             print(json.dumps(row), flush=True)
             del it
-    key = lambda r: (r["grid_arg"], r["rccl_stage"], r["step_streams"], r["graphs"])  # noqa: E731
+    key = lambda r: (r["grid_arg"], r["rccl_stage"], r["step_streams"], r["graphs"],  # noqa: E731
+                     r["close"], r["allreduce_to_host"])
     base = {key(r): r["ms_per_step"] for r in rows if r["G"] == 1}
     for r in rows:
         b = base.get(key(r))

@@ -302,6 +302,40 @@ struct Pi4 : TileDefaults<Pi4> {
       const double b2 = 2.0 * sd.b;
       // sum_u e_u (U e_m + B sum k^2), then every sample's e^2 on top (|t| <= ~1e-12)
       double t = fma(kSumK2, sd.b, static_cast<double>(U) * sd.em);
+#if MIINT_PI4_PIPE
+      // Software-pipelined by one pair: pair p+1's residuals are formed between pair p's two
+      // accumulations, so no instruction waits on the one issued just before it (at one
+      // wave per SIMD nothing else would fill that gap). Same operations, same order of the
+      // t accumulations: bitwise the plain loop's value. The empty asm statements pin the
+      // order (each takes the value just produced and the operand of the next instruction).
+      constexpr int kN = kSubs * kPairs;
+      double ec = centre_g(sd, 0), a = centre_slope(sd, b2, 0);
+      double c = fma(pk2[0], sd.b, ec);
+      double en = fma(-pk[0], a, c);
+      double ep = fma(pk[0], a, c);
+#pragma unroll
+      for (int p = 1; p < kN; ++p) {
+        const int q = p / kPairs, j = p % kPairs;
+        if (j == 0) {
+          ec = centre_g(sd, q);
+          a = centre_slope(sd, b2, q);
+        }
+        double c2 = fma(pk2[j], sd.b, ec);
+        asm volatile("" : "+v"(c2), "+v"(t));
+        t = fma(ep, ep, t);
+        asm volatile("" : "+v"(t), "+v"(c2));
+        double en2 = fma(-pk[j], a, c2);
+        asm volatile("" : "+v"(en2), "+v"(t));
+        t = fma(en, en, t);
+        asm volatile("" : "+v"(t), "+v"(c2));
+        double ep2 = fma(pk[j], a, c2);
+        asm volatile("" : "+v"(ep2), "+v"(ec));
+        en = en2;
+        ep = ep2;
+      }
+      t = fma(ep, ep, t);
+      t = fma(en, en, t);
+#else
 #pragma unroll
       for (int q = 0; q < kSubs; ++q) {
         const double ec = centre_g(sd, q);         // e at the centre (+ mean k^2 B)
@@ -319,6 +353,7 @@ struct Pi4 : TileDefaults<Pi4> {
           asm volatile("" : "+v"(t));
         }
       }
+#endif
       // U samples of s (1 + e + e^2): s U + s (sum e + sum e^2)
       return fma(sd.s, t, fma(sd.s, static_cast<double>(U), acc));
     } else {

@@ -98,6 +98,7 @@ struct RiemannConfig {
   // Bucketed batches all-reduce their step values straight into the pinned host slots
   // (RCCL's receive buffer is the mapped host memory) instead of in place on the device
   // followed by a copy to pinned memory: one stream operation and one kernel boundary fewer.
+  // Directly enqueued batches only: a captured batch graph keeps the device buffer + copy.
   bool allreduce_to_host = true;
   int step_streams = 0;         // chained graph batches: steps dealt round-robin to this many
                                 // streams (each its own chain, ramp and tail of one step
@@ -254,7 +255,8 @@ class RiemannPlan {
   bool multistep() const { return chained() && multistep_; }
   // Multi-step batches are closed inside the persistent launch (RiemannConfig::close).
   bool close_in_launch() const { return multistep() && close_launch_; }
-  // Bucketed batches all-reduce into pinned host memory (RiemannConfig::allreduce_to_host).
+  // Bucketed batches enqueued directly all-reduce into pinned host memory
+  // (RiemannConfig::allreduce_to_host); captured batch graphs keep the device buffer + copy.
   bool allreduce_to_host() const { return bucketed() && cfg_.allreduce_to_host; }
 
  private:
@@ -283,6 +285,7 @@ class RiemannPlan {
   DeviceBuffer<double> ms_partials_;  // multistep: slots x grid partials
   bool multistep_ = false;
   bool close_launch_ = false;         // multistep batches closed in-launch
+  bool capturing_ = false;            // batch_graph() is capturing (enqueue_bucket_reduce)
   DeviceBuffer<unsigned int> ms_ticket_;  // its arrival counters (close_batch_in_launch)
   DeviceBuffer<double> result_;
   DeviceBuffer<double> sync_;      // barrier(): the 1-double all-reduce's operand

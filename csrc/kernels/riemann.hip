@@ -735,19 +735,28 @@ __global__ __launch_bounds__(kMaxBlock) kFullOccupancy void riemann_multistep_ke
 // The step loop's state lifts every multi-step kernel to 106 SGPRs: 7 waves per SIMD. Those
 // with few VGPRs take the 8-wave hint instead (the extra SGPRs go to VGPR lanes, outside the
 // tile loop).
+// The table's segment tiles take the 8-wave hint too: without it they held 106 VGPRs in the
+// multi-step kernel (4 waves per SIMD, slower than chained launches: profiles/r3/
+// multistep_ab.md); with it 42 (segment tiles) / 58 (per sample) VGPRs, 78 SGPRs, no
+// scratch, and the batch runs 5.6 % faster than chained (profiles/r6/batch_tail.md).
 template <DivMode M, class F>
 constexpr bool multistep_o8() {
+  if constexpr (__is_same(F, Table) || __is_same(F, TableF32)) return true;
   return M == DivMode::kIeee && (__is_same(F, Pi4F32) || __is_same(F, Pi4F32Wide) ||
                                  __is_same(F, Pi4F32Acc32));
 }
+// Instantiations whose in-launch close would not fit their register budget (under the
+// 8-wave hint the close code spills 28 bytes: the table's tiles, the fp32 IEEE tiles): their
+// plans close batches with the closing kernel whatever RiemannConfig::close says.
+template <DivMode M, class F>
+constexpr bool multistep_close_ok() {
+  return !multistep_o8<M, F>();
+}
 // Instantiations the multi-step batch does not pay for (profiles/r3/multistep_ab.md): the
-// table's segment tiles hold 106 VGPRs in it (4 waves per SIMD against 8 chained: 70.3 vs
-// 69.4 us per 1e9), and the fp64 per-sample IEEE division tiles ran 3.3 % slower even at 8
-// waves (371 vs 359 us).
+// fp64 per-sample IEEE division tiles ran 3.3 % slower even at 8 waves (371 vs 359 us).
 template <DivMode M, class F>
 constexpr bool multistep_pays() {
-  return !(__is_same(F, Table) || __is_same(F, TableF32) ||
-           (M == DivMode::kIeee && (__is_same(F, Pi4) || __is_same(F, Pi4Wide))));
+  return !(M == DivMode::kIeee && (__is_same(F, Pi4) || __is_same(F, Pi4Wide)));
 }
 
 // Closes a multi-step launch: workgroup s sums step s's partials in index order (finalize
@@ -872,12 +881,17 @@ void launch_multistep_t(const RiemannParams& p, LaunchShape shape, const double*
                         int table_n, double* partials, int steps, unsigned rot,
                         unsigned* ticket, double scale, double* out, hipStream_t stream) {
   if constexpr (multistep_pays<M, F>()) {
-    if (ticket)
-      launch_multistep_c<M, F, true>(p, shape, table, table_n, partials, steps, rot, ticket,
-                                     scale, out, stream);
-    else
-      launch_multistep_c<M, F, false>(p, shape, table, table_n, partials, steps, rot, ticket,
-                                      scale, out, stream);
+    if constexpr (multistep_close_ok<M, F>()) {
+      if (ticket) {
+        launch_multistep_c<M, F, true>(p, shape, table, table_n, partials, steps, rot, ticket,
+                                       scale, out, stream);
+        return;
+      }
+    } else {
+      MIINT_CHECK(ticket == nullptr, "this integrand closes multi-step batches by a kernel");
+    }
+    launch_multistep_c<M, F, false>(p, shape, table, table_n, partials, steps, rot, ticket,
+                                    scale, out, stream);
   } else {
     fail("this integrand/division keeps chained batches (no multi-step kernel)", __FILE__,
          __LINE__);
@@ -901,6 +915,8 @@ template <DivMode M, class F>
 void multistep_per_cu_t(int block, bool close, int* out) {
   if constexpr (!multistep_pays<M, F>())
     *out = 0;
+  else if constexpr (!multistep_close_ok<M, F>())
+    *out = close ? 0 : multistep_occupancy<M, F, false>(block);
   else
     *out = close ? multistep_occupancy<M, F, true>(block) : multistep_occupancy<M, F, false>(block);
 }

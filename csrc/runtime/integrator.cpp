@@ -97,10 +97,13 @@ RiemannPlan::RiemannPlan(const RiemannConfig& cfg, int device, const Comm* comm)
     if (res_kernel > 0 && cfg.grid <= 0 && g > res_kernel) g = res_kernel;
     close_launch_ = cfg.close == "launch" ||
                     (cfg.close == "auto" && auto_close_in_launch(g, cfg.block));
-    const int resident =
+    // 0: this integrand has no in-launch close (it closes with the kernel regardless)
+    const int res_close =
         close_launch_
             ? riemann_multistep_grid(params_, cfg.dtype, cfg.div, cfg.block, info.num_cus, true)
-            : res_kernel;
+            : 0;
+    if (res_close == 0) close_launch_ = false;
+    const int resident = close_launch_ ? res_close : res_kernel;
     if (resident > 0 && cfg.grid <= 0 && shape_.grid > resident) shape_.grid = resident;
     multistep_ = resident > 0 && shape_.grid <= resident;
     if (!multistep_) close_launch_ = false;
@@ -264,7 +267,10 @@ void RiemannPlan::enqueue_chain_streams(hipStream_t cs, int nsteps) {
 // place and one copy follows.
 void RiemannPlan::enqueue_bucket_reduce(hipStream_t s, int nsteps) const {
   const size_t n = static_cast<size_t>(nsteps);
-  if (allreduce_to_host()) {
+  // (not inside a graph capture: RCCL may try to IPC-register a captured collective's
+  // buffers, NCCL_GRAPH_REGISTER, which pinned host memory cannot be; the captured batch
+  // keeps the device receive buffer and its copy node)
+  if (allreduce_to_host() && !capturing_) {
     comm_->allreduce_sum(result_.get(), host_.device_ptr(), n, s);
     return;
   }
@@ -341,10 +347,13 @@ const Graph* RiemannPlan::batch_graph(int nsteps) {
   // only (no fork/join onto the comm stream).
   const bool one = collective() && comm_->capture_single_stream();
   try {
+    capturing_ = true;
     capture_with(collective() ? comm_ : nullptr, *gr, compute_.get(), [&](hipStream_t s) {
       enqueue_batch(s, one ? s : comm_stream_.get(), nsteps, !one);
     });
+    capturing_ = false;
   } catch (const Error& e) {
+    capturing_ = false;
     // e.g. a collective that cannot be captured on this RCCL build: keep running with
     // direct stream enqueue (same results, more launch overhead) and say why.
     graph_error_ = e.what();

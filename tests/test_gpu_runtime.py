@@ -55,7 +55,8 @@ def test_chained_batches_equal_fused_bitwise(cuda, name, collective):
 
 
 @pytest.mark.parametrize("name", ["pi4", "pi4_fp32", "pi4_fp32acc", "sin", "poly", "train",
-                                  "sin_ieee", "pi4_fp32_ieee", "pi4_exact"])
+                                  "sin_ieee", "pi4_fp32_ieee", "pi4_exact", "table",
+                                  "table_fp32", "table_ieee"])
 def test_multistep_batches_equal_chained_bitwise(cuda, name):
     """A graph batch as ONE persistent multi-step launch + a closing kernel (workgroups rotate
     over virtual blocks from step to step) gives every step the chained batch's value, bit for
@@ -112,6 +113,19 @@ def test_multistep_close_in_launch_bitwise(cuda, shape, graphs):
     got = [a.plan.host_result(a.plan.host_index_of(k, graphs)) for k in range(steps)]
     want = [b.plan.host_result(b.plan.host_index_of(k, graphs)) for k in range(steps)]
     assert got == want and len(set(got)) == 1 and math.isfinite(got[0])
+
+
+@pytest.mark.parametrize("name,dtype,div", [("table", "fp64", "series"),
+                                            ("pi4", "fp32", "ieee")])
+def test_close_in_launch_falls_back_where_it_would_spill(cuda, name, dtype, div):
+    """Kernels under the 8-wave hint (the table's tiles, the fp32 IEEE tiles) would spill
+    with the in-launch close: their plans keep the closing kernel, same multi-step batches."""
+    a = Integrator(name, n=120_000_011, dtype=dtype, div=div, slots=20, close="launch")
+    b = Integrator(name, n=120_000_011, dtype=dtype, div=div, slots=20, close="kernel")
+    assert a.plan.multistep and not a.plan.close_in_launch and a.plan.grid == b.plan.grid
+    for it in (a, b):
+        it.run_steps(20, pipeline=False, graphs=False)
+    assert a.plan.host_result(19) == b.plan.host_result(19)
 
 
 @pytest.mark.parametrize("to_host", [False, True])
@@ -173,10 +187,11 @@ def test_multistep_tile_split_vs_torch(cuda, block):
     assert got == pytest.approx(want, rel=1e-12)
 
 
-@pytest.mark.parametrize("name,div", [("table", "series"), ("pi4", "ieee")])
+@pytest.mark.parametrize("name,div", [("pi4", "ieee")])
 def test_multistep_not_where_it_does_not_pay(cuda, name, div):
-    """The table's segment tiles and the fp64 per-sample IEEE division measured slower as
-    multi-step batches: their plans keep chained batches (multistep_pays)."""
+    """The fp64 per-sample IEEE division measured slower as multi-step batches: its plans
+    keep chained batches (multistep_pays). (The table's segment tiles joined the multi-step
+    path in round 6 under the 8-wave hint: test_multistep_batches_equal_chained_bitwise.)"""
     it = Integrator(name, n=10**8, div=div)
     assert it.plan.chained and not it.plan.multistep
 

@@ -2,7 +2,7 @@
 """Interleaved A/B of batch variants on one GPU: the same per-GPU share, several plan options.
 
 Separate runs of one variant after another drift with the clock state of the box (the same
-20-step batch at the 1/8 share measured 191-200 us from run to run, profiles/r6/close_ab.md),
+20-step batch at the 1/8 share measured 191-200 us from run to run, profiles/r6/batch_tail.md),
 so this tool builds every variant's plan first and then times them in rounds, one batch of
 each variant per round, in rotating order: every variant sees the same drift. Per variant it
 reports the median and minimum over rounds of the host time around one batch
@@ -12,7 +12,8 @@ its hipEvent span, and checks that all variants gave the same value bit for bit.
     python tools/batch_ab.py --slice 8 --steps 20 \
         --variant close=kernel --variant close=launch [--collective] [--jsonl FILE]
 
-A variant is comma-separated Integrator keywords (close=launch,allreduce_to_host=0,...).
+A variant is comma-separated Integrator keywords (close=launch,allreduce_to_host=0,...);
+graphs=1 / graphs=0 in a variant sets how that variant's batches run (else --graphs).
 """
 from __future__ import annotations
 
@@ -61,24 +62,30 @@ def main(argv=None) -> int:
 
     variants = a.variant or [""]
     plans = []
+    graphs_of = {}
     for text in variants:
+        vk = parse_variant(text)
+        name = text or "default"
+        graphs_of[name] = bool(vk.pop("graphs", a.graphs))
         kw = dict(n=int(a.n), slots=a.slots, force_collective=a.collective,
-                  slice_of=(0, a.slice), **parse_variant(text))
+                  slice_of=(0, a.slice), **vk)
         it = Integrator(a.integrand, **kw)
-        plans.append((text or "default", it))
+        if graphs_of[name]:
+            it.plan.prepare_steps(a.steps)
+        plans.append((name, it))
     # warm: >= 30 ms of each variant's batches (code objects, RCCL, clocks)
-    for _, it in plans:
+    for name, it in plans:
         for _ in range(max(1, math.ceil(0.03 / 2e-4 / a.steps))):
-            it.plan.run_steps(a.steps, a.collective, a.graphs)
+            it.plan.run_steps(a.steps, a.collective, graphs_of[name])
     host = {name: [] for name, _ in plans}
     dev = {name: [] for name, _ in plans}
     for r in range(a.rounds):
         order = plans[r % len(plans):] + plans[:r % len(plans)]
         for name, it in order:
-            t = it.plan.run_steps(a.steps, a.collective, a.graphs)
+            t = it.plan.run_steps(a.steps, a.collective, graphs_of[name])
             host[name].append(t["wall_s"] * 1e6)
             dev[name].append(t["device_ms"] * 1e3)
-    values = {name: it.plan.host_result(it.plan.host_index_of(a.steps - 1, a.graphs))
+    values = {name: it.plan.host_result(it.plan.host_index_of(a.steps - 1, graphs_of[name]))
               for name, it in plans}
     same = len(set(values.values())) == 1
     rows = []
@@ -86,7 +93,8 @@ def main(argv=None) -> int:
         h, d = host[name], dev[name]
         row = {"variant": name, "slice": a.slice, "n_per_gpu": it.plan.count,
                "grid": it.plan.grid, "steps": a.steps, "rounds": a.rounds,
-               "collective": a.collective, "graphs": a.graphs,
+               "collective": a.collective, "graphs": graphs_of[name],
+               "graph_nodes": it.plan.graph_nodes,
                "close_in_launch": it.plan.close_in_launch,
                "allreduce_to_host": it.plan.allreduce_to_host,
                "host_us_median": statistics.median(h), "host_us_min": min(h),

@@ -59,6 +59,8 @@ GUARDED = {
     "ms_sin_ieee": ("riemann", MS + r"1ENS_3SinELb0EE", 0),
     "ms_train_series": ("riemann", MS + r"0ENS_8TrainVelELb0EE", 0),
     "ms_poly7_series": ("riemann", MS + r"0ENS_4PolyILi7EEELb0EE", 0),
+    "ms_table_series": ("riemann", MS + r"0ENS_5TableELb0EE", 0),
+    "ms_table_ieee": ("riemann", MS + r"1ENS_5TableELb0EE", 0),
     # the same step loops with the in-launch close after them (RiemannConfig::close "launch")
     "msc_pi4_series_exact": ("riemann", MS + r"3ENS_3Pi4ELb1EE", 0),
     "msc_pi4_series": ("riemann", MS + r"0ENS_3Pi4ELb1EE", 0),

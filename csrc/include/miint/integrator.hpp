@@ -46,14 +46,6 @@ namespace miint {
 constexpr int kAutoStepStreams = 4;
 constexpr uint64_t kStepStreamsMaxCount = 600000000ull;
 
-// RiemannConfig::close = "auto": multi-step batches of at most this many workgroups (at the
-// default 256-thread block) are closed inside the persistent launch, larger ones by the
-// closing kernel. (See auto_close_in_launch.)
-constexpr int kAutoCloseLaunchMaxGrid = 0;
-inline bool auto_close_in_launch(int grid, int block) {
-  return block == kRiemannBlock && grid <= kAutoCloseLaunchMaxGrid;
-}
-
 struct RiemannConfig {
   Integrand integrand = Integrand::kPi4;
   double a = 0.0, b = 1.0;
@@ -92,8 +84,10 @@ struct RiemannConfig {
   //   "kernel": a closing kernel of one workgroup per step after the persistent launch;
   //   "launch": inside the persistent launch (handoff.hpp close_batch_in_launch): the last
   //             arrivals close it, no second kernel and no kernel boundary;
-  //   "auto":   kAutoCloseLaunch below.
-  // Both give the same values bit for bit.
+  //   "auto":   the closing kernel: the in-launch close measured equal at G = 1 and at every
+  //             per-GPU share of an 8-GPU step (profiles/r6/batch_tail.md).
+  // Both give the same values bit for bit. Kernels under the 8-wave hint close by the kernel
+  // whatever is asked (the close code would spill there).
   std::string close = "auto";
   // Bucketed batches all-reduce their step values straight into the pinned host slots
   // (RCCL's receive buffer is the mapped host memory) instead of in place on the device

@@ -89,14 +89,11 @@ RiemannPlan::RiemannPlan(const RiemannConfig& cfg, int device, const Comm* comm)
   MIINT_CHECK(cfg.close == "auto" || cfg.close == "kernel" || cfg.close == "launch",
               "close must be auto, kernel or launch (got " + cfg.close + ")");
   if (cfg.multistep && chained()) {
-    // the in-launch close (kAutoCloseLaunch decides "auto" from the grid the plan would
-    // run): its own instantiation, so its own residency
+    // the in-launch close ("launch"; "auto" is the closing kernel) is its own instantiation,
+    // with its own residency
     const int res_kernel =
         riemann_multistep_grid(params_, cfg.dtype, cfg.div, cfg.block, info.num_cus, false);
-    int g = shape_.grid;
-    if (res_kernel > 0 && cfg.grid <= 0 && g > res_kernel) g = res_kernel;
-    close_launch_ = cfg.close == "launch" ||
-                    (cfg.close == "auto" && auto_close_in_launch(g, cfg.block));
+    close_launch_ = cfg.close == "launch";
     // 0: this integrand has no in-launch close (it closes with the kernel regardless)
     const int res_close =
         close_launch_

@@ -7,6 +7,9 @@
 //   MIINT_FAULT_DELAY_MS=ms       rank r holds its end-of-timing mark back by ms (a slow rank:
 //                                 the timed interval of every other rank is unchanged)
 //   MIINT_FAULT_SCAN_TIMEOUT=1    rank r's train scan reports a hand-off spin timeout
+//   MIINT_FAULT_AR_HOST=1         rank r's check of the all-reduce into pinned memory fails
+//                                 (RiemannPlan::check_allreduce_to_host: every rank then
+//                                 falls back to the device buffer + copy)
 #pragma once
 
 #include <chrono>
@@ -35,6 +38,11 @@ inline void delay(int rank) {
 
 inline bool scan_timeout(int rank) {
   static const bool on = env_int("MIINT_FAULT_SCAN_TIMEOUT", 0) != 0;
+  return on && targets(rank);
+}
+
+inline bool allreduce_to_host_fails(int rank) {
+  static const bool on = env_int("MIINT_FAULT_AR_HOST", 0) != 0;
   return on && targets(rank);
 }
 

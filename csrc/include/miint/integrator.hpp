@@ -251,7 +251,16 @@ class RiemannPlan {
   bool close_in_launch() const { return multistep() && close_launch_; }
   // Bucketed batches enqueued directly all-reduce into pinned host memory
   // (RiemannConfig::allreduce_to_host); captured batch graphs keep the device buffer + copy.
-  bool allreduce_to_host() const { return bucketed() && cfg_.allreduce_to_host; }
+  // Off after check_allreduce_to_host found the transport unable to (every rank agrees).
+  bool allreduce_to_host() const {
+    return bucketed() && cfg_.allreduce_to_host && ar_host_ok_;
+  }
+  // Collective, once per plan before its first batch (launch_steps, run_steps,
+  // diagnose_batch call it): one 1-double all-reduce of rank + 1 into pinned memory, checked
+  // on the host against world (world + 1) / 2; a wrong value or an error on any rank (agreed
+  // by a device-buffer all-reduce) turns allreduce_to_host off for the plan, so a transport
+  // that cannot write host memory costs a copy, not the run.
+  void check_allreduce_to_host();
 
  private:
   void enqueue_batch(hipStream_t cs, hipStream_t rs, int nsteps, bool overlap);
@@ -280,6 +289,8 @@ class RiemannPlan {
   bool multistep_ = false;
   bool close_launch_ = false;         // multistep batches closed in-launch
   bool capturing_ = false;            // batch_graph() is capturing (enqueue_bucket_reduce)
+  bool ar_host_ok_ = true;            // check_allreduce_to_host's verdict
+  bool ar_host_checked_ = false;
   DeviceBuffer<unsigned int> ms_ticket_;  // its arrival counters (close_batch_in_launch)
   DeviceBuffer<double> result_;
   DeviceBuffer<double> sync_;      // barrier(): the 1-double all-reduce's operand

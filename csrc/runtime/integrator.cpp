@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstring>
+#include <limits>
 #include <string>
 #include <vector>
 
@@ -276,6 +277,38 @@ void RiemannPlan::enqueue_bucket_reduce(hipStream_t s, int nsteps) const {
                            hipMemcpyDeviceToHost, s));
 }
 
+void RiemannPlan::check_allreduce_to_host() {
+  if (ar_host_checked_ || !bucketed() || !cfg_.allreduce_to_host) return;
+  ar_host_checked_ = true;
+  DeviceGuard g(device_);
+  hipStream_t s = compute_.get();
+  const double want = 0.5 * static_cast<double>(world_) * (static_cast<double>(world_) + 1.0);
+  const size_t probe = host_.size() - 1;  // the ring's last slot: rewritten before any use
+  host_[probe] = std::numeric_limits<double>::quiet_NaN();
+  host_[0] = static_cast<double>(rank_) + 1.0;
+  MIINT_HIP(hipMemcpyAsync(result_.get(), host_.get(), sizeof(double), hipMemcpyHostToDevice, s));
+  bool ok = true;
+  try {
+    comm_->allreduce_sum(result_.get(), host_.device_ptr() + probe, 1, s);
+    if (cfg_.timeout_s > 0) wait_with_timeout(s, cfg_.timeout_s, comm_);
+    else compute_.sync();
+    ok = host_[probe] == want && !fault::allreduce_to_host_fails(rank_);
+  } catch (const Error&) {
+    ok = false;
+    (void)hipGetLastError();
+    compute_.sync();
+  }
+  // agree over the device-buffer path (sync_ is barrier()'s zero operand: restored)
+  host_[0] = ok ? 0.0 : 1.0;
+  MIINT_HIP(hipMemcpyAsync(sync_.get(), host_.get(), sizeof(double), hipMemcpyHostToDevice, s));
+  comm_->allreduce_sum(sync_.get(), sync_.get(), 1, s);
+  MIINT_HIP(hipMemcpyAsync(host_.get(), sync_.get(), sizeof(double), hipMemcpyDeviceToHost, s));
+  MIINT_HIP(hipMemsetAsync(sync_.get(), 0, sizeof(double), s));
+  if (cfg_.timeout_s > 0) wait_with_timeout(s, cfg_.timeout_s, comm_);
+  else compute_.sync();
+  ar_host_ok_ = host_[0] == 0.0;
+}
+
 void RiemannPlan::enqueue_batch(hipStream_t cs, hipStream_t rs, int nsteps, bool overlap) {
   if (chained()) {
     if (nsteps == 1)
@@ -387,6 +420,7 @@ int RiemannPlan::host_index_of(int k, bool graphs) const {
 void RiemannPlan::launch_steps(int steps, bool pipeline, bool graphs) {
   DeviceGuard g(device_);
   TraceRange tr("miint.plan.launch_steps");
+  check_allreduce_to_host();
   hipStream_t cs = compute_.get();
   hipStream_t rs = comm_stream_.get();
   const int S = cfg_.slots;
@@ -455,6 +489,7 @@ void RiemannPlan::barrier() {
 
 StepTiming RiemannPlan::run_steps(int steps, bool pipeline, bool graphs) {
   DeviceGuard g(device_);
+  check_allreduce_to_host();
   use_graphs(graphs, steps);
   StepTiming t;
   sync();
@@ -475,6 +510,7 @@ BatchDiag RiemannPlan::diagnose_batch(int nsteps) {
   MIINT_CHECK(nsteps >= 1 && nsteps <= cfg_.slots, "diagnose_batch: 1 <= steps <= slots");
   DeviceGuard g(device_);
   TraceRange tr("miint.plan.diagnose_batch");
+  check_allreduce_to_host();
   hipStream_t cs = compute_.get();
   const int tn = static_cast<int>(cfg_.table.size());
   BatchDiag d;

@@ -167,6 +167,28 @@ def test_diagnose_batch_accounts_for_the_timed_batch(cuda):
     assert got == {want}
 
 
+def test_allreduce_to_host_check_falls_back(cuda, monkeypatch):
+    """A transport that cannot all-reduce into pinned memory (MIINT_FAULT_AR_HOST on rank 0:
+    the plan's one-time check fails) costs a copy, not the run: the plan turns
+    allreduce_to_host off before its first batch and gives the same values. (A subprocess: the
+    fault variables are read once per process.)"""
+    code = (
+        "from cuda_v_mpi_amd import Integrator\n"
+        "kw = dict(n=10**9 // 8, slots=20, force_collective=True)\n"
+        "a = Integrator('pi4', **kw)\n"
+        "assert a.plan.allreduce_to_host\n"
+        "a.run_steps(20, pipeline=False, graphs=False)\n"
+        "assert not a.plan.allreduce_to_host\n"
+        "b = Integrator('pi4', n=10**9 // 8, slots=20)\n"
+        "b.run_steps(20, pipeline=False, graphs=False)\n"
+        "assert a.plan.host_result(19) == b.plan.host_result(19)\n"
+        "print('ok')\n")
+    env = dict(os.environ, MIINT_FAULT_RANK="0", MIINT_FAULT_AR_HOST="1")
+    p = subprocess.run(["python", "-c", code], capture_output=True, text=True, timeout=240,
+                       env=env, cwd=REPO)
+    assert p.returncode == 0 and p.stdout.strip().endswith("ok"), p.stderr[-2000:]
+
+
 @pytest.mark.parametrize("block", [64, 256, 1024])
 def test_multistep_tile_split_vs_torch(cuda, block):
     """Multi-step batches (the tile split formed once per batch, every step rotating its

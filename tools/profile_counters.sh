@@ -32,6 +32,10 @@ for g in G1 G2; do
   run pi4_ieee $g "${!g}" "$REPO/build/bin/miint" bench --iters 20 --settle 60 --div ieee
   run pi4_fp32 $g "${!g}" "$REPO/build/bin/miint" bench --iters 200 --settle 300 --dtype fp32
   run pi4_series_exact $g "${!g}" "$REPO/build/bin/miint" bench --iters 200 --settle 300 --div series_exact
+  # the 1/8 share of the headline (the per-GPU work of an 8-GPU strong step): 20- and 64-step
+  # multi-step dispatches (profiles/r6/batch_tail.md)
+  run share8_20 $g "${!g}" "$REPO/build/bin/miint" bench --n 1.25e8 --slots 20 --iters 2000 --settle 2000
+  run share8_64 $g "${!g}" "$REPO/build/bin/miint" bench --n 1.25e8 --slots 64 --iters 2048 --settle 2048
   run sin $g "${!g}" "$REPO/build/bin/miint" bench --iters 200 --settle 300 --integrand sin
   run sin_ocml $g "${!g}" "$REPO/build/bin/miint" bench --iters 4 --integrand sin --div ieee \
     --trig-library --settle 16

@@ -46,6 +46,7 @@ SAMPLES = {  # samples per dispatch of the Riemann workloads (miint bench defaul
     "train": 1e9, "poly": 1e9, "table": 1e9, "table2d": 4096 * 4096, "trainscan": 18e6,
     "pi4_fp32acc": 1e9, "pi4_series_exact": 1e9, "sin_fast": 1e9, "train_fast": 1e9, "table2d_slice8": 512 * 4096,
     "pi4_series_exact_share8": 1.25e8, "pi4_series_g": 1e9,
+    "share8_20": 1.25e8, "share8_64": 1.25e8,
     "materialize": 18e6,
 }
 

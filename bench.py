@@ -564,13 +564,15 @@ def _spread(vals: list[float]) -> dict:
 def rccl_init_lines(path: str | None, limit: int = 16) -> dict:
     """Channel and protocol facts from this rank's captured RCCL INIT log (NCCL_DEBUG_SUBSYS
     INIT,P2P,GRAPH: printed once per communicator): the distinct channel ids of the peer
-    connections, and the lines naming channels, rings or protocols."""
+    connections, and the lines naming channels, rings, trees or protocols (RCCL's LL cutoff
+    warning among them). The per-call algorithm/protocol choice is a TUNING line RCCL prints
+    for EVERY collective — a file write inside the timed region — so it is not captured."""
     import re
 
     if not path or not os.path.exists(path):
         return {"log": path, "channels": None, "lines": []}
     chans, lines = set(), []
-    keep = re.compile(r"channels|nChannels|Pattern|Ring \d+|[Pp]roto|LL128|Tree \d+")
+    keep = re.compile(r"channels|nChannels|Pattern|Ring \d+|[Pp]roto|LL128|LL cutoff|Tree \d+")
     with open(path, errors="replace") as f:
         for ln in f:
             m = re.search(r"Channel (\d+)/\d+ :", ln)

@@ -531,7 +531,9 @@ def main(argv=None) -> int:
                 # the bucketed all-reduce writes every rank's step values straight into
                 # pinned host memory (no copy after it); multi-step batches closed inside the
                 # persistent launch instead of by a closing kernel
-                "allreduce_to_host": bool(plan.allreduce_to_host) if plan is not None else False,
+                # (graph replays keep the device buffer + copy node: RiemannConfig)
+                "allreduce_to_host": bool(plan is not None and plan.allreduce_to_host and
+                                          not graphs),
                 "close_in_launch": bool(plan.close_in_launch) if plan is not None else False,
                 "fused_reduction": not args.unfused,
                 "chained_batches": bool(ran_plan and plan.chained and (graphs or plan.multistep)),

@@ -662,15 +662,16 @@ def batch_diagnostics(args, ctx, integ, plan, dev, cpu: bool, use_torch: bool,
                       transport: dict) -> dict:
     """VERDICT r5 Next #2: one untimed batch after the timed region, taken apart on every
     rank — compute (the batch's kernels), tail (closing kernel + all-reduce + copy to pinned
-    memory) and the host's part (wall - device) — with the max and min over ranks; then the
+    memory), the kernel boundaries the stage events stood in for (device - compute - tail) and
+    the host's part (wall - device) — with the max and min over ranks; then the
     communicator's 8-byte all-reduce latency and allgather bus bandwidth, and RCCL's channel
     and protocol lines from rank 0's INIT log. These say where a multi-GPU step's time went
     (the reference's reduce / barrier / broadcast costs, 4main.c:134-157)."""
     import torch
 
     steps = min(args.steps, plan.slots if plan is not None else args.slots)
-    keys = ("compute_us", "close_us", "allreduce_us", "copy_us", "tail_us", "device_us",
-            "wall_us", "marker_us")
+    keys = ("compute_us", "close_us", "allreduce_us", "copy_us", "tail_us", "boundary_us",
+            "device_us", "wall_us", "marker_us")
     if cpu:  # as the timed CPU steps run: per step the torch fp64 evaluation of the rank's
         # slice, then its gloo all-reduce (which also waits for the slowest rank)
         comp = red = 0.0
@@ -684,7 +685,7 @@ def batch_diagnostics(args, ctx, integ, plan, dev, cpu: bool, use_torch: bool,
             comp, red = comp + (t1 - t0), red + (t2 - t1)
         wall = time.perf_counter() - t_start
         d = {"steps": steps, "compute_us": comp * 1e6, "close_us": 0.0,
-             "allreduce_us": red * 1e6, "copy_us": 0.0, "tail_us": red * 1e6,
+             "allreduce_us": red * 1e6, "copy_us": 0.0, "tail_us": red * 1e6, "boundary_us": 0.0,
              "device_us": (comp + red) * 1e6, "wall_us": wall * 1e6, "marker_us": 0.0,
              "path": "cpu"}
     elif use_torch or plan is None:

@@ -36,6 +36,8 @@ struct BenchRow {
   double n = 0, result = 0, exact = 0, ms = 0;
   int gpus = 1;
   int block = 0, grid = 0;  // launch shape of rank 0's plan
+  bool multistep = false, close_in_launch = false, allreduce_to_host = false;
+  BatchDiag diag;  // --diagnose: rank 0's diagnostic batch (diag.steps == 0 otherwise)
   cli::RankFacts facts;
   cli::Topology topo;
 };
@@ -60,7 +62,7 @@ RiemannConfig make_cfg(const std::string& integ, double n, const std::string& dt
 }
 
 BenchRow bench_one(const cli::Topology& topo, RiemannConfig cfg, int iters, bool graphs,
-                   int settle_steps = -1) {
+                   int settle_steps = -1, bool diagnose = false) {
   BenchRow row;
   row.n = static_cast<double>(cfg.n);
   row.gpus = topo.world;
@@ -81,6 +83,10 @@ BenchRow bench_one(const cli::Topology& topo, RiemannConfig cfg, int iters, bool
     // of the communicator (not only this process's)
     StepTiming t = plan.run_steps(iters, comm != nullptr, graphs);
     const double ms = agree.max(t.wall_s * 1e3 / iters);
+    // untimed, after the clock: one batch of min(iters, slots) steps split into its stages
+    // (RiemannPlan::diagnose_batch; every rank runs it, it has barriers of its own)
+    BatchDiag d;
+    if (diagnose) d = plan.diagnose_batch(std::min(iters, plan.config().slots));
     std::lock_guard<std::mutex> g(mu);
     if (ms > row.ms) row.ms = ms;
     if (rank == topo.rank0) {
@@ -88,6 +94,10 @@ BenchRow bench_one(const cli::Topology& topo, RiemannConfig cfg, int iters, bool
       row.result = plan.host_result(plan.host_index_of(iters - 1, graphs));
       row.block = plan.shape().block;
       row.grid = plan.shape().grid;
+      row.multistep = plan.multistep();
+      row.close_in_launch = plan.close_in_launch();
+      row.allreduce_to_host = plan.allreduce_to_host();
+      row.diag = d;
     }
   });
   return row;
@@ -98,14 +108,28 @@ void print_row(const cli::Args& a, const BenchRow& r, const char* integ, const c
   cli::JsonRecord rec;
   rec.add("integrand", integ).add("dtype", dtype).add("rule", rule).add("n", r.n).add("gpus", r.gpus);
   r.facts.add(rec, r.topo);
-  cli::emit(a, rec.add("block", r.block)
+  rec.add("block", r.block)
                    .add("grid", r.grid)
+                   .add("multistep", r.multistep)
+                   .add("close_in_launch", r.close_in_launch)
+                   .add("allreduce_to_host", r.allreduce_to_host)
                    .add("ms_per_integration", r.ms)
                    .add("subintervals_per_s", r.n / (r.ms * 1e-3))
                    .add("result", r.result)
                    .add("analytic", r.exact)
-                   .add("abs_err", std::fabs(r.result - r.exact)),
-            true);
+                   .add("abs_err", std::fabs(r.result - r.exact));
+  if (r.diag.steps > 0)
+    rec.add("diag_steps", r.diag.steps)
+        .add("diag_compute_us", r.diag.compute_us)
+        .add("diag_close_us", r.diag.close_us)
+        .add("diag_allreduce_us", r.diag.allreduce_us)
+        .add("diag_copy_us", r.diag.copy_us)
+        .add("diag_tail_us", r.diag.tail_us())
+        .add("diag_boundary_us", r.diag.boundary_us())
+        .add("diag_device_us", r.diag.device_us)
+        .add("diag_marker_us", r.diag.marker_us)
+        .add("diag_host_us", r.diag.wall_us - r.diag.device_us);
+  cli::emit(a, rec, true);
 }
 
 int selfcheck() {
@@ -232,7 +256,8 @@ constexpr const char* kUsage =
     "       miint bench [--integrand pi4] [--n 1e9] [--dtype fp64|fp32|fp32acc] [--rule left]\n"
     "                   [--iters 200] [--gpus G] [--div series_exact|series|ieee] [--unfused] [--no-graph]\n"
     "                   [--block B] [--grid G] [--step-streams S] [--trig-library] [--settle N]\n"
-    "                   [--no-multistep] [--slots K]\n"
+    "                   [--no-multistep] [--slots K] [--close auto|kernel|launch] [--no-ar-host]\n"
+    "                   [--diagnose]\n"
     "       miint sweep [--gpus G]\n"
     "       miint table2d [--grid 4096] [--gpus G] [--slice R/W] [--no-graph]\n"
     "                     [--step-streams S] [--min-wg W] [--settle-ms MS] [--no-multistep]\n"
@@ -271,6 +296,11 @@ int main(int argc, char** argv) {
       c.step_streams = static_cast<int>(a.integer("step-streams", 0));
       c.multistep = !a.flag("no-multistep");  // A-B: chained batches instead
       c.slots = static_cast<int>(a.integer("slots", c.slots));
+      // A-B knobs of a multi-step batch's tail (profiles/r6/batch_tail.md): the closing
+      // kernel or the in-launch close; the bucketed all-reduce into pinned host slots or
+      // into the device buffer and a copy
+      c.close = a.str("close", c.close);
+      c.allreduce_to_host = !a.flag("no-ar-host");
       // validation / A-B: kIeee sin and cos by ocml per sample instead of fast_trig.hpp
       if (a.flag("trig-library")) set_trig_library(true);
       MIINT_CHECK(riemann_block_ok(c.block), "--block must be 64, 128, 256, 512 or 1024");
@@ -278,7 +308,8 @@ int main(int argc, char** argv) {
       // --settle N: untimed steps before the timed ones (default: ~60 ms worth; profiler
       // runs pass a few, so the trace holds little more than the timed dispatches)
       const BenchRow r = bench_one(topo, c, iters, graphs,
-                                   static_cast<int>(a.integer("settle", -1)));
+                                   static_cast<int>(a.integer("settle", -1)),
+                                   a.flag("diagnose"));
       if (topo.rank0 == 0)
         print_row(a, r, a.str("integrand", "pi4").c_str(), a.str("dtype", "fp64").c_str(),
                   a.str("rule", "left").c_str());

@@ -139,10 +139,16 @@ struct OneShotTiming {
 // One batch of a plan taken apart by hipEvents between its stream stages (RiemannPlan::
 // diagnose_batch; bench.py's untimed diagnostic batch on several GPUs). Microseconds.
 // An event between two stages is a queue packet of its own whose release costs the device
-// ~2 us (gfx950, ROCm 7.2: profiles/r6/batch_tail.md), so the batch runs twice: once between
+// a few us (gfx950, ROCm 7.2: profiles/r6/batch_tail.md), so the batch runs twice: once between
 // two events only (device_us, wall_us: the batch as the timed region runs it), once with an
-// event after every stage (staged_us); marker_us = (staged_us - device_us) / 3 is the price
-// of one event, and every stage below has it subtracted once.
+// event after every stage (staged_us). marker_us is one event's own price, measured on the
+// idle stream afterwards (the median gap between back-to-back events), and every stage below
+// has it subtracted once. (Round 6 first priced an event as (staged_us - device_us) / 3: two
+// runs of a 1.4 ms batch differ by more than three events, so at N = 1e9 that left ~4 us of
+// event in every empty stage.) An event between two kernels also takes the place of the
+// kernel boundary it sits in (the end-of-kernel release and the next dispatch), so the stages
+// add up to less than the plain batch: boundary_us = device_us - compute_us - tail_us is that
+// remainder (~5 us per batch on gfx950, plus the two passes' run-to-run spread).
 struct BatchDiag {
   int steps = 0;
   double compute_us = 0.0;    // the batch's kernels up to the step values' partials (a multi-
@@ -155,7 +161,8 @@ struct BatchDiag {
   double device_us = 0.0;     // the batch between two events
   double staged_us = 0.0;     // the same batch with the stage events
   double wall_us = 0.0;       // host: launch call to every stage drained (the plan's sync)
-  double tail_us() const { return device_us - compute_us; }  // close + all-reduce + copy
+  double tail_us() const { return close_us + allreduce_us + copy_us; }
+  double boundary_us() const { return device_us - compute_us - tail_us(); }
 };
 
 class RiemannPlan {

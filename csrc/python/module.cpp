@@ -326,6 +326,7 @@ PYBIND11_MODULE(_miint, m) {
              r["allreduce_us"] = d.allreduce_us;
              r["copy_us"] = d.copy_us;
              r["tail_us"] = d.tail_us();
+             r["boundary_us"] = d.boundary_us();
              r["marker_us"] = d.marker_us;
              r["device_us"] = d.device_us;
              r["staged_us"] = d.staged_us;

@@ -569,8 +569,17 @@ BatchDiag RiemannPlan::diagnose_batch(int nsteps) {
   sync();
   last_mode_ = 1;
   d.staged_us = Event::elapsed_ms(e0, e4) * 1e3;
-  const double m = std::max(0.0, (d.staged_us - d.device_us) / 3.0);
-  d.marker_us = m;
+  // one event's price: back-to-back events on the now idle stream
+  {
+    Event m[9];
+    for (Event& e : m) e.record(cs);
+    MIINT_HIP(hipStreamSynchronize(cs));
+    std::vector<double> gaps;
+    for (int i = 1; i < 9; ++i) gaps.push_back(Event::elapsed_ms(m[i - 1], m[i]) * 1e3);
+    std::nth_element(gaps.begin(), gaps.begin() + 4, gaps.end());
+    d.marker_us = gaps[4];
+  }
+  const double m = d.marker_us;
   d.compute_us = Event::elapsed_ms(e0, e1) * 1e3 - m;
   d.close_us = std::max(0.0, Event::elapsed_ms(e1, e2) * 1e3 - m);
   d.allreduce_us = std::max(0.0, Event::elapsed_ms(e2, e3) * 1e3 - m);

@@ -72,7 +72,7 @@ class Integrator:
                  chain: bool = True, comm_obj=None, threads: int = 0,
                  slice_of: tuple[int, int] | None = None, step_streams: int = 0,
                  block: int = 256, multistep: bool = True, close: str = "auto",
-                 allreduce_to_host: bool = True, **spec_kw):
+                 allreduce_to_host: bool = True, timeout_s: float = 300.0, **spec_kw):
         spec = integrands.get(integrand, **spec_kw) if isinstance(integrand, str) else integrand
         if a is not None or b is not None:
             spec = dataclasses.replace(spec, a=spec.a if a is None else a,
@@ -118,6 +118,7 @@ class Integrator:
             cfg.multistep = multistep  # graph batches as one persistent launch
             cfg.close = close  # multi-step batches closed by a kernel or inside the launch
             cfg.allreduce_to_host = allreduce_to_host  # bucketed all-reduce into pinned memory
+            cfg.timeout_s = timeout_s  # collective watchdog of the plan's sync (<= 0: none)
             if slice_of is not None:  # (rank, world): that rank's share, on this device
                 cfg.slice_rank, cfg.slice_world = int(slice_of[0]), int(slice_of[1])
             self._m = m

@@ -127,7 +127,8 @@ def test_bench_diagnostic_batch_cpu():
     js = json.loads([l for l in p.stdout.splitlines() if l.startswith("{")][-1])
     d = js["diagnostic_batch"]
     assert d["path"] == "cpu" and d["steps"] == 3
-    for k in ("compute_us", "tail_us", "allreduce_us", "device_us", "wall_us", "host_us"):
+    for k in ("compute_us", "tail_us", "boundary_us", "allreduce_us", "device_us", "wall_us",
+              "host_us"):
         assert len(d[k]["per_rank"]) == 2 and d[k]["max"] >= d[k]["min"], k
     assert d["compute_us"]["min"] > 0 and d["allreduce_us"]["min"] > 0
     c = d["comm"]

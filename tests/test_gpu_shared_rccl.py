@@ -152,7 +152,8 @@ def test_bench_two_ranks_native_rccl_one_gpu(cuda):
     assert r["native_comm_verified"] and r["config"]["allreduce_to_host"]
     d = r["diagnostic_batch"]
     assert d["path"] == "native" and d["steps"] == 10 and d["allreduce_to_host"]
-    for k in ("compute_us", "tail_us", "allreduce_us", "device_us", "wall_us", "host_us"):
+    for k in ("compute_us", "tail_us", "boundary_us", "allreduce_us", "device_us", "wall_us",
+              "host_us"):
         assert len(d[k]["per_rank"]) == 2 and d[k]["max"] >= d[k]["min"], k
     assert d["compute_us"]["min"] > 0 and d["allreduce_us"]["max"] > 0
     assert d["comm"]["transport"] == "rccl" and d["comm"]["allreduce_8b_us"] > 0

@@ -71,7 +71,8 @@ def main(argv=None) -> int:
         name = text or "default"
         graphs_of[name] = bool(vk.pop("graphs", a.graphs))
         kw = dict(n=int(a.n), slots=a.slots, force_collective=a.collective,
-                  slice_of=(0, a.slice), **vk)
+                  slice_of=(0, a.slice))
+        kw.update(vk)  # a variant may set any of these too (force_collective=1, ...)
         it = Integrator(a.integrand, **kw)
         if graphs_of[name]:
             it.plan.prepare_steps(a.steps)

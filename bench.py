@@ -26,7 +26,10 @@ never imports torch or touches the GPU itself. Every child runs the torchrun pat
 
 Warmup: the W warmup steps, then untimed repeats of the timed K-step pattern for at least
 --settle-ms (60) so the timed region starts at steady clocks (from idle the GPU ramps from
-~90 to 76.8 us per step over ~25 ms); the JSON line reports those as "warmup_settle_steps".
+~90 to 76.8 us per step over ~25 ms), then one more K-step pattern on its own (launch, sync):
+the first launch call after a sync that drained a run of queued launches holds the host
+6-8 us longer than the next ones, with the GPU idle behind it (tools/share_duty_probe.py,
+profiles/r6/batch_tail.md). The JSON line reports all of these as "warmup_settle_steps".
 
 Scaling: the headline is strong (N = 1e9 in total; --scaling weak makes --samples a per-GPU
 count instead). The results of the last batch of timed steps (every rank holds the global
@@ -85,6 +88,9 @@ def parse(argv=None) -> argparse.Namespace:
                    help="after the W warmup steps, repeat the timed K-step pattern (untimed) "
                         "for at least this long so the timed steps run at steady clocks (0 = off)")
     # (--n is a prefix of torchrun's own --nnodes/--nproc-per-node: use --samples under torchrun)
+    p.add_argument("--no-rearm-batch", action="store_true",
+                   help="A-B: no untimed K-step pattern on its own between the settle and the "
+                        "timed region")
     p.add_argument("--samples", "--n", dest="n", type=float, default=1e9,
                    help="samples in total (strong, the default: the metric's N = 1e9 split "
                         "over the GPUs) or per GPU (--scaling weak)")
@@ -377,6 +383,15 @@ def main(argv=None) -> int:
             launch(args.steps)
         finish()
         settle_steps = (1 + calls) * args.steps
+    if not cpu and not args.no_rearm_batch:
+        # the timed pattern once more, launched and synced on its own: the first launch call
+        # after the sync that drained the queued settle (or warmup) launches costs the host
+        # 6-8 us more than a launch after a synced one, while the GPU waits for it; the
+        # timed region's launch should be the steady one (tools/share_duty_probe.py: at the
+        # 1/8 share 210.4 -> 202.3 us per 20-step batch, profiles/r6/batch_tail.md)
+        launch(args.steps)
+        finish()
+        settle_steps += args.steps
 
     # ---- timed region: barrier + device sync on both sides, K steps in between
     g0 = plan.graph_launches if plan is not None else 0
@@ -471,6 +486,8 @@ def main(argv=None) -> int:
             "steps": args.steps,
             "warmup": args.warmup,
             "warmup_settle_steps": settle_steps,
+            # the untimed K-step pattern launched and synced on its own right before the clock
+            "warmup_rearm_batch": not cpu and not args.no_rearm_batch,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
             "scaling": args.scaling,

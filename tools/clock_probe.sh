@@ -22,9 +22,19 @@ probe() {  # probe NAME ITERS ARGS...
   echo "$name $(grep '^{' "gpurun_out/clock_$name.json" | tail -1)" >> "$out"
 }
 echo "idle $(rocm-smi --showclocks 2>/dev/null | grep -i 'sclk' | head -1)" >> "$out"
-probe pi4_series 30000 --integrand pi4 && \
-probe pi4_fp32 50000 --integrand pi4 --dtype fp32 && \
-probe sin_series 25000 --integrand sin && \
-probe pi4_ieee 6000 --integrand pi4 --div ieee
+if [ "${SHARES:-0}" = 1 ]; then
+  # the headline's per-GPU shares of a G-GPU strong-scaled step, in the driver's 20-step
+  # batches (profiles/r6/batch_tail.md: does the share run at G = 1's clock?)
+  probe share1 30000 --integrand pi4 --slots 20 && \
+  probe share8 200000 --integrand pi4 --n 1.25e8 --slots 20 && \
+  probe share4 110000 --integrand pi4 --n 2.5e8 --slots 20 && \
+  probe share8_again 200000 --integrand pi4 --n 1.25e8 --slots 20 && \
+  probe share1_again 30000 --integrand pi4 --slots 20
+else
+  probe pi4_series 30000 --integrand pi4 && \
+  probe pi4_fp32 50000 --integrand pi4 --dtype fp32 && \
+  probe sin_series 25000 --integrand sin && \
+  probe pi4_ieee 6000 --integrand pi4 --div ieee
+fi
 rocm-smi --showclocks >> "$out" 2>&1 || true
 echo done

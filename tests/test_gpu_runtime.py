@@ -630,6 +630,8 @@ def test_bench_contract(native, cuda):
     assert js["direct_steps_timed"] == 20 and js["graph_replays_timed"] == 0
     assert js["config"]["batch_launch"] == "direct" and js["config"]["multistep"]
     assert js["config"]["graphs"] is False
+    # the settle, then the timed pattern once more on its own before the clock (untimed)
+    assert js["warmup_rearm_batch"] and js["warmup_settle_steps"] >= 2 * 20
     # the record carries what the headline rests on: IEEE-division speed and per-point ulp
     assert js["ieee_div_value"] > 1e11 and js["ieee_div"]["abs_err"] < 2e-9
     # the headline division (series_exact): per point within 3 ulp of the IEEE path's own

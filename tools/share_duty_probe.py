@@ -13,9 +13,12 @@ same 20-step batch, in rotating order:
                 strong_slices.py, batch_ab.py);
   driver        bench.py's timed region: ~60 ms of back-to-back batches, a sync, then ONE
                 batch timed from its launch call to its sync;
-  after_settle_3rd, short_settle, idle_1ms
-                the same with the third batch after the settle, a 5-batch settle, or 1 ms
-                of idle GPU before the batch: which part of `driver` costs.
+  after_settle_3rd, short_settle, idle_1ms, second, devsync, warm1
+                the same with the third / second batch after the settle, a 5-batch settle,
+                1 ms of idle GPU, a device-wide sync or a 1-step batch before the batch:
+                which part of `driver` costs;
+  bench_like    bench.py's timed region after its re-arm batch, with the launch call, the
+                plan's sync and torch.cuda.synchronize() timed apart.
 
 Host microseconds per batch (median over reps) for each. profiles/r6/batch_tail.md.
 """
@@ -130,10 +133,33 @@ def main(argv=None) -> int:
             p.sync()
             return one("warm1")
 
+        parts = {"launch": [], "sync": [], "device_sync": [], "idle_device_sync": []}
+
+        def bench_like():  # bench.py's timed region after its re-arm batch, taken apart
+            for _ in range(settle):
+                p.launch_steps(S, False, False)
+            p.sync()
+            one(None)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            p.launch_steps(S, False, False)
+            t1 = time.perf_counter()
+            p.sync()
+            t2 = time.perf_counter()
+            torch.cuda.synchronize()
+            t3 = time.perf_counter()
+            torch.cuda.synchronize()
+            t4 = time.perf_counter()
+            parts["launch"].append((t1 - t0) * 1e6)
+            parts["sync"].append((t2 - t1) * 1e6)
+            parts["device_sync"].append((t3 - t2) * 1e6)
+            parts["idle_device_sync"].append((t4 - t3) * 1e6)
+            return t3 - t0
+
         modes = [("back_to_back", back_to_back), ("synced", synced), ("driver", driver),
                  ("after_settle_3rd", after_settle_3rd), ("short_settle", short_settle),
                  ("idle_1ms", idle_1ms), ("second", second), ("devsync", devsync),
-                 ("warm1", warm1)]
+                 ("warm1", warm1), ("bench_like", bench_like)]
         res.update({m: [] for m, _ in modes if m not in res})
         for r in range(a.reps):
             order = modes[r % len(modes):] + modes[:r % len(modes)]
@@ -147,6 +173,7 @@ def main(argv=None) -> int:
                **{f"{k}_us_min": min(v) for k, v in res.items()},
                **{f"{k}_launch_call_us_median": statistics.median(v)
                   for k, v in launch_call.items()},
+               **{f"bench_like_{k}_us_median": statistics.median(v) for k, v in parts.items()},
                "value": p.host_result(p.host_index_of(S - 1, False))}
         print(json.dumps(row), flush=True)
     return 0

@@ -383,7 +383,16 @@ def main(argv=None) -> int:
             launch(args.steps)
         finish()
         settle_steps = (1 + calls) * args.steps
-    if not cpu and not args.no_rearm_batch:
+    rearm = not cpu and not args.no_rearm_batch
+    # the native plan on several GPUs has a device barrier of its own (below); there the host
+    # barrier comes BEFORE the re-arm batch, so the GPU does not sit idle through it right
+    # before the clock: a batch that follows >= 100 us of idle GPU runs 4-7 us slower at the
+    # 1/8 share (share_duty_probe.py --idle-us), and a gloo barrier of 8 local ranks takes
+    # ~100-300 us (profiles/r6/batch_tail.md)
+    device_barrier = ran_plan and world > 1
+    if rearm:
+        if device_barrier:
+            ctx.barrier()
         # the timed pattern once more, launched and synced on its own: the first launch call
         # after the sync that drained the queued settle (or warmup) launches costs the host
         # 6-8 us more than a launch after a synced one, while the GPU waits for it; the
@@ -396,10 +405,12 @@ def main(argv=None) -> int:
     # ---- timed region: barrier + device sync on both sides, K steps in between
     g0 = plan.graph_launches if plan is not None else 0
     d0 = plan.direct_steps if plan is not None else 0
-    ctx.barrier()
+    if not (rearm and device_barrier):
+        ctx.barrier()
     if plan is not None and not cpu:
         # then a device barrier through the rank's RCCL communicator (an 8-byte all-reduce on
-        # the compute stream, polled): ranks leave a host barrier up to tens of us apart,
+        # the compute stream, polled): ranks leave a host barrier (or the re-arm batch's
+        # all-reduce) up to tens of us apart,
         # and the early ones would count that skew as step time inside the batch's
         # all-reduce; an all-reduce completes on every rank within ~us (no-op on one GPU)
         plan.barrier()
@@ -487,7 +498,13 @@ def main(argv=None) -> int:
             "warmup": args.warmup,
             "warmup_settle_steps": settle_steps,
             # the untimed K-step pattern launched and synced on its own right before the clock
-            "warmup_rearm_batch": not cpu and not args.no_rearm_batch,
+            "warmup_rearm_batch": rearm,
+            # what stands right before the clock: the host barrier (control plane), the native
+            # plan's RCCL device barrier, or the device barrier alone with the host barrier
+            # moved before the re-arm batch
+            "pre_clock_barrier": ("device" if (rearm and device_barrier) else
+                                  "host+device" if (plan is not None and not cpu and world > 1
+                                                    and ran_plan) else "host"),
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
             "scaling": args.scaling,

@@ -227,6 +227,7 @@ def test_bench_driver_launch_form_json_contract():
     assert js["launcher"] == "torchrun" and js["scaling"] == "strong"
     assert js["comm_fallback"] is None
     assert js["warmup_rearm_batch"] is False  # a GPU launch artefact: not run on the CPU path
+    assert js["pre_clock_barrier"] == "host"
     assert js["metric"].startswith("Riemann subintervals/sec at N=1e9 fp64")
     assert js["ms_per_step"] == pytest.approx(max(js["per_rank_ms"]))
     assert js["value"] == pytest.approx(js["config"]["N"] * 3 / (js["ms_per_step"] * 3e-3))

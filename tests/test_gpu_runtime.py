@@ -632,6 +632,7 @@ def test_bench_contract(native, cuda):
     assert js["config"]["graphs"] is False
     # the settle, then the timed pattern once more on its own before the clock (untimed)
     assert js["warmup_rearm_batch"] and js["warmup_settle_steps"] >= 2 * 20
+    assert js["pre_clock_barrier"] == "host"  # one GPU: no device barrier to move behind
     # the record carries what the headline rests on: IEEE-division speed and per-point ulp
     assert js["ieee_div_value"] > 1e11 and js["ieee_div"]["abs_err"] < 2e-9
     # the headline division (series_exact): per point within 3 ulp of the IEEE path's own

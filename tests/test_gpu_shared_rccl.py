@@ -147,6 +147,8 @@ def test_bench_two_ranks_native_rccl_one_gpu(cuda):
     assert r["transport_verified"] and r["transport_error"] is None
     assert r["comm_fallback"] is None and r["config"]["batch_launch"] == "direct"
     assert r["direct_steps_timed"] == 10 and r["config"]["multistep"]
+    # the host barrier moved before the re-arm batch; the RCCL barrier stands before the clock
+    assert r["warmup_rearm_batch"] and r["pre_clock_barrier"] == "device"
     assert r["config"]["bucketed_allreduce"] and r["config"]["N"] == 10**9
     assert r["config"]["n_per_gpu"] == 5 * 10**8 and r["scaling"] == "strong"
     assert r["native_comm_verified"] and r["config"]["allreduce_to_host"]

@@ -42,6 +42,9 @@ def main(argv=None) -> int:
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--batches", type=int, default=50, help="K of back_to_back")
     ap.add_argument("--settle-ms", type=float, default=60.0)
+    ap.add_argument("--idle-us", default="",
+                    help="instead: the re-arm batch, then this many us of idle GPU (a list), "
+                         "then the batch")
     a = ap.parse_args(argv)
 
     import torch
@@ -111,6 +114,18 @@ def main(argv=None) -> int:
             time.sleep(1e-3)
             return one(None)
 
+        def rearm_idle(us):  # bench.py's re-arm batch, then the GPU idle for `us` (a host
+            def fn():        # barrier's worth), then the batch
+                for _ in range(settle):
+                    p.launch_steps(S, False, False)
+                p.sync()
+                one(None)
+                t_end = time.perf_counter() + us * 1e-6
+                while time.perf_counter() < t_end:
+                    pass
+                return one(None)
+            return fn
+
         def second():  # the settle, then the second launch+sync batch
             for _ in range(settle):
                 p.launch_steps(S, False, False)
@@ -160,6 +175,9 @@ def main(argv=None) -> int:
                  ("after_settle_3rd", after_settle_3rd), ("short_settle", short_settle),
                  ("idle_1ms", idle_1ms), ("second", second), ("devsync", devsync),
                  ("warm1", warm1), ("bench_like", bench_like)]
+        if a.idle_us:
+            modes = [("second", second)] + [(f"rearm_idle_{u}us", rearm_idle(u))
+                                            for u in (int(x) for x in a.idle_us.split(","))]
         res.update({m: [] for m, _ in modes if m not in res})
         for r in range(a.reps):
             order = modes[r % len(modes):] + modes[:r % len(modes)]
@@ -169,11 +187,12 @@ def main(argv=None) -> int:
                         fn()
                 res[name].append(fn() * 1e6)
         row = {"slice": g, "steps": S, "reps": a.reps, "grid": p.grid,
-               **{f"{k}_us_median": statistics.median(v) for k, v in res.items()},
-               **{f"{k}_us_min": min(v) for k, v in res.items()},
+               **{f"{k}_us_median": statistics.median(v) for k, v in res.items() if v},
+               **{f"{k}_us_min": min(v) for k, v in res.items() if v},
                **{f"{k}_launch_call_us_median": statistics.median(v)
-                  for k, v in launch_call.items()},
-               **{f"bench_like_{k}_us_median": statistics.median(v) for k, v in parts.items()},
+                  for k, v in launch_call.items() if v},
+               **{f"bench_like_{k}_us_median": statistics.median(v)
+                  for k, v in parts.items() if v},
                "value": p.host_result(p.host_index_of(S - 1, False))}
         print(json.dumps(row), flush=True)
     return 0

@@ -180,6 +180,40 @@ __device__ __forceinline__ T block_sum_dyn(T v, T* lds) {
   return r;  // meaningful in wave 0
 }
 
+// block_sum_dyn of C independent values at once (`lds` holds C * 16 elements): per value
+// exactly block_sum_dyn's additions, so each out[c] is bitwise block_sum_dyn(v[c]). The C
+// DPP chains interleave (each hides the others' DPP wait states and latency) and the block
+// pays one barrier for all C — the multi-step kernel's per-step sum at one wave per SIMD,
+// where a single chain and a barrier every step have no other wave to issue from.
+template <int C, typename T>
+__device__ __forceinline__ void block_sums_dyn(T (&v)[C], T* lds, T (&out)[C]) {
+  constexpr int kSlots = 16;  // wave totals per value (<= 1024 threads)
+  const int nw = static_cast<int>(blockDim.x) / kWave;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+#pragma unroll
+  for (int c = 0; c < C; ++c) v[c] = wave_sum_to_last(v[c]);
+  if (nw == 1) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) out[c] = wave_broadcast_last(v[c]);
+    return;
+  }
+  if (lane == kWave - 1) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) lds[c * kSlots + wid] = v[c];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < C; ++c) out[c] = T(0);
+  if (wid == 0) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const T r = lane < nw ? lds[c * kSlots + lane] : T(0);
+      out[c] = wave_broadcast_first(lanes_sum_small(r, nw));
+    }
+  }
+}
+
 // Block-wide inclusive scan; also returns the block total through *total.
 template <int BLOCK, typename T>
 __device__ __forceinline__ T block_inclusive_scan(T v, T* lds, T* total) {

@@ -683,29 +683,72 @@ __global__ __launch_bounds__(kMaxBlock) kFullOccupancy void riemann_chained_kern
 // Each step re-derives its sample coordinates from p.a laundered through an empty asm, so
 // nothing of a step is loop-invariant: no step's work can be hoisted out of the loop or shared
 // with another, K steps are K full integrations.
+// Steps per block sum (A/B knob): C steps' lane sums are kept in registers and summed over
+// the block together (block_sums_dyn: C interleaved DPP chains, one barrier), each step's
+// value bitwise the one-at-a-time sum's.
+#ifndef MIINT_MS_CHUNK
+#define MIINT_MS_CHUNK 1
+#endif
+constexpr int kMsChunk = MIINT_MS_CHUNK;
+
 template <DivMode M, class F, bool CLOSE>
 __device__ __forceinline__ void multistep_body(const RiemannParams& p, const double* table,
                                                int table_n, double* partials, int steps,
                                                unsigned rot, unsigned* ticket, double scale,
                                                double* out) {
   using Acc = typename AccOf<F>::type;
-  // The block sum's LDS slots alternate between steps: step s + 2 writes red[s & 1] only
-  // after every wave passed step s + 1's block-sum barrier, which wave 0 reaches after its
-  // step-s reads — so no second barrier per step, and waves 1-3 start the next step while
-  // wave 0 finishes the cross-wave sum.
-  __shared__ double red[2][kMaxBlock / kWave];
-  __shared__ Acc red_acc[2][__is_same(Acc, double) ? 1 : kMaxBlock / kWave];
+  constexpr int C = kMsChunk;
+  // The block sum's LDS slots alternate between block sums: sum k + 2 writes red[k & 1] only
+  // after every wave passed sum k + 1's barrier, which wave 0 reaches after its sum-k reads
+  // — so no second barrier per sum, and waves 1-3 start the next step while wave 0 finishes
+  // the cross-wave sum.
+  __shared__ double red[2][C * (kMaxBlock / kWave)];
+  __shared__ Acc red_acc[2][__is_same(Acc, double) ? 1 : C * (kMaxBlock / kWave)];
   __shared__ double lds[lds_words<M, F>()];
   const F f = make_functor<M, F>(p, table, table_n, lds);
   const unsigned nb = gridDim.x;
   const TileSplit sp = tile_split<F::template tile_len<M>()>(p.n);  // the same every step
   unsigned vb = blockIdx.x;
-  for (int s = 0; s < steps; ++s) {
+  unsigned seq = 0;  // block sums so far (LDS buffer seq & 1)
+  int s = 0;
+  if constexpr (C > 1) {
+    for (; s + C <= steps; s += C, ++seq) {
+      const unsigned vb0 = vb;
+      Acc l[C];
+#pragma unroll
+      for (int k = 0; k < C; ++k) l[k] = Acc(0);
+#pragma unroll 1
+      for (int c = 0; c < C; ++c) {
+        RiemannParams q = p;
+        asm volatile("" : "+s"(q.a));  // a fresh value every step (no instructions)
+        const Acc x = lane_sum<M>(q, f, vb, sp);
+#pragma unroll
+        for (int k = 0; k < C; ++k) l[k] = k == c ? x : l[k];  // uniform select, no scratch
+        vb += rot;
+        if (vb >= nb) vb -= nb;
+      }
+      Acc v[C];
+      if constexpr (__is_same(Acc, double)) block_sums_dyn<C>(l, red[seq & 1], v);
+      else block_sums_dyn<C>(l, red_acc[seq & 1], v);
+      if (threadIdx.x == 0) {
+        unsigned w = vb0;
+#pragma unroll
+        for (int k = 0; k < C; ++k) {
+          const double vk = static_cast<double>(v[k]);
+          if constexpr (CLOSE) slot_store(&partials[static_cast<size_t>(s + k) * nb + w], vk);
+          else partials[static_cast<size_t>(s + k) * nb + w] = vk;
+          w += rot;
+          if (w >= nb) w -= nb;
+        }
+      }
+    }
+  }
+  for (; s < steps; ++s, ++seq) {
     RiemannParams q = p;
     asm volatile("" : "+s"(q.a));  // a fresh value every step (no instructions)
     double v;
-    if constexpr (__is_same(Acc, double)) v = block_sum_dyn(lane_sum<M>(q, f, vb, sp), red[s & 1]);
-    else v = static_cast<double>(block_sum_dyn(lane_sum<M>(q, f, vb, sp), red_acc[s & 1]));
+    if constexpr (__is_same(Acc, double)) v = block_sum_dyn(lane_sum<M>(q, f, vb, sp), red[seq & 1]);
+    else v = static_cast<double>(block_sum_dyn(lane_sum<M>(q, f, vb, sp), red_acc[seq & 1]));
     if (threadIdx.x == 0) {
       // in-launch close: write-through, read by other workgroups' closers in this launch
       if constexpr (CLOSE) slot_store(&partials[static_cast<size_t>(s) * nb + vb], v);

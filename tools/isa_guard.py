@@ -33,6 +33,9 @@ import tempfile
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BASELINE = os.path.join(REPO, "tools", "isa_baseline.json")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+# extra -D switches of an A/B variant (e.g. ISA_DEFS="-DMIINT_MS_CHUNK=4"), compared against
+# the default build's baseline
+DEFS = os.environ.get("ISA_DEFS", "").split()
 VALU_SLACK = 1.03
 
 # name -> (kernel file, symbol regex, samples per hot-loop iteration or 0 = not one tile)
@@ -81,7 +84,7 @@ GUARDED = {
 def compile_asm(stem: str, outdir: str) -> str:
     out = os.path.join(outdir, stem + ".s")
     subprocess.run([HIPCC, "-std=c++17", "-O3", "-fPIC", "-I" + os.path.join(REPO, "csrc", "include"),
-                    "--offload-arch=gfx950", "--cuda-device-only", "-S",
+                    "--offload-arch=gfx950", "--cuda-device-only", "-S", *DEFS,
                     os.path.join(REPO, "csrc", "kernels", stem + ".hip"), "-o", out],
                    check=True, capture_output=True, text=True)
     with open(out) as f:

@@ -683,13 +683,21 @@ __global__ __launch_bounds__(kMaxBlock) kFullOccupancy void riemann_chained_kern
 // Each step re-derives its sample coordinates from p.a laundered through an empty asm, so
 // nothing of a step is loop-invariant: no step's work can be hoisted out of the loop or shared
 // with another, K steps are K full integrations.
-// Steps per block sum (A/B knob): C steps' lane sums are kept in registers and summed over
-// the block together (block_sums_dyn: C interleaved DPP chains, one barrier), each step's
-// value bitwise the one-at-a-time sum's.
+// Steps per block sum (A/B knob, MIINT_MS_CHUNK; fp64 Pi4 kernels only): C steps' lane sums
+// are kept in registers and summed over the block together (block_sums_dyn: C interleaved
+// DPP chains, one barrier per C steps), each step's value bitwise the one-at-a-time sum's.
+// At the 1/8 share (one wave per SIMD) C = 4 cut a wave's waits from 4.6 % to 3.5 % of its
+// cycles, but interleaved A/Bs put its time within the spread of C = 1 at every share and at
+// G = 1 (profiles/r6/roofline_share.md, batch_tail.md), and it takes the headline kernel
+// from 62 to 69 VGPRs: the default stays 1 (the other integrands always; the polynomial's
+// kernel would lose a wave per SIMD at 79 VGPRs).
 #ifndef MIINT_MS_CHUNK
 #define MIINT_MS_CHUNK 1
 #endif
-constexpr int kMsChunk = MIINT_MS_CHUNK;
+template <class F>
+constexpr int ms_chunk() {
+  return __is_same(F, Pi4) ? MIINT_MS_CHUNK : 1;
+}
 
 template <DivMode M, class F, bool CLOSE>
 __device__ __forceinline__ void multistep_body(const RiemannParams& p, const double* table,
@@ -697,7 +705,7 @@ __device__ __forceinline__ void multistep_body(const RiemannParams& p, const dou
                                                unsigned rot, unsigned* ticket, double scale,
                                                double* out) {
   using Acc = typename AccOf<F>::type;
-  constexpr int C = kMsChunk;
+  constexpr int C = ms_chunk<F>();
   // The block sum's LDS slots alternate between block sums: sum k + 2 writes red[k & 1] only
   // after every wave passed sum k + 1's barrier, which wave 0 reaches after its sum-k reads
   // — so no second barrier per sum, and waves 1-3 start the next step while wave 0 finishes

@@ -13,6 +13,8 @@ G1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VALU_FMA_F64 SQ_I
 G2="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU_MUL_F64 SQ_THREAD_CYCLES_VALU"
 G3="FETCH_SIZE GRBM_GUI_ACTIVE SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR"
 G4="WRITE_SIZE GRBM_GUI_ACTIVE SQ_LDS_UNALIGNED_STALL SQ_INSTS_FLAT"
+# where a wave's cycles go (waiting on anything / on instruction fetch), for the share vs G = 1
+G5="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_IFETCH SQ_INSTS_VALU GRBM_GUI_ACTIVE"
 
 # ONLY="name1 name2": run just those workloads (default: all)
 want() { [ -z "${ONLY:-}" ] || [[ " $ONLY " == *" $1 "* ]]; }
@@ -53,5 +55,9 @@ done
 for g in G1 G2 G3 G4; do
   run trainscan $g "${!g}" "$REPO/build/bin/trainscan"
   run materialize $g "${!g}" "$REPO/build/bin/cintegrate" --materialize
+done
+for g in G5; do
+  run g1_w $g "${!g}" "$REPO/build/bin/miint" bench --n 1e9 --slots 20 --iters 400 --settle 400
+  run share8_w $g "${!g}" "$REPO/build/bin/miint" bench --n 1.25e8 --slots 20 --iters 2000 --settle 2000
 done
 echo "pmc done"
